@@ -1,0 +1,124 @@
+/*
+ * mff.h — C ABI of libmff.so, the MI355X (gfx950) minute-factor engine.
+ *
+ * The reference (C-X-Lu/Replication-of-Minute-Frequency-Factor) has no FFI: its
+ * operator API is a Python callable, `calculate_method(df) -> df`, handed to
+ * `MinFreqFactor.cal_exposure_by_min_data` (MinuteFrequentFactorCICC.py:50-55) and
+ * invoked per day file at MinuteFrequentFactorCICC.py:22.  Each entry point below
+ * replaces one piece of that path; the reference interface it replaces is cited on
+ * every declaration.  INTEGRATION.md shows the ctypes binding a maintainer adds.
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers owned by the caller (the library never
+ *    allocates or frees caller memory).  Host pointers are marked `host`.
+ *  - `stream` is a hipStream_t passed as void* (NULL = default stream).  Every call
+ *    is asynchronous on that stream; none synchronises, allocates, or copies, so a
+ *    caller may capture them into a hipGraph.
+ *  - Return 0 on success, negative on error; mff_last_error() gives a thread-local
+ *    message.  No C++ exception crosses this ABI.
+ *  - Panel layout: field planes open/high/low/close/volume, each float32 [D][S][240]
+ *    (day, stock, minute 0..239 = 09:30..11:29, 13:00..14:59); presence mask
+ *    uint32 [D][S][8], bit (m % 32) of word (m / 32) set when bar m exists.
+ *    Volume must be integral, 0 <= v <= 2^24 (fp32-exact), prices finite > 0.
+ *  - Output layout: val float64 [rows][D][S], state uint8 [rows][D][S] with
+ *    0 = ABSENT (the reference emits no row), 1 = NULL (polars null),
+ *    2 = VALUE (may be NaN / +-inf).
+ */
+#ifndef MFF_H
+#define MFF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MFF_NUM_FACTORS 58
+#define MFF_STATE_ABSENT 0
+#define MFF_STATE_NULL 1
+#define MFF_STATE_VALUE 2
+
+/* stage 2 methods, MinuteFrequentFactorCICC.py:190-238 */
+#define MFF_ROLL_O 0   /* identity            MF:190-198 */
+#define MFF_ROLL_M 1   /* rolling_mean        MF:199-209 */
+#define MFF_ROLL_Z 2   /* (x-mean)/std(ddof0) MF:210-227 */
+#define MFF_ROLL_STD 3 /* rolling_std(ddof0)  MF:228-238 */
+
+/* stage 3 kinds */
+#define MFF_XS_Z 0
+#define MFF_XS_RANK 1
+
+int mff_version(void);
+const char* mff_last_error(void);
+int mff_num_factors(void);
+/* name of factor `id` (reference column name, e.g. "mmt_pm"); NULL if out of range */
+const char* mff_factor_name(int id);
+
+/*
+ * Stage 1: the per-(stock, day) factor kernels.
+ * Replaces: every `cal_<name>(df)` of MinuteFrequentFactorCalculateMethodsCICC.py
+ * (CM:12-1406) applied per day file by `_process_single_file`
+ * (MinuteFrequentFactorCICC.py:17-25), for D days x S stocks at once.
+ * factor_ids (host, nf entries): catalogue ids in output-row order.
+ * pdf_query: float64 [5][D][S] workspace, required when any doc_pdf* id is requested
+ * (the doc_pdf values are then produced by mff_pdf_* below), else may be NULL.
+ */
+int mff_stage1(const float* open, const float* high, const float* low,
+               const float* close, const float* volume, const uint32_t* valid,
+               int S, int D, const int32_t* factor_ids /* host */, int nf,
+               double* val, uint8_t* state, double* pdf_query, void* stream);
+
+/*
+ * doc_pdf60..95 frame-wide rank (CM:1015-1017: `.rank()` over ALL rows of the day
+ * frame, every code).  Three device phases; between count and finalize a multi-GPU
+ * caller sums `counts` over ranks (all-reduce), see INTEGRATION.md.
+ * Each phase works on days [d0, d0+nd) of arrays laid out over all D days.
+ *   sort:     queries of R ranks, float64 [R][5][D][S_loc] (NaN = none)
+ *             -> q_sorted uint64 [nd][M], M = R*5*S_loc <= 32767 (total-order keys)
+ *   count:    this rank's keys c_last/c_b against q_sorted
+ *             -> counts uint32 [nd][M][2] (n_less, n_eq) over local keys
+ *   finalize: own queries [5][D][S_loc] -> val/state rows pdf_rows[5] (host)
+ * workspace: mff_pdf_workspace_bytes(S_loc, R, nd) bytes of device scratch.
+ */
+size_t mff_pdf_workspace_bytes(int S_loc, int R, int nd);
+int mff_pdf_sort(const double* q_all, int R, int S_loc, int D, int d0, int nd,
+                 uint64_t* q_sorted, void* workspace, void* stream);
+int mff_pdf_count(const float* close, const uint32_t* valid, int S_loc, int D, int d0,
+                  int nd, const uint64_t* q_sorted, int M, uint32_t* counts,
+                  void* workspace, void* stream);
+int mff_pdf_finalize(const double* q_local, const uint64_t* q_sorted,
+                     const uint32_t* counts, int S_loc, int D, int d0, int nd, int M,
+                     const int32_t* pdf_rows /* host, 5 entries, -1 = skip */,
+                     double* val, uint8_t* state, void* stream);
+
+/*
+ * Stage 2: N-day rolling post-processing over present days, per stock.
+ * Replaces: MinFreqFactor.cal_final_exposure(frequency=N, method, mode='days')
+ * (MinuteFrequentFactorCICC.py:187-240).  rows = number of factor rows.
+ * Requires 1 <= N <= 64.
+ */
+int mff_stage2(const double* val, const uint8_t* state, int rows, int D, int S,
+               int N, int method, double* out_val, uint8_t* out_state, void* stream);
+
+/*
+ * Stage 3: per-day cross-sectional z-score (ddof=1) or average rank over stocks with
+ * state VALUE and non-NaN value.  No single reference function; closest semantics
+ * Factor.py:99-105 (coverage), :163-186 (per-date Pearson / Spearman), :285-291 (qcut).
+ * z-score, multi-GPU: mff_xs_moments per rank -> all-gather [R][rows][D][3] ->
+ * mff_xs_zscore.  rank: all-gather values/states [R][rows][D][S_loc] -> mff_xs_rank.
+ */
+int mff_xs_moments(const double* val, const uint8_t* state, int rows, int D, int S,
+                   double* moments /* [rows][D][3]: n, mean, M2 */, void* stream);
+int mff_xs_zscore(const double* val, const uint8_t* state, int rows, int D, int S,
+                  const double* moments_all, int R, double* out_val,
+                  uint8_t* out_state, void* stream);
+size_t mff_xs_rank_workspace_bytes(int rows, int D, int S_loc, int R);
+int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_loc,
+                const double* val_all, const uint8_t* state_all, int R,
+                double* out_val, uint8_t* out_state, void* workspace, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MFF_H */

@@ -1,0 +1,1017 @@
+"""CPU oracle for the CICC minute-factor hot path.  TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as the checker / the timed CPU baseline.  The product
+(``replication-of-minute-frequency-factor_amd/``) never imports it.
+
+What it is
+----------
+A plain numpy restatement of the reference arithmetic, written from the reference
+files read as text:
+
+* stage 1 — the 58 ``cal_*`` functions of
+  ``MinuteFrequentFactorCalculateMethodsCICC.py`` (cited ``CM:<line>``),
+* stage 2 — the N-day rolling post-processing of ``MinuteFrequentFactorCICC.py``
+  ``cal_final_exposure(mode='days')`` (``MF:187-240``),
+* stage 3 — the per-date cross-sectional z-score / average rank defined in
+  SURVEY.md §8(a) row S3 (closest reference semantics ``FA:99-105,163-186,285-291``).
+
+Each ``cal_*`` here takes a *day frame* (the reference input: one trading day, all
+codes, long format, rows ordered by (code, time) — SURVEY C4) and returns
+``{code: value}`` for the rows the reference would emit; ``None`` is a polars null,
+codes missing from the dict are absent rows.  The step order of every function
+follows its reference counterpart line by line so the two can be read side by side.
+
+Parity status
+-------------
+The reference computes with polars (Rust), which is not importable in this
+container (ordinary ``ModuleNotFoundError``).  This restatement is
+therefore pinned by
+
+* the polars moment values reproduced in narwhals docstrings
+  (``narwhals/expr.py:550-585``: skew [1,2,3,4,5]=0, [1,1,2,10,100]=1.472427;
+  kurtosis -1.3 and 0.210657) — ``tests/test_oracle_kat.py``;
+* hand-derived known-answer vectors for every factor family, committed under
+  ``tests/golden/`` with the script that made them.
+
+Against polars itself the values are **parity unpinned**; every polars-semantics
+assumption is written down as rule S1-S13 / canonical choice C1-C6 (SURVEY.md §8(c)
+plus C6 below) and implemented in one helper each.
+
+C6 (stage 2, this build): a rolling window whose N values are identical has std
+exactly 0 and mean exactly the value, so ``z`` is 0/0 = NaN there.
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+
+NULL = None
+
+# ----------------------------------------------------------------------------
+# polars semantics helpers
+# ----------------------------------------------------------------------------
+
+
+def _isnan(x) -> bool:
+    return x is not None and isinstance(x, float) and math.isnan(x)
+
+
+def tot_gt(a, b) -> Optional[bool]:
+    """S11: total-order ``a > b`` (NaN greater than every number, NaN == NaN)."""
+    if a is None or b is None:
+        return None
+    an, bn = math.isnan(a), math.isnan(b)
+    if an or bn:
+        return an and not bn
+    return a > b
+
+
+def tot_lt(a, b) -> Optional[bool]:
+    return tot_gt(b, a)
+
+
+def tot_ne(a, b) -> Optional[bool]:
+    if a is None or b is None:
+        return None
+    an, bn = math.isnan(a), math.isnan(b)
+    if an or bn:
+        return not (an and bn)
+    return a != b
+
+
+def _div(a, b):
+    """IEEE f64 division with null propagation (S10)."""
+    if a is None or b is None:
+        return None
+    with np.errstate(all="ignore"):
+        return float(np.float64(a) / np.float64(b))
+
+
+def _nn(x: Sequence) -> np.ndarray:
+    """Non-null values of a python list as f64 array."""
+    return np.array([v for v in x if v is not None], dtype=np.float64)
+
+
+def _constant(x: np.ndarray) -> bool:
+    # C3: a set of finite values has variance exactly zero iff they are identical.
+    return x.size > 0 and bool(np.isfinite(x[0])) and bool(np.all(x == x[0]))
+
+
+def _mean_exact(x: np.ndarray) -> float:
+    """Mean with the C3 guarantee: identical values give exactly that value."""
+    if _constant(x):
+        return float(x[0])
+    with np.errstate(all="ignore"):
+        return float(np.mean(x))
+
+
+def pl_mean(x) -> Optional[float]:
+    """S9/S10: mean of non-null values; null when there are none; NaN propagates."""
+    a = _nn(x) if not isinstance(x, np.ndarray) else x
+    if a.size == 0:
+        return None
+    with np.errstate(all="ignore"):
+        return float(np.mean(a))
+
+
+def pl_var(x, ddof: int = 1) -> Optional[float]:
+    """S1: sample variance; null if n <= ddof; exactly 0 for identical values (C3)."""
+    a = _nn(x) if not isinstance(x, np.ndarray) else x
+    n = a.size
+    if n <= ddof:
+        return None
+    if _constant(a):
+        return 0.0
+    with np.errstate(all="ignore"):
+        m = np.mean(a)
+        return float(np.sum((a - m) ** 2) / (n - ddof))
+
+
+def pl_std(x, ddof: int = 1) -> Optional[float]:
+    v = pl_var(x, ddof)
+    return None if v is None else math.sqrt(v) if not math.isnan(v) else float("nan")
+
+
+def pl_skew(x) -> Optional[float]:
+    """S2: biased skewness g1 = m3 / m2**1.5.  n=0 -> null, n=1 -> NaN, n=2 -> 0.0,
+    m2 = 0 -> NaN (narwhals/_pandas_like/series.py:533-545 mirrors polars)."""
+    a = _nn(x) if not isinstance(x, np.ndarray) else x
+    n = a.size
+    if n == 0:
+        return None
+    if n == 1:
+        return float("nan")
+    if np.any(np.isnan(a)):
+        return float("nan")
+    if _constant(a):
+        return float("nan")
+    if n == 2:
+        return 0.0
+    with np.errstate(all="ignore"):
+        d = a - np.mean(a)
+        m2 = np.mean(d * d)
+        m3 = np.mean(d * d * d)
+        return float(m3 / m2 ** 1.5) if m2 != 0 else float("nan")
+
+
+def pl_kurt(x) -> Optional[float]:
+    """S2: Fisher kurtosis without bias correction, m4 / m2**2 - 3."""
+    a = _nn(x) if not isinstance(x, np.ndarray) else x
+    n = a.size
+    if n == 0:
+        return None
+    if n == 1:
+        return float("nan")
+    if np.any(np.isnan(a)):
+        return float("nan")
+    if _constant(a):
+        return float("nan")
+    with np.errstate(all="ignore"):
+        d = a - np.mean(a)
+        m2 = np.mean(d * d)
+        m4 = np.mean(d ** 4)
+        return float(m4 / m2 ** 2 - 3.0) if m2 != 0 else float("nan")
+
+
+def pl_corr(x: Sequence, y: Sequence) -> float:
+    """S3: Pearson over pairs where both sides are non-null.  Fewer than two pairs or a
+    zero denominator give NaN (never null)."""
+    pairs = [(a, b) for a, b in zip(x, y) if a is not None and b is not None]
+    if len(pairs) < 2:
+        return float("nan")
+    xa = np.array([p[0] for p in pairs], dtype=np.float64)
+    ya = np.array([p[1] for p in pairs], dtype=np.float64)
+    if np.any(np.isnan(xa)) or np.any(np.isnan(ya)):
+        return float("nan")
+    if _constant(xa) or _constant(ya):
+        return float("nan")
+    with np.errstate(all="ignore"):
+        dx = xa - np.mean(xa)
+        dy = ya - np.mean(ya)
+        den = math.sqrt(float(np.sum(dx * dx)) * float(np.sum(dy * dy)))
+        if den == 0.0:
+            return float("nan")
+        return float(np.sum(dx * dy) / den)
+
+
+def pl_pct_change(x: Sequence) -> List[Optional[float]]:
+    """S4: (x_i - x_{i-1}) / x_{i-1}; first element null."""
+    out: List[Optional[float]] = [None]
+    for i in range(1, len(x)):
+        out.append(_div(float(x[i]) - float(x[i - 1]), float(x[i - 1])))
+    return out
+
+
+def pl_shift(x: Sequence, n: int) -> List[Optional[float]]:
+    """S5: shift within the group, null at the edge."""
+    L = len(x)
+    if n >= 0:
+        return [None] * min(n, L) + [float(v) for v in x[: max(L - n, 0)]]
+    n = -n
+    return [float(v) for v in x[n:]] + [None] * min(n, L)
+
+
+def pl_sum(x) -> float:
+    """S9: sum of non-null values, empty sum 0."""
+    a = _nn(x) if not isinstance(x, np.ndarray) else x
+    with np.errstate(all="ignore"):
+        return float(np.sum(a)) if a.size else 0.0
+
+
+def pl_product(x) -> float:
+    p = 1.0
+    for v in x:
+        p *= float(v)
+    return p
+
+
+def avg_rank(values: np.ndarray) -> np.ndarray:
+    """S6: ``rank()`` default — method 'average', ascending, 1-based, f64."""
+    n = values.size
+    order = np.argsort(values, kind="stable")
+    sv = values[order]
+    ranks = np.empty(n, dtype=np.float64)
+    i = 0
+    while i < n:
+        j = i
+        while j + 1 < n and sv[j + 1] == sv[i]:
+            j += 1
+        ranks[order[i : j + 1]] = (i + 1 + j + 1) / 2.0
+        i = j + 1
+    return ranks
+
+
+# ----------------------------------------------------------------------------
+# Day frame: the reference input (``pl.read_parquet(day file)``, MF:22)
+# ----------------------------------------------------------------------------
+
+
+class DayFrame:
+    """One trading day, long format, rows ordered by (code, time) (C4)."""
+
+    def __init__(self, code, date, time, open_, high, low, close, volume):
+        self.code = np.asarray(code)
+        self.date = date
+        self.time = np.asarray(time, dtype=np.int64)
+        self.open = np.asarray(open_, dtype=np.float64)
+        self.high = np.asarray(high, dtype=np.float64)
+        self.low = np.asarray(low, dtype=np.float64)
+        self.close = np.asarray(close, dtype=np.float64)
+        self.volume = np.asarray(volume, dtype=np.float64)
+        n = self.code.size
+        if n:
+            cut = np.flatnonzero(self.code[1:] != self.code[:-1]) + 1
+            starts = np.concatenate([[0], cut])
+            ends = np.concatenate([cut, [n]])
+        else:
+            starts = ends = np.zeros(0, dtype=np.int64)
+        self.groups = [(self.code[s], s, e) for s, e in zip(starts, ends)]
+
+    def g(self, name, s, e):
+        return getattr(self, name)[s:e]
+
+
+def minute_to_time(m: np.ndarray) -> np.ndarray:
+    """Minute index 0..239 -> HHMMSSmmm start label (SURVEY §8(a) time grid)."""
+    m = np.asarray(m, dtype=np.int64)
+    clock = np.where(m < 120, 9 * 60 + 30 + m, 13 * 60 + (m - 120))
+    return (clock // 60) * 10000000 + (clock % 60) * 100000
+
+
+# ----------------------------------------------------------------------------
+# Momentum: session segments (CM:10-90)
+# ----------------------------------------------------------------------------
+
+
+def _seg_pair(df: DayFrame, times) -> Dict:
+    # filter(time in [a, b]) -> sort(code, date, time) -> close.last() / open.first()
+    out = {}
+    for code, s, e in df.groups:
+        t = df.time[s:e]
+        sel = np.isin(t, times)
+        if not sel.any():
+            continue
+        idx = np.flatnonzero(sel)
+        idx = idx[np.argsort(t[idx], kind="stable")]
+        out[code] = _div(df.close[s + idx[-1]], df.open[s + idx[0]])
+    return out
+
+
+def cal_mmt_pm(df):  # CM:12-24
+    return _seg_pair(df, [130000000, 145900000])
+
+
+def cal_mmt_last30(df):  # CM:27-39
+    return _seg_pair(df, [143000000, 145900000])
+
+
+def cal_mmt_am(df):  # CM:63-75
+    return _seg_pair(df, [93000000, 112900000])
+
+
+def cal_mmt_between(df):  # CM:78-90
+    return _seg_pair(df, [100000000, 142900000])
+
+
+def cal_mmt_paratio(df):  # CM:42-60
+    out = {}
+    for code, s, e in df.groups:
+        t = df.time[s:e]
+        sess = np.where(t <= 113000000, 0, 1)  # CM:49-52
+        mmts = []
+        for k in (0, 1):  # C1: AM group first, PM group last
+            idx = np.flatnonzero(sess == k)
+            if idx.size == 0:
+                continue
+            # close.last() / open.first() - 1 in frame order (CM:54)
+            mmts.append(_div(df.close[s + idx[-1]], df.open[s + idx[0]]) - 1.0)
+        out[code] = mmts[-1] - mmts[0]  # mmt.last() - mmt.first() (CM:57)
+    return out
+
+
+# ----------------------------------------------------------------------------
+# Momentum: 50-minute OLS of high on low (CM:93-376)
+# ----------------------------------------------------------------------------
+
+
+def _minute_in_trade(time: np.ndarray) -> np.ndarray:
+    # CM:98-106: time // 1e7 * 60 + time % 1e7 / 1e5, cast Int64, then session offset
+    tm = (time // 10000000 * 60 + (time % 10000000) / 100000).astype(np.int64)
+    return np.where(tm < 720, tm - 570, tm - 660)
+
+
+def _ols_windows(df: DayFrame, s: int, e: int):
+    """rolling(index_column='minute_in_trade', period='50i', group_by=[code, date])
+    (CM:114-118) then filter(n >= 50) (CM:129).  S12: window (t-50, t]."""
+    mins = _minute_in_trade(df.time[s:e])
+    x = df.low[s:e]
+    y = df.high[s:e]
+    wins = []
+    for i in range(mins.size):
+        t = mins[i]
+        lo = np.searchsorted(mins, t - 50, side="right")
+        hi = i + 1
+        n = hi - lo
+        if n < 50:
+            continue
+        wx, wy = x[lo:hi], y[lo:hi]
+        cx, cy = _constant(wx), _constant(wy)
+        mx, my = _mean_exact(wx), _mean_exact(wy)
+        with np.errstate(all="ignore"):
+            var_x = 0.0 if cx else float(np.mean((wx - mx) ** 2))  # ddof=0 (CM:120)
+            var_y = 0.0 if cy else float(np.mean((wy - my) ** 2))  # ddof=0 (CM:121)
+            cov = 0.0 if (cx or cy) else float(np.mean((wx - mx) * (wy - my)))  # CM:119
+        wins.append((cov, var_x, var_y, mx, my))
+    return wins
+
+
+def _beta(w):
+    cov, vx, vy, mx, my = w
+    # CM:131-134
+    return _div(cov, vx) if vx != 0 else _div(my, mx)
+
+
+def _pow(a, p):
+    with np.errstate(all="ignore"):
+        return float(np.power(np.float64(a), p))
+
+
+def cal_mmt_ols_qrs(df):  # CM:93-173
+    out = {}
+    for code, s, e in df.groups:
+        wins = _ols_windows(df, s, e)
+        if not wins:
+            continue
+        betas, qs = [], []
+        for w in wins:
+            cov, vx, vy, mx, my = w
+            betas.append(_beta(w))
+            # CM:135-140: cov**0.5 / (var_x * var_y), null when the product is 0
+            qs.append(_div(_pow(cov, 0.5), vx * vy) if vy * vx != 0 else None)
+        b = np.array(betas)
+        beta_mean = pl_mean(b)
+        beta_std = pl_std(b)
+        beta_last = betas[-1]
+        csm = pl_mean(qs)
+        cond_a = tot_ne(beta_std, 0.0)
+        cond_b = csm is not None
+        # CM:159-171: when(...).then(csm * (last - mean) / std).otherwise(0)
+        if cond_a is True and cond_b:
+            out[code] = _div(csm * (beta_last - beta_mean), beta_std)
+        else:
+            out[code] = 0.0
+    return out
+
+
+def _ols_mean_of(df, fn):
+    out = {}
+    for code, s, e in df.groups:
+        wins = _ols_windows(df, s, e)
+        if not wins:
+            continue
+        vals = []
+        for cov, vx, vy, mx, my in wins:
+            vals.append(fn(cov, vx, vy) if vx * vy != 0 else None)
+        m = pl_mean(vals)
+        out[code] = 0.0 if m is None else m  # fill_null(0)
+    return out
+
+
+def cal_mmt_ols_corr_square_mean(df):  # CM:176-222
+    return _ols_mean_of(df, lambda c, vx, vy: _div(_pow(c, 2), vx * vy))
+
+
+def cal_mmt_ols_corr_mean(df):  # CM:225-271
+    return _ols_mean_of(df, lambda c, vx, vy: _div(c, _pow(vx * vy, 0.5)))
+
+
+def cal_mmt_ols_beta_mean(df):  # CM:274-324
+    out = {}
+    for code, s, e in df.groups:
+        wins = _ols_windows(df, s, e)
+        if wins:
+            out[code] = pl_mean(np.array([_beta(w) for w in wins]))
+    return out
+
+
+def cal_mmt_ols_beta_zscore_last(df):  # CM:327-376
+    out = {}
+    for code, s, e in df.groups:
+        wins = _ols_windows(df, s, e)
+        if not wins:
+            continue
+        b = np.array([_beta(w) for w in wins])
+        sd = pl_std(b)
+        mean = pl_mean(b)
+        if tot_gt(sd, 0.0) is True:  # when(std > 0), null -> otherwise (CM:369-373)
+            out[code] = _div(b[-1] - mean, sd)
+        else:
+            out[code] = mean
+    return out
+
+
+# ----------------------------------------------------------------------------
+# Momentum: volume-ranked (CM:379-480)
+# ----------------------------------------------------------------------------
+
+
+def _vol_rank_ret(df, k, top):
+    out = {}
+    for code, s, e in df.groups:
+        v = df.volume[s:e]
+        sv = np.sort(v)
+        if top:  # volume >= volume.top_k(k).min()  (CM:391-396)
+            theta = sv[-k] if v.size >= k else sv[0]
+            sel = v >= theta
+        else:  # volume <= volume.bottom_k(k).max()  (CM:417-422)
+            theta = sv[k - 1] if v.size >= k else sv[-1]
+            sel = v <= theta
+        ret = [_div(c, o) for c, o in zip(df.close[s:e][sel], df.open[s:e][sel])]
+        out[code] = pl_product(ret) - 1.0  # ret.product() - 1
+    return out
+
+
+def cal_mmt_top50VolumeRet(df):  # CM:379-402
+    return _vol_rank_ret(df, 50, True)
+
+
+def cal_mmt_bottom50VolumeRet(df):  # CM:405-428
+    return _vol_rank_ret(df, 50, False)
+
+
+def cal_mmt_top20VolumeRet(df):  # CM:431-454
+    return _vol_rank_ret(df, 20, True)
+
+
+def cal_mmt_bottom20VolumeRet(df):  # CM:457-480 — bottom_k(50) [sic, CM:471]
+    return _vol_rank_ret(df, 50, False)
+
+
+# ----------------------------------------------------------------------------
+# Volatility (CM:483-642) and higher moments (CM:645-729)
+# ----------------------------------------------------------------------------
+
+
+def _returns(df, s, e):
+    with np.errstate(all="ignore"):
+        return df.close[s:e] / df.open[s:e] - 1.0  # close / open - 1
+
+
+def _per_group(df, fn):
+    return {code: fn(s, e) for code, s, e in df.groups}
+
+
+def cal_vol_volume1min(df):  # CM:485-496
+    return _per_group(df, lambda s, e: pl_std(df.volume[s:e]))
+
+
+def cal_vol_range1min(df):  # CM:499-515
+    def f(s, e):
+        with np.errstate(all="ignore"):
+            return pl_std(df.high[s:e] / df.low[s:e])
+    return _per_group(df, f)
+
+
+def cal_vol_return1min(df):  # CM:518-534
+    return _per_group(df, lambda s, e: pl_std(_returns(df, s, e)))
+
+
+def _updown(r: np.ndarray, up: bool) -> np.ndarray:
+    # when(return > 0).then(return).otherwise(None)  (S11 total order)
+    if up:
+        keep = [bool(tot_gt(float(x), 0.0)) for x in r]
+    else:
+        keep = [bool(tot_lt(float(x), 0.0)) for x in r]
+    return r[np.array(keep, dtype=bool)] if r.size else r
+
+
+def _fill0(x):
+    return 0.0 if x is None else x
+
+
+def cal_vol_upVol(df):  # CM:537-560
+    return _per_group(df, lambda s, e: _fill0(pl_std(_updown(_returns(df, s, e), True))))
+
+
+def cal_vol_upRatio(df):  # CM:563-588
+    def f(s, e):
+        r = _returns(df, s, e)
+        return _div(_fill0(pl_std(_updown(r, True))), pl_std(r))
+    return _per_group(df, f)
+
+
+def cal_vol_downVol(df):  # CM:591-614
+    return _per_group(df, lambda s, e: _fill0(pl_std(_updown(_returns(df, s, e), False))))
+
+
+def cal_vol_downRatio(df):  # CM:617-642
+    def f(s, e):
+        r = _returns(df, s, e)
+        return _div(_fill0(pl_std(_updown(r, False))), pl_std(r))
+    return _per_group(df, f)
+
+
+def cal_shape_skew(df):  # CM:647-657
+    return _per_group(df, lambda s, e: pl_skew(_returns(df, s, e)))
+
+
+def cal_shape_kurt(df):  # CM:660-670
+    return _per_group(df, lambda s, e: pl_kurt(_returns(df, s, e)))
+
+
+def cal_shape_skratio(df):  # CM:673-687 (output columns ordered date, code)
+    def f(s, e):
+        r = _returns(df, s, e)
+        return _div(pl_skew(r), pl_kurt(r))
+    return _per_group(df, f)
+
+
+def _vshare(df, s, e):
+    v = df.volume[s:e]
+    with np.errstate(all="ignore"):
+        return v / np.sum(v)  # volume / volume.sum()
+
+
+def cal_shape_skewVol(df):  # CM:690-700
+    return _per_group(df, lambda s, e: pl_skew(_vshare(df, s, e)))
+
+
+def cal_shape_kurtVol(df):  # CM:703-713
+    return _per_group(df, lambda s, e: pl_kurt(_vshare(df, s, e)))
+
+
+def cal_shape_skratioVol(df):  # CM:716-729
+    def f(s, e):
+        vd = _vshare(df, s, e)
+        return _div(pl_skew(vd), pl_kurt(vd))
+    return _per_group(df, f)
+
+
+# ----------------------------------------------------------------------------
+# Liquidity (CM:732-831)
+# ----------------------------------------------------------------------------
+
+
+def cal_liq_amihud_1min(df):  # CM:734-761
+    def f(s, e):
+        pc = pl_pct_change(df.close[s:e])  # pct_change().over('code')
+        tot = []
+        for p, v in zip(pc, df.volume[s:e]):
+            pa = 0.0 if p is None else abs(p)  # .abs().fill_null(0)
+            tot.append(_div(pa, v) if v > 0 else 0.0)
+        return pl_sum(tot)
+    return _per_group(df, f)
+
+
+def _filtered_sum(df, pred):
+    out = {}
+    for code, s, e in df.groups:
+        sel = pred(df.time[s:e])
+        if sel.any():
+            out[code] = pl_sum(df.volume[s:e][sel])
+    return out
+
+
+def cal_liq_closeprevol(df):  # CM:764-775
+    return _filtered_sum(df, lambda t: t < 145700000)
+
+
+def cal_liq_closevol(df):  # CM:778-789
+    return _filtered_sum(df, lambda t: t >= 145700000)
+
+
+def cal_liq_firstCallR(df):  # CM:792-802
+    return _per_group(df, lambda s, e: _div(df.volume[s], pl_sum(df.volume[s:e])))
+
+
+def cal_liq_lastCallR(df):  # CM:805-820
+    def f(s, e):
+        v = df.volume[s:e]
+        return _div(pl_sum(v[df.time[s:e] >= 145700000]), pl_sum(v))
+    return _per_group(df, f)
+
+
+def cal_liq_openvol(df):  # CM:823-831
+    return _per_group(df, lambda s, e: float(df.volume[s]))
+
+
+# ----------------------------------------------------------------------------
+# Volume-price correlation (CM:834-932)
+# ----------------------------------------------------------------------------
+
+
+def cal_corr_prv(df):  # CM:836-847
+    return _per_group(df, lambda s, e: pl_corr(pl_pct_change(df.close[s:e]),
+                                               list(df.volume[s:e])))
+
+
+def _nonzero_groups(df):
+    """filter(volume != 0) then re-group (CM:855-857, CM:924-926)."""
+    for code, s, e in df.groups:
+        sel = df.volume[s:e] != 0
+        if sel.any():
+            yield code, df.close[s:e][sel], df.volume[s:e][sel]
+
+
+def cal_corr_prvr(df):  # CM:850-874
+    return {code: pl_corr(pl_pct_change(c), pl_pct_change(v))
+            for code, c, v in _nonzero_groups(df)}
+
+
+def cal_corr_pv(df):  # CM:877-888
+    return _per_group(df, lambda s, e: pl_corr(list(df.close[s:e]), list(df.volume[s:e])))
+
+
+def cal_corr_pvd(df):  # CM:891-902
+    return _per_group(df, lambda s, e: pl_corr(list(df.close[s:e]),
+                                               pl_shift(df.volume[s:e], 1)))
+
+
+def cal_corr_pvl(df):  # CM:905-916
+    return _per_group(df, lambda s, e: pl_corr(list(df.close[s:e]),
+                                               pl_shift(df.volume[s:e], -1)))
+
+
+def cal_corr_pvr(df):  # CM:919-932
+    return {code: pl_corr(list(c), pl_pct_change(v)) for code, c, v in _nonzero_groups(df)}
+
+
+# ----------------------------------------------------------------------------
+# Chip distribution (CM:935-1201)
+# ----------------------------------------------------------------------------
+
+
+def _doc_levels(df, s, e):
+    """with_columns(volume_d = v / v.sum().over(code, date),
+                    return = close.last().over(code, date) / close)
+       .group_by([code, date, return]).agg(volume_d.sum())   (CM:943-950)
+    Level sums accumulate in frame (bar) order.  C7: when the integral level volumes
+    are all equal the shares are taken as identical (exact arithmetic), so the
+    moments below are NaN rather than a function of float summation order."""
+    v = df.volume[s:e]
+    c = df.close[s:e]
+    with np.errstate(all="ignore"):
+        vd = v / np.sum(v)
+        key = c[-1] / c
+    levels: Dict[float, float] = {}
+    vol: Dict[float, float] = {}
+    for k, x, vv in zip(key.tolist(), vd.tolist(), v.tolist()):
+        levels[k] = levels.get(k, 0.0) + x
+        vol[k] = vol.get(k, 0.0) + vv
+    shares = np.array(list(levels.values()))
+    V = np.array(list(vol.values()))
+    if shares.size >= 2 and np.all(V == V[0]) and np.all(np.isfinite(shares)):
+        shares = np.full(shares.size, shares[0])
+    return shares
+
+
+def cal_doc_kurt(df):  # CM:937-957
+    return _per_group(df, lambda s, e: pl_kurt(_doc_levels(df, s, e)))
+
+
+def cal_doc_skew(df):  # CM:960-980
+    return _per_group(df, lambda s, e: pl_skew(_doc_levels(df, s, e)))
+
+
+def cal_doc_std(df):  # CM:983-1003 — .skew() [sic, CM:999]
+    return _per_group(df, lambda s, e: pl_skew(_doc_levels(df, s, e)))
+
+
+def _doc_pdf(df, p):
+    """CM:1006-1138.  The rank is frame-wide (CM:1015-1017): every row of every code of
+    the day.  C2: levels are cum-summed in ascending-rank order."""
+    out = {}
+    if not df.groups:
+        return out
+    with np.errstate(all="ignore"):
+        last_close = np.empty_like(df.close)
+        for code, s, e in df.groups:
+            last_close[s:e] = df.close[e - 1]
+        key = last_close / df.close
+    rank = avg_rank(key)
+    for code, s, e in df.groups:
+        v = df.volume[s:e]
+        with np.errstate(all="ignore"):
+            vd = v / np.sum(v)
+        levels: Dict[float, float] = {}
+        for rk, x in zip(rank[s:e].tolist(), vd.tolist()):
+            levels[rk] = levels.get(rk, 0.0) + x
+        cum = 0.0
+        best = None
+        for rk in sorted(levels):  # C2
+            cum = cum + levels[rk]
+            if tot_gt(cum, p) is True:  # cum_sum() > p, S11
+                best = rk if best is None else min(best, rk)
+        out[code] = best  # .filter(...).sort().first(): null if none passes
+    return out
+
+
+def cal_doc_pdf60(df):  # CM:1006-1030
+    return _doc_pdf(df, 0.6)
+
+
+def cal_doc_pdf70(df):  # CM:1033-1057
+    return _doc_pdf(df, 0.7)
+
+
+def cal_doc_pdf80(df):  # CM:1060-1084
+    return _doc_pdf(df, 0.8)
+
+
+def cal_doc_pdf90(df):  # CM:1087-1111
+    return _doc_pdf(df, 0.9)
+
+
+def cal_doc_pdf95(df):  # CM:1114-1138
+    return _doc_pdf(df, 0.95)
+
+
+def _doc_vol_topk(df, k):
+    def f(s, e):
+        v = df.volume[s:e]
+        with np.errstate(all="ignore"):
+            vd = v / np.sum(v)
+        # top_k(k) (S7, NaN is largest under total order) then sum
+        if np.any(np.isnan(vd)):
+            return float("nan")
+        top = np.sort(vd)[::-1][:k]
+        return pl_sum(top)
+    return _per_group(df, f)
+
+
+def cal_doc_vol10_ratio(df):  # CM:1141-1159
+    return _doc_vol_topk(df, 10)
+
+
+def cal_doc_vol5_ratio(df):  # CM:1162-1180
+    return _doc_vol_topk(df, 5)
+
+
+def cal_doc_vol50_ratio(df):  # CM:1183-1201 — top_k(5) [sic, CM:1196]
+    return _doc_vol_topk(df, 5)
+
+
+# ----------------------------------------------------------------------------
+# Fund flow (CM:1203-1406)
+# ----------------------------------------------------------------------------
+
+
+def _tail_ret_ratio(df, t0, plus_one):
+    out = {}
+    for code, s, e in df.groups:
+        sel = df.time[s:e] >= t0
+        if not sel.any():
+            continue
+        v = df.volume[s:e][sel]
+        with np.errstate(all="ignore"):
+            ret = df.close[s:e][sel] / df.open[s:e][sel] - 1.0
+        sv = pl_sum(v)  # volume.sum().over('code') on the filtered frame
+        den = sv + 1.0 if plus_one else (1.0 if sv == 0 else sv)
+        with np.errstate(all="ignore"):
+            vd = v / den
+            out[code] = pl_sum(vd * ret)
+    return out
+
+
+def cal_trade_bottom20retRatio(df):  # CM:1206-1224
+    return _tail_ret_ratio(df, 144000000, True)
+
+
+def cal_trade_bottom50retRatio(df):  # CM:1227-1248
+    return _tail_ret_ratio(df, 141000000, False)
+
+
+def _window_share(df, pred):
+    def f(s, e):
+        v = df.volume[s:e]
+        part = pl_sum(np.where(pred(df.time[s:e]), v, 0.0))
+        tot = pl_sum(v)
+        return _div(part, tot) if tot > 0 else 0.125
+    return _per_group(df, f)
+
+
+def cal_trade_headRatio(df):  # CM:1251-1277
+    return _window_share(df, lambda t: t <= 100000000)
+
+
+def cal_trade_tailRatio(df):  # CM:1280-1306
+    return _window_share(df, lambda t: t >= 143000000)
+
+
+def _head_ret_ratio(df, t1, mode):
+    out = {}
+    for code, s, e in df.groups:
+        sel = df.time[s:e] <= t1
+        if not sel.any():
+            continue
+        v = df.volume[s:e][sel]
+        with np.errstate(all="ignore"):
+            vd = v / np.sum(v)  # volume / volume.sum().over(code, date)
+            pc = df.close[s:e][sel] / df.open[s:e][sel] - 1.0
+            if mode == "all":
+                num = pc
+            elif mode == "neg":
+                num = np.where(pc < 0, np.abs(pc), 0.0)
+            else:
+                num = np.where(pc > 0, np.abs(pc), 0.0)
+            out[code] = pl_mean(num / vd)
+    return out
+
+
+def cal_trade_top20retRatio(df):  # CM:1309-1328
+    return _head_ret_ratio(df, 95000000, "all")
+
+
+def cal_trade_top50retRatio(df):  # CM:1331-1350
+    return _head_ret_ratio(df, 102000000, "all")
+
+
+def cal_trade_topNeg20retRatio(df):  # CM:1353-1378
+    return _head_ret_ratio(df, 95000000, "neg")
+
+
+def cal_trade_topPos20retRatio(df):  # CM:1381-1406
+    return _head_ret_ratio(df, 95000000, "pos")
+
+
+# ----------------------------------------------------------------------------
+# Catalogue in reference order (CM:12-1381)
+# ----------------------------------------------------------------------------
+
+ORACLE_FUNCS: Dict[str, Callable] = {}
+for _name in [
+    "mmt_pm", "mmt_last30", "mmt_paratio", "mmt_am", "mmt_between",
+    "mmt_ols_qrs", "mmt_ols_corr_square_mean", "mmt_ols_corr_mean",
+    "mmt_ols_beta_mean", "mmt_ols_beta_zscore_last",
+    "mmt_top50VolumeRet", "mmt_bottom50VolumeRet", "mmt_top20VolumeRet",
+    "mmt_bottom20VolumeRet",
+    "vol_volume1min", "vol_range1min", "vol_return1min", "vol_upVol", "vol_upRatio",
+    "vol_downVol", "vol_downRatio",
+    "shape_skew", "shape_kurt", "shape_skratio", "shape_skewVol", "shape_kurtVol",
+    "shape_skratioVol",
+    "liq_amihud_1min", "liq_closeprevol", "liq_closevol", "liq_firstCallR",
+    "liq_lastCallR", "liq_openvol",
+    "corr_prv", "corr_prvr", "corr_pv", "corr_pvd", "corr_pvl", "corr_pvr",
+    "doc_kurt", "doc_skew", "doc_std", "doc_pdf60", "doc_pdf70", "doc_pdf80",
+    "doc_pdf90", "doc_pdf95", "doc_vol10_ratio", "doc_vol5_ratio", "doc_vol50_ratio",
+    "trade_bottom20retRatio", "trade_bottom50retRatio", "trade_headRatio",
+    "trade_tailRatio", "trade_top20retRatio", "trade_top50retRatio",
+    "trade_topNeg20retRatio", "trade_topPos20retRatio",
+]:
+    ORACLE_FUNCS[_name] = globals()["cal_" + _name]
+del _name
+
+ORACLE_NAMES = list(ORACLE_FUNCS)
+
+# Output state codes (SURVEY §8(a) output contract)
+ABSENT, NULLV, VALUE = 0, 1, 2
+
+
+# ----------------------------------------------------------------------------
+# Dense-panel drivers
+# ----------------------------------------------------------------------------
+
+
+def day_frame_from_panel(panel, d: int) -> DayFrame:
+    """Build the reference day frame for day ``d`` of a dense panel dict with keys
+    open/high/low/close/volume ([D][S][240] f32), present ([D][S][240] bool), codes."""
+    pres = panel["present"][d]
+    s_idx, m_idx = np.nonzero(pres)  # row-major: ordered by (stock, minute) = C4
+    codes = np.asarray(panel["codes"])[s_idx]
+    f = lambda k: panel[k][d][s_idx, m_idx].astype(np.float64)
+    return DayFrame(codes, d, minute_to_time(m_idx), f("open"), f("high"), f("low"),
+                    f("close"), f("volume"))
+
+
+def oracle_stage1(panel, names: Sequence[str] = None):
+    """Dense (val[F][D][S] f64, state[F][D][S] u8) for the requested factors."""
+    names = list(names or ORACLE_NAMES)
+    D, S = panel["present"].shape[:2]
+    code_index = {c: i for i, c in enumerate(panel["codes"])}
+    val = np.zeros((len(names), D, S), dtype=np.float64)
+    state = np.zeros((len(names), D, S), dtype=np.uint8)
+    for d in range(D):
+        df = day_frame_from_panel(panel, d)
+        for fi, nm in enumerate(names):
+            res = ORACLE_FUNCS[nm](df)
+            for code, x in res.items():
+                s = code_index[code]
+                if x is None:
+                    state[fi, d, s] = NULLV
+                else:
+                    state[fi, d, s] = VALUE
+                    val[fi, d, s] = x
+    return val, state
+
+
+def oracle_stage2(val: np.ndarray, state: np.ndarray, N: int, method: str):
+    """MF:187-240, ``cal_final_exposure(N, method, mode='days')`` on one factor.
+
+    ``val``/``state`` are [D][S]; rows are the long frame sorted [date, code]
+    (MF:100,109); per code the rolling acts over its PRESENT rows in date order
+    (ABSENT days skipped, S13).  Returns dense (val, state) [D][S]."""
+    D, S = val.shape
+    out_v = np.zeros_like(val)
+    out_s = np.zeros_like(state)
+    for s in range(S):
+        rows = [d for d in range(D) if state[d, s] != ABSENT]
+        xs = [None if state[d, s] == NULLV else float(val[d, s]) for d in rows]
+        for k, d in enumerate(rows):
+            x = xs[k]
+            if method == "o":  # MF:190-198
+                res = x
+            else:
+                if k + 1 < N:
+                    res = None
+                else:
+                    win = xs[k + 1 - N : k + 1]
+                    if any(w is None for w in win):  # min_samples=N (S13)
+                        res = None
+                    else:
+                        w = np.array(win, dtype=np.float64)
+                        mean = _mean_exact(w)
+                        var0 = pl_var(w, ddof=0)
+                        with np.errstate(all="ignore"):
+                            sd = math.sqrt(var0) if not math.isnan(var0) else float("nan")
+                        if method == "m":  # MF:199-209
+                            res = mean
+                        elif method == "std":  # MF:228-238
+                            res = sd
+                        elif method == "z":  # MF:210-227
+                            res = None if x is None else _div(x - mean, sd)
+                        else:
+                            raise ValueError("Unknown method")
+            out_s[d, s] = NULLV if res is None else VALUE
+            out_v[d, s] = 0.0 if res is None else res
+    return out_v, out_s
+
+
+def oracle_stage3(val: np.ndarray, state: np.ndarray, kind: str):
+    """Per-date cross-sectional z-score (ddof=1) or average rank.
+
+    Included: state VALUE and non-NaN.  Excluded VALUE-NaN rows stay NaN, NULL rows
+    stay NULL, ABSENT rows stay ABSENT.  z: n < 2 -> NULL for every included row."""
+    D, S = val.shape
+    out_v = np.zeros_like(val)
+    out_s = state.copy()
+    for d in range(D):
+        inc = (state[d] == VALUE) & ~np.isnan(val[d])
+        nanrow = (state[d] == VALUE) & np.isnan(val[d])
+        out_v[d, nanrow] = np.nan
+        x = val[d, inc]
+        if kind == "rank":
+            out_v[d, inc] = avg_rank(x)
+        elif kind == "z":
+            if x.size < 2:
+                out_s[d, inc] = NULLV
+                continue
+            mean = _mean_exact(x)
+            sd = math.sqrt(pl_var(x, ddof=1)) if not np.any(np.isinf(x)) else float("nan")
+            with np.errstate(all="ignore"):
+                out_v[d, inc] = (x - mean) / sd
+        else:
+            raise ValueError(kind)
+    return out_v, out_s

@@ -1,0 +1,113 @@
+// mff_stage2.hip — N-day rolling post-processing (MinuteFrequentFactorCICC.py:187-240).
+//
+// cal_final_exposure(N, method, mode='days') applies, per code over its rows sorted by
+// date (MF:100,109), polars rolling_mean / rolling_std(ddof=0) with window N and
+// min_samples=N (S13).  Rows exist only for present stock-days, so ABSENT days are
+// skipped, not counted; a window holding a null has < N samples -> null.
+//
+// Layout: one wavefront per (factor row, 64 consecutive stocks); lane = stock, loop
+// over days reading val[row][d][s0..s0+63] (512 coalesced bytes per day).  Each lane
+// keeps its last N present values in an LDS ring [N][64] (bank = lane, conflict-free)
+// and a 64-bit null mask, and recomputes the window from scratch each present day:
+// mean = x0 + sum(x - x0)/N (x0 = oldest value when finite, C3), var = sum((x-mean)^2)/N.
+// From scratch (not a sliding sum) so NaN/inf affect only the windows holding them,
+// and a constant window gives std exactly 0 (C6: z = 0/0 = NaN).
+#include "../../include/mff.h"
+#include "mff_internal.h"
+#include "mff_wave.h"
+
+namespace mff {
+
+constexpr int S2_MAXN = 64;
+
+__global__ __launch_bounds__(64) void k_stage2(const double* val, const uint8_t* state, int D, int S, int N,
+                                                int method, double* out_val, uint8_t* out_state) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* ring = reinterpret_cast<double*>(smem);  // [N][64]
+  const int nsb = (S + 63) / 64;
+  const int row = blockIdx.x / nsb;
+  const int s = (blockIdx.x % nsb) * 64 + lane_id();
+  const bool act = s < S;
+  const size_t plane = (size_t)D * S;
+  const double* v = val + row * plane;
+  const uint8_t* st = state + row * plane;
+  double* ov = out_val + row * plane;
+  uint8_t* os = out_state + row * plane;
+  const int lane = lane_id();
+
+  int cnt = 0, pos = 0;
+  uint64_t nullm = 0;
+  double xn = 0.0;
+  uint8_t sn = MFF_STATE_ABSENT;
+  if (act) {
+    xn = v[s];
+    sn = st[s];
+  }
+  for (int d = 0; d < D; ++d) {
+    const double x = xn;
+    const uint8_t sx = sn;
+    if (act && d + 1 < D) {  // prefetch next day
+      xn = v[(size_t)(d + 1) * S + s];
+      sn = st[(size_t)(d + 1) * S + s];
+    }
+    if (!act) continue;
+    const size_t o = (size_t)d * S + s;
+    if (sx == MFF_STATE_ABSENT) {
+      os[o] = MFF_STATE_ABSENT;
+      ov[o] = 0.0;
+      continue;
+    }
+    const bool isnull = sx == MFF_STATE_NULL;
+    if (method == MFF_ROLL_O) {
+      ov[o] = isnull ? 0.0 : x;
+      os[o] = sx;
+      continue;
+    }
+    ring[pos * 64 + lane] = isnull ? 0.0 : x;
+    nullm = isnull ? (nullm | (1ull << pos)) : (nullm & ~(1ull << pos));
+    const int oldest = (pos + 1 == N) ? 0 : pos + 1;
+    pos = oldest;
+    ++cnt;
+    if (cnt < N || nullm != 0) {
+      ov[o] = 0.0;
+      os[o] = MFF_STATE_NULL;
+      continue;
+    }
+    double x0 = ring[oldest * 64 + lane];
+    if (!__builtin_isfinite(x0)) x0 = 0.0;
+    double s1 = 0.0;
+    for (int i = 0; i < N; ++i) s1 += ring[i * 64 + lane] - x0;
+    const double mean = x0 + s1 / (double)N;
+    double s2 = 0.0;
+    for (int i = 0; i < N; ++i) {
+      const double dlt = ring[i * 64 + lane] - mean;
+      s2 += dlt * dlt;
+    }
+    const double sd = sqrt(s2 / (double)N);
+    double res;
+    if (method == MFF_ROLL_M) res = mean;
+    else if (method == MFF_ROLL_STD) res = sd;
+    else res = (x - mean) / sd;  // MFF_ROLL_Z, x not null here
+    ov[o] = res;
+    os[o] = MFF_STATE_VALUE;
+  }
+}
+
+}  // namespace mff
+
+using namespace mff;
+
+extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int D, int S, int N,
+                          int method, double* out_val, uint8_t* out_state, void* stream) {
+  clear_error();
+  MFF_REQUIRE(rows > 0 && D > 0 && S > 0, "mff_stage2: bad sizes rows=%d D=%d S=%d", rows, D, S);
+  MFF_REQUIRE(N >= 1 && N <= S2_MAXN, "mff_stage2: N=%d outside [1, %d]", N, S2_MAXN);
+  MFF_REQUIRE(method >= MFF_ROLL_O && method <= MFF_ROLL_STD, "mff_stage2: unknown method %d", method);
+  MFF_REQUIRE(val && state && out_val && out_state, "mff_stage2: NULL buffer");
+  const long long nblk = (long long)rows * ((S + 63) / 64);
+  const size_t lds = (size_t)N * 64 * 8;
+  hipLaunchKernelGGL(k_stage2, dim3((unsigned)nblk), dim3(64), lds, as_stream(stream), val, state, D, S,
+                     N, method, out_val, out_state);
+  MFF_LAUNCH_CHECK();
+  return 0;
+}

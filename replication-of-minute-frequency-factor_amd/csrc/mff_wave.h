@@ -1,0 +1,300 @@
+// mff_wave.h — wave64 primitives for one stock-day held in one wavefront.
+//
+// Layout ("blocked"): lane l (0..59) owns bars m = 4l+0 .. 4l+3 as four register
+// slots k = 0..3; lanes 60..63 own nothing.  One float4 load per lane per field plane
+// covers the 960 contiguous bytes of a stock-day.
+// Presence of every bar is kept wave-uniform as four 64-bit ballots
+// (Bits.b[k] bit l == bar 4l+k present), so segment endpoints, window counts and
+// first/last bars are scalar bit arithmetic.
+//
+// Reductions broadcast their result to every lane (xor butterfly: every lane sums the
+// same partial sums in mirrored order, so all lanes hold a bitwise-identical value).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mff {
+
+constexpr int WAVE = 64;
+constexpr int NBAR = 240;
+
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63u); }
+
+// ---------------------------------------------------------------- bit casts
+__device__ __forceinline__ uint32_t fbits(float x) { return __float_as_uint(x); }
+__device__ __forceinline__ float bitsf(uint32_t b) { return __uint_as_float(b); }
+__device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
+__device__ __forceinline__ double bitsd(uint64_t b) { return __longlong_as_double((long long)b); }
+
+__device__ __forceinline__ double qnan() { return __longlong_as_double(0x7ff8000000000000ll); }
+
+// S11: polars compares floats in total order: NaN is above every number.
+__device__ __forceinline__ bool tot_gt(double a, double b) {
+  return (a > b) || (__builtin_isnan(a) && !__builtin_isnan(b));
+}
+__device__ __forceinline__ bool tot_lt(double a, double b) { return tot_gt(b, a); }
+__device__ __forceinline__ bool tot_ne(double a, double b) {
+  bool an = __builtin_isnan(a), bn = __builtin_isnan(b);
+  return (an || bn) ? !(an && bn) : (a != b);
+}
+
+// ---------------------------------------------------------------- cross-lane moves
+__device__ __forceinline__ int bperm_i(int src, int v) {
+  return __builtin_amdgcn_ds_bpermute(src << 2, v);
+}
+__device__ __forceinline__ uint32_t bperm(int src, uint32_t v) { return (uint32_t)bperm_i(src, (int)v); }
+__device__ __forceinline__ float bperm(int src, float v) {
+  return __int_as_float(bperm_i(src, __float_as_int(v)));
+}
+__device__ __forceinline__ double bperm(int src, double v) {
+  uint64_t b = dbits(v);
+  int lo = bperm_i(src, (int)(uint32_t)b), hi = bperm_i(src, (int)(uint32_t)(b >> 32));
+  return bitsd(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+__device__ __forceinline__ uint64_t bperm(int src, uint64_t v) {
+  int lo = bperm_i(src, (int)(uint32_t)v), hi = bperm_i(src, (int)(uint32_t)(v >> 32));
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// value of a wave-uniform lane
+__device__ __forceinline__ float rdlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ double rdlane(double v, int l) {
+  uint64_t b = dbits(v);
+  uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return bitsd(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ uint64_t rdlane(uint64_t v, int l) {
+  uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// element e (wave-uniform) of a blocked 4-slot array
+template <typename T>
+__device__ __forceinline__ T elem(const T (&x)[4], int e) {
+  int k = e & 3;
+  T v = (k == 0) ? x[0] : (k == 1) ? x[1] : (k == 2) ? x[2] : x[3];
+  return rdlane(v, e >> 2);
+}
+
+// ---------------------------------------------------------------- reductions
+__device__ __forceinline__ double wsum(double x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+__device__ __forceinline__ double wprod(double x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x *= __shfl_xor(x, o);
+  return x;
+}
+__device__ __forceinline__ uint32_t wsum_u32(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o);
+  return x;
+}
+
+// ---------------------------------------------------------------- presence bits
+struct Bits {
+  uint64_t b[4];
+};
+
+__device__ __forceinline__ Bits ballot4(const bool (&p)[4]) {
+  Bits r;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r.b[k] = __ballot(p[k]);
+  return r;
+}
+__device__ __forceinline__ int count(const Bits& B) {
+  return __popcll(B.b[0]) + __popcll(B.b[1]) + __popcll(B.b[2]) + __popcll(B.b[3]);
+}
+__device__ __forceinline__ bool any(const Bits& B) { return (B.b[0] | B.b[1] | B.b[2] | B.b[3]) != 0; }
+__device__ __forceinline__ bool test(const Bits& B, int m) { return (B.b[m & 3] >> (m >> 2)) & 1ull; }
+// first / last set element index (4l+k), -1 when empty
+__device__ __forceinline__ int first_of(const Bits& B) {
+  int best = 1 << 20;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (B.b[k]) best = min(best, 4 * (int)__builtin_ctzll(B.b[k]) + k);
+  return best == (1 << 20) ? -1 : best;
+}
+__device__ __forceinline__ int last_of(const Bits& B) {
+  int best = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (B.b[k]) best = max(best, 4 * (63 - (int)__builtin_clzll(B.b[k])) + k);
+  return best;
+}
+// bars in [lo, hi] (inclusive), as Bits
+__device__ __forceinline__ Bits range_bits(int lo, int hi) {
+  Bits R;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int l0 = (lo - k + 3) >> 2;  // ceil((lo-k)/4), lo-k >= -3
+    if (lo - k < 0) l0 = 0;
+    int l1 = (hi - k) >> 2;      // floor((hi-k)/4)
+    if (hi - k < 0) l1 = -1;
+    uint64_t m = 0;
+    if (l1 >= l0) {
+      uint64_t upto = (l1 >= 63) ? ~0ull : ((1ull << (l1 + 1)) - 1);
+      uint64_t below = (l0 <= 0) ? 0ull : ((1ull << l0) - 1);
+      m = upto & ~below;
+    }
+    R.b[k] = m;
+  }
+  return R;
+}
+__device__ __forceinline__ Bits band(const Bits& A, const Bits& B) {
+  Bits R;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) R.b[k] = A.b[k] & B.b[k];
+  return R;
+}
+// this lane's slot k membership
+__device__ __forceinline__ bool mine(const Bits& B, int k) { return (B.b[k] >> lane_id()) & 1ull; }
+
+// ---------------------------------------------------------------- scans
+// inclusive prefix over all 64 lanes
+__device__ __forceinline__ double wscan_incl(double x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    double y = __shfl_up(x, o);
+    if (l >= o) x += y;
+  }
+  return x;
+}
+__device__ __forceinline__ uint32_t wscan_incl_u32(uint32_t x) {
+  const int l = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = (uint32_t)__shfl_up((int)x, o);
+    if (l >= o) x += y;
+  }
+  return x;
+}
+// inclusive prefix over the 256 blocked elements (bar order)
+__device__ __forceinline__ void scan4(double (&v)[4]) {
+  v[1] += v[0];
+  v[2] += v[1];
+  v[3] += v[2];
+  double inc = wscan_incl(v[3]);
+  double ex = __shfl_up(inc, 1);
+  if (lane_id() == 0) ex = 0.0;
+  v[0] += ex; v[1] += ex; v[2] += ex; v[3] += ex;
+}
+__device__ __forceinline__ void scan4_u32(uint32_t (&v)[4]) {
+  v[1] += v[0];
+  v[2] += v[1];
+  v[3] += v[2];
+  uint32_t inc = wscan_incl_u32(v[3]);
+  uint32_t ex = (uint32_t)__shfl_up((int)inc, 1);
+  if (lane_id() == 0) ex = 0;
+  v[0] += ex; v[1] += ex; v[2] += ex; v[3] += ex;
+}
+
+// For each element: the value of the nearest PREVIOUS element with flag set
+// (polars shift(1) / pct_change over present rows, S4/S5).
+template <typename T>
+__device__ __forceinline__ void prev_valid(const T (&x)[4], const bool (&f)[4], T (&prev)[4], bool (&has)[4]) {
+  const int l = lane_id();
+  bool lh = f[0] | f[1] | f[2] | f[3];
+  T lv = f[3] ? x[3] : f[2] ? x[2] : f[1] ? x[1] : x[0];
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T ov = __shfl_up(lv, o);
+    int oh = __shfl_up((int)lh, o);
+    if (l >= o && !lh) { lv = ov; lh = oh != 0; }
+  }
+  T cv = __shfl_up(lv, 1);
+  bool ch = __shfl_up((int)lh, 1) != 0;
+  if (l == 0) ch = false;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    prev[k] = cv;
+    has[k] = ch;
+    if (f[k]) { cv = x[k]; ch = true; }
+  }
+}
+// nearest NEXT element with flag set (polars shift(-1))
+template <typename T>
+__device__ __forceinline__ void next_valid(const T (&x)[4], const bool (&f)[4], T (&next)[4], bool (&has)[4]) {
+  const int l = lane_id();
+  bool lh = f[0] | f[1] | f[2] | f[3];
+  T lv = f[0] ? x[0] : f[1] ? x[1] : f[2] ? x[2] : x[3];
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T ov = __shfl_down(lv, o);
+    int oh = __shfl_down((int)lh, o);
+    if (l + o < 64 && !lh) { lv = ov; lh = oh != 0; }
+  }
+  T cv = __shfl_down(lv, 1);
+  bool ch = __shfl_down((int)lh, 1) != 0;
+  if (l == 63) ch = false;
+#pragma unroll
+  for (int k = 3; k >= 0; --k) {
+    next[k] = cv;
+    has[k] = ch;
+    if (f[k]) { cv = x[k]; ch = true; }
+  }
+}
+
+// ---------------------------------------------------------------- bitonic sort
+// Ascending sort of the 256 blocked elements (e = 4*lane + k).
+template <typename K>
+__device__ __forceinline__ void cmpx_local(K& a, K& b, bool up) {
+  bool sw = up ? (a > b) : (a < b);
+  K t = a;
+  a = sw ? b : a;
+  b = sw ? t : b;
+}
+template <typename K>
+__device__ __forceinline__ void bitonic256(K (&a)[4]) {
+  const int l = lane_id();
+#pragma unroll
+  for (int size = 2; size <= 256; size <<= 1) {
+#pragma unroll
+    for (int j = size >> 1; j > 0; j >>= 1) {
+      if (j >= 4) {
+        const int lj = j >> 2;
+        const bool lower = (l & lj) == 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int e = 4 * l + k;
+          const bool up = (e & size) == 0;
+          K p = __shfl_xor(a[k], lj);
+          K mn = a[k] < p ? a[k] : p;
+          K mx = a[k] < p ? p : a[k];
+          a[k] = (lower == up) ? mn : mx;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if ((k & j) == 0) {
+            const int e = 4 * l + k;
+            cmpx_local(a[k], a[k | j], (e & size) == 0);
+          }
+        }
+      }
+    }
+  }
+}
+
+// f64 total-order image as u64 (ascending u64 == ascending total order; -0 == +0)
+__device__ __forceinline__ uint64_t ord64(double x) {
+  if (x == 0.0) x = 0.0;
+  uint64_t b = dbits(x);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double unord64(uint64_t k) {
+  uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+  return bitsd(b);
+}
+
+}  // namespace mff

@@ -1,0 +1,180 @@
+"""Device engine: dense panels in HBM -> libmff.so kernels.
+
+Everything here works on torch tensors that already live on one GPU (torch is only the
+buffer / stream carrier); each function issues asynchronous libmff calls on the
+current torch stream.  Multi-GPU collectives (doc_pdf frame-wide rank, stage-3
+cross-sections) are delegated to a ``comm`` object (:mod:`mff.dist`), so the same code
+runs single-GPU (``comm=None``) and stock-sharded.
+
+Stage map:
+  :func:`compute_factors`  stage 1, the 58 cal_* of MinuteFrequentFactorCalculateMethodsCICC.py
+  :func:`rolling`          stage 2, MinFreqFactor.cal_final_exposure(mode='days') (MF:187-240)
+  :func:`cross_section`    stage 3, per-day z-score / average rank
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib, catalog
+from .synth import pack_mask, stack_fields
+
+ABSENT, NULL, VALUE = 0, 1, 2
+ROLL_METHODS = {"o": 0, "m": 1, "z": 2, "std": 3}
+PDF_MAX_QUERIES = 32767  # per day, all ranks (mff_pdf_count LDS bins)
+
+
+def _stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+@dataclass
+class DevicePanel:
+    """One device's dense panel.
+
+    bars: float32 [5][D][S][240] (open, high, low, close, volume planes)
+    mask: int32 [D][S][8] presence bits (bit m%32 of word m//32)
+    """
+
+    bars: torch.Tensor
+    mask: torch.Tensor
+    codes: List[str] = field(default_factory=list)
+    dates: List = field(default_factory=list)
+
+    @property
+    def D(self) -> int:
+        return int(self.bars.shape[1])
+
+    @property
+    def S(self) -> int:
+        return int(self.bars.shape[2])
+
+    @property
+    def device(self):
+        return self.bars.device
+
+    def plane(self, k: int) -> torch.Tensor:
+        return self.bars[k]
+
+    @classmethod
+    def from_host(cls, panel, device="cuda") -> "DevicePanel":
+        """Host dict (see :mod:`mff.synth`) -> device tensors.  Validates the input
+        contract the kernels rely on (include/mff.h)."""
+        validate_host_panel(panel)
+        bars = torch.from_numpy(np.ascontiguousarray(stack_fields(panel))).to(device)
+        mask = torch.from_numpy(pack_mask(panel["present"]).view(np.int32)).to(device)
+        return cls(bars, mask, list(panel["codes"]), list(panel["dates"]))
+
+
+def validate_host_panel(panel) -> None:
+    pres = panel["present"]
+    v = panel["volume"][pres]
+    if v.size and (np.any(v < 0) or np.any(v > 2 ** 24) or np.any(v != np.rint(v))):
+        raise ValueError("volume must be integral and within [0, 2**24] (fp32-exact)")
+    for k in ("open", "high", "low", "close"):
+        x = panel[k][pres]
+        if x.size and (not np.all(np.isfinite(x)) or np.any(x <= 0)):
+            raise ValueError(f"{k} must be finite and > 0 on present bars")
+
+
+def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, comm=None,
+                    pdf_day_batch: Optional[int] = None):
+    """Stage 1 for the requested factors (default: all 58, reference order).
+
+    Returns (val float64 [nf][D][S], state uint8 [nf][D][S], ids)."""
+    lib = _lib.load()
+    ids = catalog.resolve(names)
+    nf, D, S = len(ids), panel.D, panel.S
+    dev = panel.device
+    val = torch.empty((nf, D, S), dtype=torch.float64, device=dev)
+    state = torch.empty((nf, D, S), dtype=torch.uint8, device=dev)
+    need_pdf = any(i in catalog.PDF_IDS for i in ids)
+    pdfq = torch.empty((5, D, S), dtype=torch.float64, device=dev) if need_pdf else None
+    b = panel.bars
+    _lib.check(lib.mff_stage1(_lib.ptr(b[0]), _lib.ptr(b[1]), _lib.ptr(b[2]), _lib.ptr(b[3]),
+                              _lib.ptr(b[4]), _lib.ptr(panel.mask), S, D,
+                              _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
+                              _lib.ptr(pdfq), _stream(dev)), "mff_stage1")
+    if need_pdf:
+        rows = [ids.index(i) if i in ids else -1 for i in catalog.PDF_IDS]
+        pdf_ranks(panel, pdfq, rows, val, state, comm=comm, day_batch=pdf_day_batch)
+    return val, state, ids
+
+
+def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, rows: List[int], val, state, comm=None,
+              day_batch: Optional[int] = None, workspace_budget: int = 2 << 30):
+    """doc_pdf frame-wide ranks (CM:1015-1017) for all days, in day batches."""
+    lib = _lib.load()
+    D, S = panel.D, panel.S
+    dev = panel.device
+    R = 1 if comm is None else comm.world_size
+    q_all = pdfq if comm is None else comm.all_gather(pdfq)  # [R][5][D][S]
+    M = R * 5 * S
+    if M > PDF_MAX_QUERIES:
+        raise _lib.MffError(f"doc_pdf: {M} queries per day exceed {PDF_MAX_QUERIES} "
+                            f"(ranks*5*stocks); shard fewer stocks per day")
+    if day_batch is None:
+        per_day = lib.mff_pdf_workspace_bytes(S, R, 1) + M * 8 + M * 8
+        day_batch = max(1, min(D, workspace_budget // max(per_day, 1)))
+    st = _stream(dev)
+    for d0 in range(0, D, day_batch):
+        nd = min(day_batch, D - d0)
+        ws = torch.empty(lib.mff_pdf_workspace_bytes(S, R, nd), dtype=torch.uint8, device=dev)
+        q_sorted = torch.empty((nd, M), dtype=torch.int64, device=dev)
+        counts = torch.empty((nd, M, 2), dtype=torch.int32, device=dev)
+        _lib.check(lib.mff_pdf_sort(_lib.ptr(q_all), R, S, D, d0, nd, _lib.ptr(q_sorted),
+                                    _lib.ptr(ws), st), "mff_pdf_sort")
+        _lib.check(lib.mff_pdf_count(_lib.ptr(panel.bars[3]), _lib.ptr(panel.mask), S, D, d0, nd,
+                                     _lib.ptr(q_sorted), M, _lib.ptr(counts), _lib.ptr(ws), st),
+                   "mff_pdf_count")
+        if comm is not None:
+            comm.all_reduce_sum(counts)
+        _lib.check(lib.mff_pdf_finalize(_lib.ptr(pdfq), _lib.ptr(q_sorted), _lib.ptr(counts), S, D,
+                                        d0, nd, M, _lib.int_array(rows), _lib.ptr(val),
+                                        _lib.ptr(state), st), "mff_pdf_finalize")
+
+
+def rolling(val: torch.Tensor, state: torch.Tensor, N: int, method: str):
+    """Stage 2 on [rows][D][S] (MF:187-240): returns (out_val, out_state)."""
+    lib = _lib.load()
+    if method not in ROLL_METHODS:
+        raise ValueError("Unknown method")
+    if not isinstance(N, int):
+        raise ValueError(f"Unsupported frequency for days: {N}")
+    rows, D, S = val.shape
+    ov = torch.empty_like(val)
+    os_ = torch.empty_like(state)
+    _lib.check(lib.mff_stage2(_lib.ptr(val), _lib.ptr(state), rows, D, S, N, ROLL_METHODS[method],
+                              _lib.ptr(ov), _lib.ptr(os_), _stream(val.device)), "mff_stage2")
+    return ov, os_
+
+
+def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None):
+    """Stage 3 on [rows][D][S_loc]: per-day z-score ('z') or average rank ('rank')."""
+    lib = _lib.load()
+    rows, D, S = val.shape
+    dev = val.device
+    st = _stream(dev)
+    ov = torch.empty_like(val)
+    os_ = torch.empty_like(state)
+    R = 1 if comm is None else comm.world_size
+    if kind == "z":
+        mom = torch.empty((rows, D, 3), dtype=torch.float64, device=dev)
+        _lib.check(lib.mff_xs_moments(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(mom), st),
+                   "mff_xs_moments")
+        mom_all = mom if comm is None else comm.all_gather(mom)
+        _lib.check(lib.mff_xs_zscore(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(mom_all), R,
+                                     _lib.ptr(ov), _lib.ptr(os_), st), "mff_xs_zscore")
+    elif kind == "rank":
+        v_all = val if comm is None else comm.all_gather(val)
+        s_all = state if comm is None else comm.all_gather(state)
+        ws = torch.empty(lib.mff_xs_rank_workspace_bytes(rows, D, S, R), dtype=torch.uint8, device=dev)
+        _lib.check(lib.mff_xs_rank(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(v_all),
+                                   _lib.ptr(s_all), R, _lib.ptr(ov), _lib.ptr(os_), _lib.ptr(ws), st),
+                   "mff_xs_rank")
+    else:
+        raise ValueError(kind)
+    return ov, os_

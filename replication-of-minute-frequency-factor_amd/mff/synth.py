@@ -1,0 +1,204 @@
+"""Synthetic minute-bar panels (SURVEY.md §8(d) "Synthetic inputs").
+
+Two generators with the same distribution:
+
+* :func:`make_panel` — numpy PCG64 on the host, seed ``20251024 + config``; used by the
+  parity tests and golden fixtures (deterministic bit for bit).
+* :func:`make_panel_device` — torch on the GPU, for the full-size bench configs
+  (60 GB at config 4 cannot be generated on the host and pushed over PCIe per run).
+
+Panel layout (host dict):
+  ``open/high/low/close/volume``: float32 [D][S][240]; absent bars hold NaN so a kernel
+  that reads an absent bar poisons its output instead of passing by luck.
+  ``present``: bool [D][S][240]; ``codes``: sorted code strings; ``dates``: ISO dates.
+
+Prices: per-stock start lognormal(ln 15, 0.8) clipped to [1, 500]; per-minute log-return
+N(0, sigma_s), sigma_s ~ U(5e-4, 3e-3); open = previous close; high/low add |N|*tick beyond
+max/min(open, close); everything rounded to the 0.01 tick then cast to fp32 (ties and
+flat windows).  Volume: lognormal with a U-shaped intraday profile x stock scale,
+rounded to multiples of 100, capped at 2**24 (fp32-exact), 1 % zero-volume bars.
+Ragged panels (config 5) add suspended stock-days, missing bars, gap runs and flat
+zero-volume days.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+from typing import Dict, List
+
+import numpy as np
+
+MINUTES = 240
+TICK = 0.01
+VOL_CAP = float(2 ** 24)
+BASE_SEED = 20251024
+
+
+def trading_dates(D: int, start=_dt.date(2020, 1, 2)) -> List[_dt.date]:
+    out, d = [], start
+    while len(out) < D:
+        if d.weekday() < 5:
+            out.append(d)
+        d += _dt.timedelta(days=1)
+    return out
+
+
+def stock_codes(S: int) -> List[str]:
+    codes = []
+    for i in range(S):
+        n = i + 1
+        codes.append(f"{n:06d}.SZ" if i % 2 == 0 else f"{600000 + n:06d}.SH")
+    return sorted(codes)
+
+
+def _u_profile() -> np.ndarray:
+    m = np.arange(MINUTES, dtype=np.float64)
+    return 1.0 + 2.0 * ((m - 119.5) / 119.5) ** 2
+
+
+def _round_tick(x):
+    return np.round(x / TICK) * TICK
+
+
+def make_panel(S: int, D: int, config: int = 2, ragged: bool = False,
+               seed: int | None = None) -> Dict:
+    rng = np.random.Generator(np.random.PCG64(BASE_SEED + config if seed is None else seed))
+    p_prev = np.clip(rng.lognormal(np.log(15.0), 0.8, size=S), 1.0, 500.0)
+    p_prev = np.maximum(_round_tick(p_prev), TICK)
+    sigma = rng.uniform(5e-4, 3e-3, size=S)
+    vscale = rng.lognormal(np.log(800.0), 1.0, size=S)
+    prof = _u_profile()
+
+    shape = (D, S, MINUTES)
+    o = np.empty(shape, np.float32)
+    h = np.empty(shape, np.float32)
+    lo = np.empty(shape, np.float32)
+    c = np.empty(shape, np.float32)
+    v = np.empty(shape, np.float32)
+    present = np.ones(shape, dtype=bool)
+
+    for d in range(D):
+        gap = np.exp(rng.normal(0.0, 2.0 * sigma))
+        day_open = np.maximum(_round_tick(p_prev * gap), TICK)
+        lr = rng.normal(0.0, 1.0, size=(S, MINUTES)) * sigma[:, None]
+        close = np.maximum(_round_tick(day_open[:, None] * np.exp(np.cumsum(lr, axis=1))), TICK)
+        opn = np.concatenate([day_open[:, None], close[:, :-1]], axis=1)
+        hi = _round_tick(np.maximum(opn, close) + np.abs(rng.normal(0, 1, (S, MINUTES))) * 2 * TICK)
+        low = np.maximum(_round_tick(np.minimum(opn, close) - np.abs(rng.normal(0, 1, (S, MINUTES))) * 2 * TICK), TICK)
+        vol = np.round(vscale[:, None] * prof[None, :] * rng.lognormal(0.0, 0.6, (S, MINUTES))) * 100.0
+        vol[rng.random((S, MINUTES)) < 0.01] = 0.0
+        vol = np.minimum(vol, VOL_CAP - (VOL_CAP % 100))
+        o[d], h[d], lo[d], c[d], v[d] = opn, hi, low, close, vol
+        p_prev = close[:, -1]
+
+    if ragged:
+        _make_ragged(rng, o, h, lo, c, v, present)
+
+    for arr in (o, h, lo, c, v):
+        arr[~present] = np.nan
+    return {"open": o, "high": h, "low": lo, "close": c, "volume": v,
+            "present": present, "codes": stock_codes(S), "dates": trading_dates(D)}
+
+
+def _make_ragged(rng, o, h, lo, c, v, present):
+    D, S, M = present.shape
+    # 3 % of stock-days suspended, in contiguous runs of 1..10 days
+    target = int(round(0.03 * D * S))
+    done = 0
+    while done < target:
+        s = rng.integers(S)
+        d0 = rng.integers(D)
+        run = int(rng.integers(1, 11))
+        d1 = min(D, d0 + run)
+        present[d0:d1, s, :] = False
+        done += d1 - d0
+    # 0.5 % of bars missing at random
+    present &= rng.random(present.shape) >= 0.005
+    # 5 contiguous-gap stock-days per 1000
+    n_gap = max(1, int(round(0.005 * D * S)))
+    for _ in range(n_gap):
+        d, s = rng.integers(D), rng.integers(S)
+        a = int(rng.integers(0, M - 10))
+        b = int(min(M, a + rng.integers(5, 60)))
+        present[d, s, a:b] = False
+    # 0.2 % flat stock-days with zero volume
+    n_flat = max(1, int(round(0.002 * D * S)))
+    for _ in range(n_flat):
+        d, s = rng.integers(D), rng.integers(S)
+        px = c[d, s, 0] if np.isfinite(c[d, s, 0]) else np.float32(10.0)
+        o[d, s, :] = h[d, s, :] = lo[d, s, :] = c[d, s, :] = px
+        v[d, s, :] = 0.0
+
+
+def pack_mask(present: np.ndarray) -> np.ndarray:
+    """bool [..., 240] -> uint32 [..., 8] (bit m % 32 of word m // 32 = bar m present)."""
+    sh = present.shape[:-1]
+    bits = present.reshape(-1, 8, 32).astype(np.uint64)
+    w = (bits << np.arange(32, dtype=np.uint64)).sum(axis=2).astype(np.uint32)
+    return w.reshape(*sh, 8)
+
+
+def unpack_mask(words: np.ndarray) -> np.ndarray:
+    sh = words.shape[:-1]
+    w = words.reshape(-1, 8, 1).astype(np.uint64)
+    bits = ((w >> np.arange(32, dtype=np.uint64)) & 1).astype(bool)
+    return bits.reshape(*sh, MINUTES)
+
+
+def stack_fields(panel: Dict) -> np.ndarray:
+    """Host panel -> the device bar layout float32 [5][D][S][240] (open, high, low, close, volume)."""
+    return np.stack([panel[k] for k in ("open", "high", "low", "close", "volume")])
+
+
+def subpanel(panel: Dict, stocks=None, days=None) -> Dict:
+    st = slice(None) if stocks is None else stocks
+    dy = slice(None) if days is None else days
+    out = {k: panel[k][dy][:, st] for k in ("open", "high", "low", "close", "volume", "present")}
+    out["codes"] = list(np.asarray(panel["codes"])[st])
+    out["dates"] = list(np.asarray(panel["dates"], dtype=object)[dy])
+    return out
+
+
+def make_panel_device(S: int, D: int, device, config: int = 3, day_chunk: int = 50,
+                      ragged: bool = False):
+    """Same distribution as :func:`make_panel`, generated on ``device`` with torch.
+
+    Returns (bars float32 [5][D][S][240], mask int32 [D][S][8]).  Used only where the
+    panel is too large for the host path (bench configs 3/4)."""
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(BASE_SEED + config)
+    f64 = dict(device=device, dtype=torch.float64)
+    bars = torch.empty((5, D, S, MINUTES), device=device, dtype=torch.float32)
+    p_prev = torch.exp(torch.randn(S, generator=g, **f64) * 0.8 + np.log(15.0)).clamp(1.0, 500.0)
+    p_prev = torch.clamp(torch.round(p_prev / TICK) * TICK, min=TICK)
+    sigma = torch.rand(S, generator=g, **f64) * (3e-3 - 5e-4) + 5e-4
+    vscale = torch.exp(torch.randn(S, generator=g, **f64) + np.log(800.0))
+    prof = torch.as_tensor(_u_profile(), **f64)
+    rt = lambda x: torch.round(x / TICK) * TICK
+    for d0 in range(0, D, day_chunk):
+        for d in range(d0, min(D, d0 + day_chunk)):
+            gap = torch.exp(torch.randn(S, generator=g, **f64) * 2.0 * sigma)
+            day_open = torch.clamp(rt(p_prev * gap), min=TICK)
+            lr = torch.randn((S, MINUTES), generator=g, **f64) * sigma[:, None]
+            close = torch.clamp(rt(day_open[:, None] * torch.exp(torch.cumsum(lr, 1))), min=TICK)
+            opn = torch.cat([day_open[:, None], close[:, :-1]], 1)
+            hi = rt(torch.maximum(opn, close) + torch.randn((S, MINUTES), generator=g, **f64).abs() * 2 * TICK)
+            low = torch.clamp(rt(torch.minimum(opn, close) - torch.randn((S, MINUTES), generator=g, **f64).abs() * 2 * TICK), min=TICK)
+            vol = torch.round(vscale[:, None] * prof[None, :] * torch.exp(torch.randn((S, MINUTES), generator=g, **f64) * 0.6)) * 100.0
+            vol = torch.where(torch.rand((S, MINUTES), generator=g, **f64) < 0.01, torch.zeros_like(vol), vol)
+            vol = torch.clamp(vol, max=VOL_CAP - (VOL_CAP % 100))
+            for k, x in enumerate((opn, hi, low, close, vol)):
+                bars[k, d] = x.to(torch.float32)
+            p_prev = close[:, -1]
+    mask = torch.full((D, S, 8), -1, device=device, dtype=torch.int32)
+    if ragged:
+        # suspended stock-days (3 %) and random missing bars (0.5 %)
+        sus = torch.rand((D, S), generator=g, device=device) < 0.03
+        mask[sus] = 0
+        miss = torch.rand((D, S, MINUTES), generator=g, device=device) < 0.005
+        bitsv = (~miss).view(D, S, 8, 32).to(torch.int64)
+        words = (bitsv << torch.arange(32, device=device, dtype=torch.int64)).sum(-1)
+        words = words.to(torch.int64).where(words < 2 ** 31, words - 2 ** 32).to(torch.int32)
+        mask = mask & words
+    return bars, mask

@@ -1,0 +1,173 @@
+"""GPU parity: libmff.so kernels vs the CPU oracle (tolerance rule C5, tests/parity.py).
+
+Every test calls the product path (mff.engine -> ctypes -> libmff.so HIP kernels) and
+compares with either a committed golden fixture (tests/golden/, made by the oracle) or
+the oracle run live on the same seeded inputs.
+"""
+import numpy as np
+import pytest
+
+from parity import compare
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _golden(name):
+    from golden.make_golden import load
+    return load(name)
+
+
+def _run_stage1(panel, dev, names=None):
+    from mff import engine
+    dp = engine.DevicePanel.from_host(panel, dev)
+    val, state, ids = engine.compute_factors(dp, names)
+    torch.cuda.synchronize()
+    return val.cpu().numpy(), state.cpu().numpy(), ids
+
+
+def _check_all(gv, gs, z_val, z_state, names):
+    """gv/gs rows are `names` in request order; z_val/z_state rows are catalogue order."""
+    from mff import catalog
+    bad = []
+    for r, nm in enumerate(names):
+        i = catalog.ID[nm]
+        bad += compare(gv[r], gs[r], z_val[i], z_state[i], nm)
+    assert not bad, "\n".join(bad)
+
+
+@pytest.mark.parametrize("fixture", ["panel_ragged.npz", "panel_edge.npz"])
+def test_stage1_all_factors_golden(dev, fixture):
+    panel, z = _golden(fixture)
+    gv, gs, ids = _run_stage1(panel, dev)
+    from mff import catalog
+    assert list(z["names"]) == catalog.NAMES
+    _check_all(gv, gs, z["val"], z["state"], catalog.NAMES)
+
+
+def test_stage1_subset_config1(dev):
+    """BASELINE config 1: realized vol / skew / kurt only (reads open + close planes)."""
+    panel, z = _golden("panel_ragged.npz")
+    names = ["vol_return1min", "shape_skew", "shape_kurt"]
+    gv, gs, ids = _run_stage1(panel, dev, names)
+    assert gv.shape[0] == 3
+    _check_all(gv, gs, z["val"], z["state"], names)
+
+
+def test_stage1_subset_order_and_pdf_only(dev):
+    panel, z = _golden("panel_ragged.npz")
+    names = ["doc_pdf95", "mmt_pm", "doc_pdf60", "corr_pvr"]
+    gv, gs, ids = _run_stage1(panel, dev, names)
+    _check_all(gv, gs, z["val"], z["state"], names)
+
+
+def test_stage1_live_oracle_new_seed(dev):
+    import mff_oracle as O
+    from mff import synth, catalog
+    panel = synth.make_panel(37, 2, config=11, ragged=True)
+    ov, os_ = O.oracle_stage1(panel)
+    gv, gs, ids = _run_stage1(panel, dev)
+    _check_all(gv, gs, ov, os_, catalog.NAMES)
+
+
+def test_doc_pdf_merge_path(dev):
+    """M = 5*S = 8,500 > 8,192 queries per day: the sort finishes with a global merge pass."""
+    import mff_oracle as O
+    from mff import synth
+    panel = synth.make_panel(1700, 1, config=12)
+    names = ["doc_pdf60", "doc_pdf95"]
+    ov, os_ = O.oracle_stage1(panel, names)
+    gv, gs, _ = _run_stage1(panel, dev, names)
+    bad = []
+    for r, nm in enumerate(names):
+        bad += compare(gv[r], gs[r], ov[r], os_[r], nm, atol=0.0, rtol=0.0)
+    assert not bad, "\n".join(bad)
+
+
+def test_stage2_golden(dev):
+    from golden.make_golden import STAGE23_FACTORS
+    from mff import engine, catalog
+    panel, z = _golden("panel_ragged.npz")
+    bad = []
+    for nm in STAGE23_FACTORS:
+        i = catalog.ID[nm]
+        v = torch.from_numpy(z["val"][i][None]).to(dev)
+        s = torch.from_numpy(z["state"][i][None]).to(dev)
+        for meth in ("o", "m", "z", "std"):
+            rv, rs = engine.rolling(v, s, 3, meth)
+            torch.cuda.synchronize()
+            bad += compare(rv[0].cpu().numpy(), rs[0].cpu().numpy(), z[f"s2_{nm}_{meth}_val"],
+                           z[f"s2_{nm}_{meth}_state"], f"{nm}/{meth}", atol=1e-12)
+    assert not bad, "\n".join(bad)
+
+
+def _random_long_panel(D, S, seed):
+    """[D][S] factor column with ABSENT / NULL / NaN / +inf entries, a constant column
+    (std 0 windows) and heavy ties."""
+    rng = np.random.default_rng(seed)
+    val = rng.normal(size=(D, S)) * rng.choice([1e-3, 1.0, 1e5], size=(1, S))
+    ties = rng.random((D, S)) < 0.3
+    val[ties] = np.round(val[ties])
+    state = np.full((D, S), 2, np.uint8)
+    state[rng.random((D, S)) < 0.05] = 0
+    state[rng.random((D, S)) < 0.02] = 1
+    val[rng.random((D, S)) < 0.01] = np.nan
+    val[rng.random((D, S)) < 0.005] = np.inf
+    val[:, 3] = 1.25
+    return val, state
+
+
+@pytest.mark.parametrize("N", [1, 5, 20])
+def test_stage2_live(dev, N):
+    import mff_oracle as O
+    from mff import engine
+    val, state = _random_long_panel(70, 130, N)
+    bad = []
+    for meth in ("o", "m", "z", "std"):
+        ov, os_ = O.oracle_stage2(val, state, N, meth)
+        rv, rs = engine.rolling(torch.from_numpy(val[None]).to(dev), torch.from_numpy(state[None]).to(dev),
+                                N, meth)
+        torch.cuda.synchronize()
+        bad += compare(rv[0].cpu().numpy(), rs[0].cpu().numpy(), ov, os_, f"N{N}/{meth}", atol=1e-9)
+    assert not bad, "\n".join(bad)
+
+
+@pytest.mark.parametrize("kind", ["z", "rank"])
+@pytest.mark.parametrize("S", [130, 9000])
+def test_stage3_live(dev, kind, S):
+    import mff_oracle as O
+    from mff import engine
+    val, state = _random_long_panel(6, S, 3)
+    val[2, :] = 7.0  # constant day -> z NaN (0/0)
+    val[:, :40] = np.round(val[:, :40])  # ties for the rank
+    ov, os_ = O.oracle_stage3(val, state, kind)
+    rv, rs = engine.cross_section(torch.from_numpy(val[None]).to(dev), torch.from_numpy(state[None]).to(dev),
+                                  kind)
+    torch.cuda.synchronize()
+    bad = compare(rv[0].cpu().numpy(), rs[0].cpu().numpy(), ov, os_, f"xs/{kind}", atol=1e-12,
+                  rtol=0.0 if kind == "rank" else 1e-6)
+    assert not bad, "\n".join(bad)
+
+
+def test_stage3_golden(dev):
+    from golden.make_golden import STAGE23_FACTORS
+    from mff import engine, catalog
+    panel, z = _golden("panel_ragged.npz")
+    bad = []
+    for nm in STAGE23_FACTORS:
+        i = catalog.ID[nm]
+        for kind in ("z", "rank"):
+            rv, rs = engine.cross_section(torch.from_numpy(z["val"][i][None]).to(dev),
+                                          torch.from_numpy(z["state"][i][None]).to(dev), kind)
+            torch.cuda.synchronize()
+            bad += compare(rv[0].cpu().numpy(), rs[0].cpu().numpy(), z[f"s3_{nm}_{kind}_val"],
+                           z[f"s3_{nm}_{kind}_state"], f"{nm}/{kind}", atol=1e-12)
+    assert not bad, "\n".join(bad)
