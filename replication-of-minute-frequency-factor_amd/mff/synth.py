@@ -130,9 +130,13 @@ def _make_ragged(rng, o, h, lo, c, v, present):
 
 
 def pack_mask(present: np.ndarray) -> np.ndarray:
-    """bool [..., 240] -> uint32 [..., 8] (bit m % 32 of word m // 32 = bar m present)."""
+    """bool [..., 240] -> uint32 [..., 8] (bit m % 32 of word m // 32 = bar m present;
+    bits 240..255 of the last word are zero)."""
     sh = present.shape[:-1]
-    bits = present.reshape(-1, 8, 32).astype(np.uint64)
+    flat = present.reshape(-1, MINUTES)
+    padded = np.zeros((flat.shape[0], 256), dtype=np.uint64)
+    padded[:, :MINUTES] = flat
+    bits = padded.reshape(-1, 8, 32)
     w = (bits << np.arange(32, dtype=np.uint64)).sum(axis=2).astype(np.uint32)
     return w.reshape(*sh, 8)
 
@@ -140,8 +144,8 @@ def pack_mask(present: np.ndarray) -> np.ndarray:
 def unpack_mask(words: np.ndarray) -> np.ndarray:
     sh = words.shape[:-1]
     w = words.reshape(-1, 8, 1).astype(np.uint64)
-    bits = ((w >> np.arange(32, dtype=np.uint64)) & 1).astype(bool)
-    return bits.reshape(*sh, MINUTES)
+    bits = ((w >> np.arange(32, dtype=np.uint64)) & 1).astype(bool).reshape(-1, 256)
+    return bits[:, :MINUTES].reshape(*sh, MINUTES)
 
 
 def stack_fields(panel: Dict) -> np.ndarray:

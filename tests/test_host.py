@@ -1,0 +1,96 @@
+"""Host-side logic and the C-ABI surface (no GPU calls)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import mff_oracle as O
+from mff import _lib, catalog, synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "mff.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mff_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_catalogue_matches_oracle_and_reference_order():
+    assert catalog.NAMES == O.ORACLE_NAMES
+    assert len(catalog.NAMES) == 58
+    # reference def lines strictly increasing (catalogue follows file order)
+    lines = [catalog.REF_LINE[n] for n in catalog.NAMES]
+    assert lines == sorted(lines)
+    assert catalog.PDF_IDS == [42, 43, 44, 45, 46]
+
+
+def test_algorithmic_bytes():
+    assert catalog.algorithmic_bytes_per_stock_day(range(58)) == 5354
+    ids = catalog.resolve(["vol_return1min", "shape_skew", "shape_kurt"])
+    assert catalog.fields_for(ids) == [0, 3]
+    assert catalog.algorithmic_bytes_per_stock_day(ids) == 32 + 2 * 960 + 27
+
+
+def test_library_loads_and_exports_every_header_symbol():
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _lib.SIGNATURES, f"{n} declared in mff.h but not bound in _lib.py"
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (mff_\w+)", out))
+    assert set(names) <= exported
+
+
+def test_library_catalogue_and_errors_without_gpu():
+    lib = _lib.load()
+    assert lib.mff_num_factors() == 58
+    assert [lib.mff_factor_name(i).decode() for i in range(58)] == catalog.NAMES
+    assert lib.mff_factor_name(58) is None
+    # argument validation happens before any device work
+    rc = lib.mff_stage2(None, None, 1, 1, 1, 99, 1, None, None, None)
+    assert rc < 0 and b"N=99" in lib.mff_last_error()
+    with pytest.raises(_lib.MffError):
+        _lib.check(rc, "mff_stage2")
+    assert lib.mff_pdf_workspace_bytes(300, 1, 10) > 0
+
+
+def test_mask_roundtrip():
+    rng = np.random.default_rng(0)
+    pres = rng.random((3, 5, 240)) < 0.7
+    w = synth.pack_mask(pres)
+    assert w.shape == (3, 5, 8) and w.dtype == np.uint32
+    assert (synth.unpack_mask(w) == pres).all()
+    assert synth.pack_mask(np.ones((1, 240), bool))[0].tolist() == [0xFFFFFFFF] * 7 + [0xFFFF]
+
+
+def test_synth_deterministic_and_contract():
+    from mff.engine import validate_host_panel
+    a = synth.make_panel(20, 3, config=2, ragged=True)
+    b = synth.make_panel(20, 3, config=2, ragged=True)
+    for k in ("open", "close", "volume"):
+        assert np.array_equal(a[k], b[k], equal_nan=True)
+    assert (a["present"] == b["present"]).all()
+    validate_host_panel(a)
+    v = a["volume"][a["present"]]
+    assert (v == np.rint(v)).all() and v.max() <= 2 ** 24 and (v % 100 == 0).all()
+    assert np.isnan(a["close"][~a["present"]]).all()
+    bad = dict(a)
+    bad["volume"] = a["volume"].copy()
+    bad["volume"][a["present"]] += 0.5
+    with pytest.raises(ValueError):
+        validate_host_panel(bad)
+
+
+def test_edge_fixture_covers_every_case():
+    from golden.make_golden import EDGE_CASES, load
+    panel, z = load("panel_edge.npz")
+    assert panel["present"].shape[1] == len(EDGE_CASES)
+    st = z["state"]
+    assert (st == 0).any() and (st == 1).any() and (st == 2).any()
+    assert np.isnan(z["val"][st == 2]).any()
