@@ -1,0 +1,199 @@
+#!/usr/bin/env python
+"""bench.py — BASELINE.json headline: factor stock-days/s (whole node) + % of HBM roofline
+on 5,000 stocks x 240 min x 2,500 days.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Step = one pass of stage 1 (all 58 CICC factors, including the doc_pdf frame-wide rank
+and its cross-rank exchange) over the whole panel, inputs already resident in HBM.
+The panel (S stocks x D days) is sharded by stock over the ranks: total work is fixed,
+so "scaling" is "strong".  value = S*D*K / max-over-ranks(wall time of the K steps).
+
+roofline: the fused stage-1 kernel (k_stage1), algorithmic bytes per launch =
+5,354 B/stock-day (4,832 B OHLCV+mask in, 58 x 9 B out) x local stock-days,
+over its average duration from HIP events on its launch stream; peak 8.0 TB/s
+(MI355X_MICROARCH.md).  traffic: HBM bytes per launch from the committed rocprofv3 PMC
+passes (profiles/pmc_stage1.json, FETCH_SIZE doubled per the gfx950 correction), or null.
+
+cpu_baseline: the CPU oracle (oracle/mff_oracle.py, a numpy restatement of the reference
+cal_* functions) timed on this host, rank 0 at N=1, on a bounded sample of the same
+synthetic distribution, with day-frame tasks over a process pool like the reference's
+joblib Parallel(n_jobs=-1) (MinuteFrequentFactorCICC.py:85-94).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "replication-of-minute-frequency-factor_amd")
+sys.path.insert(0, PKG)
+
+METRIC = "factor stock-days/sec (whole node) + % of HBM roofline, 5000×240min×2500d"
+HBM_PEAK_GBS = 8000.0
+
+
+def _oracle_day(args):
+    panel, d = args
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import mff_oracle as O
+    from mff import synth
+    sub = synth.subpanel(panel, days=slice(d, d + 1))
+    O.oracle_stage1(sub)
+    return d
+
+
+def cpu_baseline(days: int, stocks: int, workers: int):
+    """Oracle over `days` day-frames of `stocks` stocks, one task per day (fork pool)."""
+    from mff import synth
+    panel = synth.make_panel(stocks, days, config=4)
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        list(pool.imap_unordered(_oracle_day, [(panel, d) for d in range(days)]))
+    dt = time.perf_counter() - t0
+    return {"value": days * stocks / dt, "unit": "stock-days/s", "cores": workers, "kind": "port",
+            "sample": f"{days} days x {stocks} stocks (all 58 factors, numpy oracle), "
+                      f"{workers} worker processes, one day frame per task; wall {dt:.2f} s"}
+
+
+def load_pmc(S_loc: int, D: int):
+    path = os.path.join(ROOT, "profiles", "pmc_stage1.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pmc = json.load(f)
+    if pmc.get("stocks") != S_loc or pmc.get("days") != D:
+        return None
+    return pmc.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--stocks", type=int, default=5000)
+    ap.add_argument("--days", type=int, default=2500)
+    ap.add_argument("--cpu-days", type=int, default=16)
+    ap.add_argument("--cpu-stocks", type=int, default=40)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+
+    # CPU baseline first, before anything touches the GPU (the pool forks).
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        workers = max(1, min(16, os.cpu_count() or 1, args.cpu_days))
+        cpu = cpu_baseline(args.cpu_days, args.cpu_stocks, workers)
+
+    import torch
+    from mff import catalog, dist, engine, synth
+
+    comm, local = dist.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    S, D = args.stocks, args.days
+    s0, s1 = dist.shard_bounds(S, world, rank)
+    S_loc = s1 - s0
+    bars, mask = synth.make_panel_device(S_loc, D, dev, config=4, seed_offset=rank)
+    panel = engine.DevicePanel(bars, mask)
+    torch.cuda.synchronize()
+
+    def step(events=None):
+        return engine.compute_factors(panel, comm=comm, events=events)
+
+    for _ in range(args.warmup):
+        out = step()
+        del out
+    torch.cuda.synchronize()
+    if comm is not None:
+        comm.barrier()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        out = step(evs[k])
+        del out
+    torch.cuda.synchronize()
+    if comm is not None:
+        comm.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if comm is not None:
+        comm.all_reduce_max(el)
+    elapsed = float(el.item())
+
+    k_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, len(evs))
+    ids = list(range(catalog.N_FACTORS))
+    bytes_launch = catalog.algorithmic_bytes_per_stock_day(ids) * S_loc * D
+    achieved = bytes_launch / (k_ms * 1e-3) / 1e9
+    traffic = load_pmc(S_loc, D)
+
+    extras = {}
+    if not args.no_extras:
+        val, state, _ = step()
+        torch.cuda.synchronize()
+        def timed(fn):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            r = fn()
+            torch.cuda.synchronize()
+            return (time.perf_counter() - t) * 1e3, r
+        extras["stage1_kernel_ms"] = round(k_ms, 3)
+        extras["step_ms_rank0"] = round(elapsed / args.steps * 1e3, 3)
+        ms, _ = timed(lambda: engine.rolling(val, state, 20, "z"))
+        extras["stage2_z20_all58_ms"] = round(ms, 3)
+        ms, _ = timed(lambda: engine.cross_section(val, state, "z", comm=comm))
+        extras["stage3_z_all58_ms"] = round(ms, 3)
+        ms, _ = timed(lambda: engine.cross_section(val[:4], state[:4], "rank", comm=comm))
+        extras["stage3_rank_4factors_ms"] = round(ms, 3)
+        del val, state
+
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": S * D * args.steps / elapsed,
+            "unit": "stock-days/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": f"c4: {S} stocks x 240 min x {D} days, all 58 CICC factors "
+                            f"(stage 1 incl. doc_pdf frame-wide rank)",
+                "stocks": S, "days": D, "minutes": 240, "factors": 58,
+                "parallelism": f"stock-sharded x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "k_stage1",
+                "bytes_per_launch": bytes_launch,
+                "avg_kernel_ms": round(k_ms, 3),
+            },
+            "cpu_baseline": cpu,
+            "extras": extras,
+        }
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -74,15 +74,16 @@ int mff_stage1(const float* open, const float* high, const float* low,
  * frame, every code).  Three device phases; between count and finalize a multi-GPU
  * caller sums `counts` over ranks (all-reduce), see INTEGRATION.md.
  * Each phase works on days [d0, d0+nd) of arrays laid out over all D days.
- *   sort:     queries of R ranks, float64 [R][5][D][S_loc] (NaN = none)
- *             -> q_sorted uint64 [nd][M], M = R*5*S_loc <= 32767 (total-order keys)
+ *   sort:     queries of R ranks, float64 [R][5][D][S_all] (NaN = none; each rank's
+ *             [5][D][S_loc] padded to S_all with NaN)
+ *             -> q_sorted uint64 [nd][M], M = R*5*S_all <= 32767 (total-order keys)
  *   count:    this rank's keys c_last/c_b against q_sorted
  *             -> counts uint32 [nd][M][2] (n_less, n_eq) over local keys
  *   finalize: own queries [5][D][S_loc] -> val/state rows pdf_rows[5] (host)
  * workspace: mff_pdf_workspace_bytes(S_loc, R, nd) bytes of device scratch.
  */
 size_t mff_pdf_workspace_bytes(int S_loc, int R, int nd);
-int mff_pdf_sort(const double* q_all, int R, int S_loc, int D, int d0, int nd,
+int mff_pdf_sort(const double* q_all, int R, int S_all, int D, int d0, int nd,
                  uint64_t* q_sorted, void* workspace, void* stream);
 int mff_pdf_count(const float* close, const uint32_t* valid, int S_loc, int D, int d0,
                   int nd, const uint64_t* q_sorted, int M, uint32_t* counts,
@@ -106,16 +107,17 @@ int mff_stage2(const double* val, const uint8_t* state, int rows, int D, int S,
  * state VALUE and non-NaN value.  No single reference function; closest semantics
  * Factor.py:99-105 (coverage), :163-186 (per-date Pearson / Spearman), :285-291 (qcut).
  * z-score, multi-GPU: mff_xs_moments per rank -> all-gather [R][rows][D][3] ->
- * mff_xs_zscore.  rank: all-gather values/states [R][rows][D][S_loc] -> mff_xs_rank.
+ * mff_xs_zscore.  rank: all-gather values/states [R][rows][D][S_all] (every rank's
+ * columns padded to S_all with ABSENT) -> mff_xs_rank.
  */
 int mff_xs_moments(const double* val, const uint8_t* state, int rows, int D, int S,
                    double* moments /* [rows][D][3]: n, mean, M2 */, void* stream);
 int mff_xs_zscore(const double* val, const uint8_t* state, int rows, int D, int S,
                   const double* moments_all, int R, double* out_val,
                   uint8_t* out_state, void* stream);
-size_t mff_xs_rank_workspace_bytes(int rows, int D, int S_loc, int R);
+size_t mff_xs_rank_workspace_bytes(int rows, int D, int S_all, int R);
 int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_loc,
-                const double* val_all, const uint8_t* state_all, int R,
+                const double* val_all, const uint8_t* state_all, int R, int S_all,
                 double* out_val, uint8_t* out_state, void* workspace, void* stream);
 
 #ifdef __cplusplus

@@ -128,15 +128,15 @@ struct XsLoader {
 
 __global__ __launch_bounds__(SORT_THREADS) void k_xs_rank(const double* val, const uint8_t* state, int rows,
                                                            int D, int S, const double* val_all,
-                                                           const uint8_t* state_all, int R, double* out_val,
-                                                           uint8_t* out_state, uint64_t* ws) {
+                                                           const uint8_t* state_all, int R, int S_all,
+                                                           double* out_val, uint8_t* out_state, uint64_t* ws) {
   __shared__ uint64_t sk[SORT_CAP];
-  const int M = R * S;
+  const int M = R * S_all;
   const size_t nseg = (size_t)rows * D;
   uint64_t* srt = ws + (size_t)blockIdx.x * 2 * M;
   uint64_t* tmp = srt + M;
   for (size_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-    XsLoader ld{val_all, state_all, nseg, (int)seg, S};
+    XsLoader ld{val_all, state_all, nseg, (int)seg, S_all};
     const uint64_t* sorted;
     if (M <= SORT_CAP) {
       int P = 1;
@@ -207,24 +207,24 @@ int mff_xs_zscore(const double* val, const uint8_t* state, int rows, int D, int 
   return 0;
 }
 
-size_t mff_xs_rank_workspace_bytes(int rows, int D, int S_loc, int R) {
+size_t mff_xs_rank_workspace_bytes(int rows, int D, int S_all, int R) {
   const long long nseg = (long long)rows * D;
   const long long g = nseg < XS_RANK_GRID ? nseg : XS_RANK_GRID;
-  const long long M = (long long)R * S_loc;
+  const long long M = (long long)R * S_all;
   return M <= SORT_CAP ? 256 : (size_t)(g * 2 * M * 8);
 }
 
 int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_loc, const double* val_all,
-                const uint8_t* state_all, int R, double* out_val, uint8_t* out_state, void* workspace,
-                void* stream) {
+                const uint8_t* state_all, int R, int S_all, double* out_val, uint8_t* out_state,
+                void* workspace, void* stream) {
   clear_error();
-  MFF_REQUIRE(rows > 0 && D > 0 && S_loc > 0 && R >= 1, "mff_xs_rank: bad sizes");
+  MFF_REQUIRE(rows > 0 && D > 0 && S_loc > 0 && R >= 1 && S_all >= S_loc, "mff_xs_rank: bad sizes");
   MFF_REQUIRE(val && state && val_all && state_all && out_val && out_state && workspace,
               "mff_xs_rank: NULL buffer");
   const long long nseg = (long long)rows * D;
   const int g = (int)(nseg < XS_RANK_GRID ? nseg : XS_RANK_GRID);
   hipLaunchKernelGGL(k_xs_rank, dim3(g), dim3(SORT_THREADS), 0, as_stream(stream), val, state, rows, D, S_loc,
-                     val_all, state_all, R, out_val, out_state, reinterpret_cast<uint64_t*>(workspace));
+                     val_all, state_all, R, S_all, out_val, out_state, reinterpret_cast<uint64_t*>(workspace));
   MFF_LAUNCH_CHECK();
   return 0;
 }

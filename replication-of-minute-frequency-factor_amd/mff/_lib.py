@@ -33,7 +33,7 @@ SIGNATURES = {
     "mff_xs_moments": (c_int, [P, P, c_int, c_int, c_int, P, P]),
     "mff_xs_zscore": (c_int, [P, P, c_int, c_int, c_int, P, c_int, P, P, P]),
     "mff_xs_rank_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
-    "mff_xs_rank": (c_int, [P, P, c_int, c_int, c_int, P, P, c_int, P, P, P, P]),
+    "mff_xs_rank": (c_int, [P, P, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P, P]),
 }
 
 _lock = threading.Lock()

@@ -81,9 +81,11 @@ def validate_host_panel(panel) -> None:
 
 
 def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, comm=None,
-                    pdf_day_batch: Optional[int] = None):
+                    pdf_day_batch: Optional[int] = None, events=None):
     """Stage 1 for the requested factors (default: all 58, reference order).
 
+    ``events``: optional (start, end) torch.cuda.Event pair recorded on the launch stream
+    around the fused stage-1 kernel alone (bench.py's roofline timing).
     Returns (val float64 [nf][D][S], state uint8 [nf][D][S], ids)."""
     lib = _lib.load()
     ids = catalog.resolve(names)
@@ -94,10 +96,14 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
     need_pdf = any(i in catalog.PDF_IDS for i in ids)
     pdfq = torch.empty((5, D, S), dtype=torch.float64, device=dev) if need_pdf else None
     b = panel.bars
+    if events is not None:
+        events[0].record()
     _lib.check(lib.mff_stage1(_lib.ptr(b[0]), _lib.ptr(b[1]), _lib.ptr(b[2]), _lib.ptr(b[3]),
                               _lib.ptr(b[4]), _lib.ptr(panel.mask), S, D,
                               _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
                               _lib.ptr(pdfq), _stream(dev)), "mff_stage1")
+    if events is not None:
+        events[1].record()
     if need_pdf:
         rows = [ids.index(i) if i in ids else -1 for i in catalog.PDF_IDS]
         pdf_ranks(panel, pdfq, rows, val, state, comm=comm, day_batch=pdf_day_batch)
@@ -111,8 +117,9 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, rows: List[int], val, stat
     D, S = panel.D, panel.S
     dev = panel.device
     R = 1 if comm is None else comm.world_size
-    q_all = pdfq if comm is None else comm.all_gather(pdfq)  # [R][5][D][S]
-    M = R * 5 * S
+    S_all = S if comm is None else _agreed_max(comm, S, dev)
+    q_all = pdfq if comm is None else comm.all_gather(_pad_last(pdfq, S_all, float("nan")))
+    M = R * 5 * S_all
     if M > PDF_MAX_QUERIES:
         raise _lib.MffError(f"doc_pdf: {M} queries per day exceed {PDF_MAX_QUERIES} "
                             f"(ranks*5*stocks); shard fewer stocks per day")
@@ -125,7 +132,7 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, rows: List[int], val, stat
         ws = torch.empty(lib.mff_pdf_workspace_bytes(S, R, nd), dtype=torch.uint8, device=dev)
         q_sorted = torch.empty((nd, M), dtype=torch.int64, device=dev)
         counts = torch.empty((nd, M, 2), dtype=torch.int32, device=dev)
-        _lib.check(lib.mff_pdf_sort(_lib.ptr(q_all), R, S, D, d0, nd, _lib.ptr(q_sorted),
+        _lib.check(lib.mff_pdf_sort(_lib.ptr(q_all), R, S_all, D, d0, nd, _lib.ptr(q_sorted),
                                     _lib.ptr(ws), st), "mff_pdf_sort")
         _lib.check(lib.mff_pdf_count(_lib.ptr(panel.bars[3]), _lib.ptr(panel.mask), S, D, d0, nd,
                                      _lib.ptr(q_sorted), M, _lib.ptr(counts), _lib.ptr(ws), st),
@@ -135,6 +142,21 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, rows: List[int], val, stat
         _lib.check(lib.mff_pdf_finalize(_lib.ptr(pdfq), _lib.ptr(q_sorted), _lib.ptr(counts), S, D,
                                         d0, nd, M, _lib.int_array(rows), _lib.ptr(val),
                                         _lib.ptr(state), st), "mff_pdf_finalize")
+
+
+def _agreed_max(comm, n: int, dev) -> int:
+    t = torch.tensor([n], dtype=torch.int64, device=dev)
+    comm.all_reduce_max(t)
+    return int(t.item())
+
+
+def _pad_last(t: torch.Tensor, n: int, fill) -> torch.Tensor:
+    """Pad the last (stock) axis to n with `fill` (uneven shards before an all-gather)."""
+    if t.shape[-1] == n:
+        return t
+    out = torch.full(tuple(t.shape[:-1]) + (n,), fill, dtype=t.dtype, device=t.device)
+    out[..., : t.shape[-1]] = t
+    return out
 
 
 def rolling(val: torch.Tensor, state: torch.Tensor, N: int, method: str):
@@ -169,12 +191,14 @@ def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None):
         _lib.check(lib.mff_xs_zscore(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(mom_all), R,
                                      _lib.ptr(ov), _lib.ptr(os_), st), "mff_xs_zscore")
     elif kind == "rank":
-        v_all = val if comm is None else comm.all_gather(val)
-        s_all = state if comm is None else comm.all_gather(state)
-        ws = torch.empty(lib.mff_xs_rank_workspace_bytes(rows, D, S, R), dtype=torch.uint8, device=dev)
+        S_all = S if comm is None else _agreed_max(comm, S, dev)
+        v_all = val if comm is None else comm.all_gather(_pad_last(val, S_all, 0.0))
+        s_all = state if comm is None else comm.all_gather(_pad_last(state, S_all, ABSENT))
+        ws = torch.empty(lib.mff_xs_rank_workspace_bytes(rows, D, S_all, R), dtype=torch.uint8,
+                         device=dev)
         _lib.check(lib.mff_xs_rank(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(v_all),
-                                   _lib.ptr(s_all), R, _lib.ptr(ov), _lib.ptr(os_), _lib.ptr(ws), st),
-                   "mff_xs_rank")
+                                   _lib.ptr(s_all), R, S_all, _lib.ptr(ov), _lib.ptr(os_),
+                                   _lib.ptr(ws), st), "mff_xs_rank")
     else:
         raise ValueError(kind)
     return ov, os_

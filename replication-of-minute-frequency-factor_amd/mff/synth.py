@@ -163,7 +163,7 @@ def subpanel(panel: Dict, stocks=None, days=None) -> Dict:
 
 
 def make_panel_device(S: int, D: int, device, config: int = 3, day_chunk: int = 50,
-                      ragged: bool = False):
+                      ragged: bool = False, seed_offset: int = 0):
     """Same distribution as :func:`make_panel`, generated on ``device`` with torch.
 
     Returns (bars float32 [5][D][S][240], mask int32 [D][S][8]).  Used only where the
@@ -171,7 +171,7 @@ def make_panel_device(S: int, D: int, device, config: int = 3, day_chunk: int = 
     import torch
 
     g = torch.Generator(device=device)
-    g.manual_seed(BASE_SEED + config)
+    g.manual_seed(BASE_SEED + config + 1000 * seed_offset)
     f64 = dict(device=device, dtype=torch.float64)
     bars = torch.empty((5, D, S, MINUTES), device=device, dtype=torch.float32)
     p_prev = torch.exp(torch.randn(S, generator=g, **f64) * 0.8 + np.log(15.0)).clamp(1.0, 500.0)
@@ -196,13 +196,14 @@ def make_panel_device(S: int, D: int, device, config: int = 3, day_chunk: int = 
                 bars[k, d] = x.to(torch.float32)
             p_prev = close[:, -1]
     mask = torch.full((D, S, 8), -1, device=device, dtype=torch.int32)
+    mask[..., 7] = 0xFFFF  # bars 224..239; bits 240..255 stay clear
     if ragged:
         # suspended stock-days (3 %) and random missing bars (0.5 %)
         sus = torch.rand((D, S), generator=g, device=device) < 0.03
-        mask[sus] = 0
-        miss = torch.rand((D, S, MINUTES), generator=g, device=device) < 0.005
-        bitsv = (~miss).view(D, S, 8, 32).to(torch.int64)
-        words = (bitsv << torch.arange(32, device=device, dtype=torch.int64)).sum(-1)
-        words = words.to(torch.int64).where(words < 2 ** 31, words - 2 ** 32).to(torch.int32)
-        mask = mask & words
+        keep = torch.rand((D, S, MINUTES), generator=g, device=device) >= 0.005
+        keep &= ~sus[..., None]
+        padded = torch.zeros((D, S, 256), dtype=torch.int64, device=device)
+        padded[..., :MINUTES] = keep.to(torch.int64)
+        words = (padded.view(D, S, 8, 32) << torch.arange(32, device=device, dtype=torch.int64)).sum(-1)
+        mask = torch.where(words >= 2 ** 31, words - 2 ** 32, words).to(torch.int32)
     return bars, mask
