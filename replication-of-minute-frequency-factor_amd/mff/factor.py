@@ -1,0 +1,403 @@
+"""`Factor` and `MinFreqFactor`: the reference's user surface (Factor.py,
+MinuteFrequentFactorCICC.py) over the HIP engine.
+
+Kept: constructor arguments, attribute names (factor_name, factor_exposure, IC, ICIR,
+rank_IC, rank_ICIR), method names and arguments, output column names, error messages
+and the incremental-update / atomic-persistence behaviour.  Changed: frames are pandas
+(pyarrow-backed float columns keep polars' null vs NaN) because polars is not part of
+this stack; the hard-coded Windows data paths (FA:49,70; MF:64,68) are defaults that
+environment variables (MFF_PV_PATH, MFF_EXPOSURE_DIR, MFF_KLINE_DIR) or arguments
+override.
+
+Device work:
+  cal_exposure_by_min_data(cal_xxx)  -> stage-1 kernel over day-file batches
+  cal_final_exposure(N, m, 'days')   -> stage-2 rolling kernel
+The evaluation methods (coverage, ic_test, group_test) run on the host.
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+import warnings
+from typing import Literal, Optional
+
+import numpy as np
+
+from . import catalog, frames
+
+_PV_PATH = os.environ.get("MFF_PV_PATH", r"D:\QuantData\Price_Volume.parquet")
+_EXPOSURE_DIR = os.environ.get("MFF_EXPOSURE_DIR", r"D:\QuantData\MinuteFreqFactor")
+_KLINE_DIR = os.environ.get("MFF_KLINE_DIR", r"D:\QuantData\KLine_cleaned")
+
+
+def _pd():
+    import pandas as pd
+    return pd
+
+
+def _plt():
+    try:
+        import matplotlib.pyplot as plt
+        return plt
+    except ImportError:
+        warnings.warn("matplotlib is not installed; plot_out ignored")
+        return None
+
+
+def _float_values(col):
+    """(values f64 with NaN for null, isnull mask)."""
+    pd = _pd()
+    if isinstance(col.dtype, pd.ArrowDtype):
+        arr = col.array._pa_array.combine_chunks()
+        isnull = np.asarray(arr.is_null().to_numpy(zero_copy_only=False), dtype=bool)
+        x = np.asarray(arr.fill_null(np.nan).to_numpy(zero_copy_only=False), dtype=np.float64)
+        return x, isnull
+    x = np.asarray(col.to_numpy(dtype=np.float64, na_value=np.nan))
+    return x, np.asarray(col.isna().to_numpy())
+
+
+class Factor:
+    """Factor.py:7-350."""
+
+    COLUMN_DICT = {  # CSMAR daily price-volume columns (Factor.py:32-47)
+        "Trddt": "date", "Stkcd": "code", "Opnprc": "open", "Hiprc": "high", "Loprc": "low",
+        "Clsprc": "close", "Dnshrtrd": "volume", "Dnvaltrd": "amount", "ChangeRatio": "pct_change",
+        "Dsmvosd": "cmc", "Dsmvtll": "tmc", "Adjprcwd": "close_adjust", "LimitDown": "limit_down",
+        "LimitUp": "limit_up",
+    }
+
+    def __init__(self, factor_name: str, factor_exposure=None):
+        self.factor_name = factor_name
+        self.factor_exposure = factor_exposure
+        self.IC = None
+        self.ICIR = None
+        self.rank_IC = None
+        self.rank_ICIR = None
+
+    # ------------------------------------------------------------------ IO
+    @staticmethod
+    def _read_daily_pv_data(column_need=None, path: Optional[str] = None):
+        """Factor.py:21-62: CSMAR daily PV parquet, columns renamed, Trddt parsed."""
+        import pyarrow.parquet as pq
+
+        pd = _pd()
+        df = pq.read_table(path or _PV_PATH).to_pandas()
+        df = df.rename(columns=Factor.COLUMN_DICT)
+        df["date"] = pd.to_datetime(df["date"], format="%Y-%m-%d").dt.date
+        if column_need is None:
+            column_need = list(Factor.COLUMN_DICT.values())
+        return df[[c for c in column_need if c in df.columns]]
+
+    def to_parquet(self, path: str = None):
+        """Factor.py:64-90: write through a temp file in the target dir, then rename."""
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+
+        if path is None:
+            path = _EXPOSURE_DIR
+        if not path.endswith(".parquet"):
+            path = os.path.join(path, f"{self.factor_name}.parquet")
+        temp_dir = os.path.dirname(path) or "."
+        with tempfile.NamedTemporaryFile(dir=temp_dir, delete=False, suffix=".parquet") as tmp:
+            temp_path = tmp.name
+        try:
+            pq.write_table(pa.Table.from_pandas(self.factor_exposure, preserve_index=False), temp_path)
+            os.replace(temp_path, path)
+        except Exception:
+            if os.path.exists(temp_path):
+                os.remove(temp_path)
+            raise
+
+    # ------------------------------------------------------------------ evaluation
+    def _valid_exposure(self):
+        """filter(~is_nan()) (FA:100-101, 167-168): drops NaN and null rows."""
+        df = self.factor_exposure
+        x, isnull = _float_values(df[self.factor_name])
+        keep = ~isnull & ~np.isnan(x)
+        out = df.loc[keep, ["code", "date"]].copy()
+        out[self.factor_name] = x[keep]
+        return out
+
+    def coverage(self, plot_out=True, return_df=False):
+        """Factor.py:92-125: per-date count of non-NaN exposures."""
+        v = self._valid_exposure()
+        cov = v.groupby("date")[self.factor_name].count().sort_index().reset_index()
+        if plot_out:
+            plt = _plt()
+            if plt is not None:
+                plt.figure(figsize=(12, 8))
+                plt.bar(cov["date"], cov[self.factor_name], color="tab:blue", alpha=0.6,
+                        label=f"{self.factor_name} coverage")
+                plt.xticks(rotation=45)
+                plt.grid(True, linestyle="--", alpha=0.7)
+                plt.legend(loc="best")
+                plt.title("coverage plot")
+                plt.tight_layout()
+                plt.show()
+        return cov if return_df else None
+
+    @staticmethod
+    def _future_return(pv, future_days: int):
+        """FA:142-162: exp(rolling_sum(log(1+pct), N, min_samples=N)) - 1, shifted -N,
+        per code in date order."""
+        pv = pv.sort_values(["code", "date"]).reset_index(drop=True)
+        lg = np.log(pv["pct_change"].astype(float) + 1.0)
+        roll = lg.groupby(pv["code"]).transform(
+            lambda s: s.rolling(future_days, min_periods=future_days).sum())
+        rc = np.exp(roll) - 1.0
+        fut = rc.groupby(pv["code"]).shift(-future_days)
+        return pv[["code", "date"]].assign(future_return=fut.to_numpy())
+
+    def ic_test(self, future_days: int = 5, plot_out: bool = True, plot_variable: str = "IC",
+                return_df: bool = False, pv_data=None):
+        """Factor.py:127-229: per-date Pearson (IC) and Spearman (rank_IC) of the exposure
+        with the future N-day compounded return; IC/ICIR/rank_IC/rank_ICIR."""
+        pd = _pd()
+        pv = pv_data if pv_data is not None else self._read_daily_pv_data(["code", "date", "pct_change"])
+        fut = self._future_return(pv, future_days)
+        df = self._valid_exposure().merge(fut, on=["code", "date"], how="left")
+        rows = []
+        for date, g in df.groupby("date", sort=True):
+            g = g.dropna(subset=[self.factor_name, "future_return"])
+            x, y = g[self.factor_name].to_numpy(), g["future_return"].to_numpy()
+            ic = _pearson(x, y)
+            ric = _pearson(_avg_rank(x), _avg_rank(y)) if x.size else np.nan
+            rows.append((date, ic, ric))
+        ic_df = pd.DataFrame(rows, columns=["date", "IC", "rank_IC"])
+        ic_df = ic_df[~ic_df["IC"].isna()].sort_values("date").reset_index(drop=True)
+        self.IC = float(ic_df["IC"].mean())
+        self.rank_IC = float(ic_df["rank_IC"].mean())
+        self.ICIR = self.IC / float(ic_df["IC"].std())
+        self.rank_ICIR = self.rank_IC / float(ic_df["rank_IC"].std())
+        if plot_out:
+            plt = _plt()
+            if plt is not None:
+                fig, ax1 = plt.subplots(figsize=(12, 6))
+                ax1.bar(ic_df["date"], ic_df[plot_variable], color="tab:blue", alpha=0.6, width=1.0)
+                ax2 = ax1.twinx()
+                ax2.plot(ic_df["date"], ic_df[plot_variable].cumsum(), color="tab:red",
+                         linewidth=2.0, label=f"cum {plot_variable}")
+                plt.title(f"{plot_variable} plot")
+                plt.tight_layout()
+                plt.show()
+        return ic_df if return_df else None
+
+    def group_test(self, frequency: Literal["weekly", "monthly", "quarterly", "yearly"] = "monthly",
+                   weight_param: Literal["tmc", "cmc", None] = None, group_num: int = 5,
+                   plot_out: bool = True, return_df: bool = False, pv_data=None):
+        """Factor.py:231-350: per-date qcut into `group_num` groups, per-period compounding,
+        one-period lag, equal or cap-weighted group returns."""
+        pd = _pd()
+        freq = {"weekly": "W-SUN", "monthly": "M", "quarterly": "Q", "yearly": "Y"}[frequency]
+        pv = pv_data if pv_data is not None else self._read_daily_pv_data(
+            ["code", "date", "pct_change", "tmc", "cmc"])
+        ex = self.factor_exposure[["code", "date", self.factor_name]].copy()
+        ex[self.factor_name], _ = _float_values(ex[self.factor_name])
+        df = ex.merge(pv, on=["code", "date"], how="left")
+        labels = [f"group_{i + 1}" for i in range(group_num)]
+
+        def qc(s):
+            try:
+                return pd.qcut(s, group_num, labels=labels, duplicates="raise").astype(object)
+            except ValueError:
+                b = pd.qcut(s, group_num, labels=False, duplicates="drop")
+                return b.map(lambda i: None if pd.isna(i) else labels[int(i)])
+        df["group"] = df.groupby("date")[self.factor_name].transform(qc)
+        df["period"] = pd.to_datetime(df["date"]).dt.to_period(freq)
+        df = df.sort_values(["code", "date"])
+        agg = df.groupby(["code", "period"]).agg(
+            pct_change=("pct_change", lambda s: float(np.prod(1.0 + s.astype(float))) - 1.0),
+            group=("group", "last"), tmc=("tmc", "last") if "tmc" in df else ("pct_change", "last"),
+            cmc=("cmc", "last") if "cmc" in df else ("pct_change", "last")).reset_index()
+        agg["date"] = (agg["period"].dt.end_time.dt.normalize() + pd.Timedelta(days=1)).dt.date
+        agg = agg.sort_values(["date", "group"])
+        for c in ("group", "tmc", "cmc"):
+            agg[c] = agg.groupby("code")[c].shift(1)
+        agg = agg[~agg["group"].isna()]
+
+        def wmean(g):
+            if weight_param is None:
+                return g["pct_change"].mean()
+            w = g[weight_param].astype(float)
+            return float((g["pct_change"] * w).sum() / w.sum()) if w.sum() != 0 else 0.0
+        group_df = agg.groupby(["date", "group"]).apply(wmean, include_groups=False).rename("pct_change").reset_index()
+        group_df = group_df.sort_values(["date", "group"]).reset_index(drop=True)
+        if plot_out:
+            plt = _plt()
+            if plt is not None:
+                plt.figure(figsize=(12, 8))
+                for grp, g in group_df.groupby("group"):
+                    plt.plot(g["date"], (g["pct_change"] + 1).cumprod(), label=grp, linewidth=2)
+                plt.legend(loc="best")
+                plt.title("group return", fontsize=16)
+                plt.tight_layout()
+                plt.show()
+        return group_df if return_df else None
+
+
+def _avg_rank(x):
+    order = np.argsort(x, kind="stable")
+    sx = x[order]
+    r = np.empty(x.size)
+    i = 0
+    while i < x.size:
+        j = i
+        while j + 1 < x.size and sx[j + 1] == sx[i]:
+            j += 1
+        r[order[i:j + 1]] = (i + j + 2) / 2.0
+        i = j + 1
+    return r
+
+
+def _pearson(x, y):
+    if x.size < 2:
+        return np.nan
+    dx, dy = x - x.mean(), y - y.mean()
+    den = np.sqrt((dx * dx).sum() * (dy * dy).sum())
+    return float((dx * dy).sum() / den) if den != 0 else np.nan
+
+
+class MinFreqFactor(Factor):
+    """MinuteFrequentFactorCICC.py:8-245."""
+
+    def __init__(self, factor_name, factor_exposure=None):
+        super().__init__(factor_name, factor_exposure)
+
+    @staticmethod
+    def _read_day_file(path):
+        import pyarrow.parquet as pq
+        return pq.read_table(path)
+
+    @staticmethod
+    def _process_single_file(file_name, folder_path, calculate_method):
+        """MF:17-25: a host callable on one day file; errors print and skip the day."""
+        try:
+            file_path = os.path.join(folder_path, file_name)
+            return calculate_method(MinFreqFactor._read_day_file(file_path).to_pandas())
+        except Exception as e:
+            print(f"处理文件 {file_name} 时出错: {str(e)}")
+            return None
+
+    @staticmethod
+    def _read_exposure(factor_name: str, path: Optional[str], default_path: str):
+        """MF:27-48."""
+        import pyarrow.parquet as pq
+
+        if path is None:
+            path = default_path
+        if path.endswith(".parquet"):
+            return pq.read_table(path).to_pandas(types_mapper=_arrow_float_mapper)
+        if os.path.isdir(path) and f"{factor_name}.parquet" in os.listdir(path):
+            return pq.read_table(os.path.join(path, f"{factor_name}.parquet")).to_pandas(
+                types_mapper=_arrow_float_mapper)
+        return None
+
+    def cal_exposure_by_min_data(self, calculate_method, path: str = None, n_jobs: int = None,
+                                 folder_path: Optional[str] = None, batch_days: int = 64,
+                                 device=None):
+        """MF:50-112: compute the exposure from per-day minute files, updating an
+        existing exposure incrementally (only dates after its max date).
+
+        `calculate_method` is one of the mff ``cal_*`` functions (or a factor name): the
+        day files are read in batches of `batch_days`, turned into one dense panel and
+        run through the stage-1 kernel.  Any other callable runs per file on the host
+        exactly as the reference does (joblib process pool, errors print and skip)."""
+        pd = _pd()
+        factor_exposure = self._read_exposure(
+            factor_name=self.factor_name,
+            default_path=os.path.join(_EXPOSURE_DIR, "CICC Factor"), path=path)
+        folder_path = folder_path or _KLINE_DIR
+        file_names = sorted(f for f in os.listdir(folder_path) if f.endswith(".parquet"))
+        index = pd.DataFrame({"file_name": file_names})
+        index["date"] = pd.to_datetime(index["file_name"].str[:8], format="%Y%m%d").dt.date
+        if factor_exposure is not None:  # MF:79-81
+            end_date = max(frames._as_date(x) for x in factor_exposure["date"])
+            index = index[index["date"] > end_date]
+
+        name = getattr(calculate_method, "_mff_factor", None)
+        if isinstance(calculate_method, str):
+            name = calculate_method[4:] if calculate_method.startswith("cal_") else calculate_method
+        valid = []
+        if len(index) > 0:
+            if name is not None and name in catalog.ID:
+                valid = self._gpu_batches(index["file_name"].tolist(), folder_path, name,
+                                          batch_days, device)
+            else:
+                from joblib import Parallel, delayed
+
+                results = Parallel(n_jobs=-1 if n_jobs is None else n_jobs)(
+                    delayed(self._process_single_file)(f, folder_path, calculate_method)
+                    for f in index["file_name"])
+                valid = [r for r in results if r is not None]
+
+        if factor_exposure is None:
+            self.factor_exposure = _sort(pd.concat(valid, ignore_index=True)) if valid else None
+        elif valid:
+            self.factor_exposure = _sort(pd.concat([factor_exposure] + valid, ignore_index=True))
+        else:
+            self.factor_exposure = factor_exposure
+
+    def _gpu_batches(self, files, folder_path, name, batch_days, device):
+        import pyarrow as pa
+
+        from .factors import compute_long
+
+        out = []
+        for b0 in range(0, len(files), batch_days):
+            tables = []
+            for f in files[b0:b0 + batch_days]:
+                try:
+                    tables.append(self._read_day_file(os.path.join(folder_path, f)))
+                except Exception as e:  # MF:23-25: report and skip the day
+                    print(f"处理文件 {f} 时出错: {str(e)}")
+            if not tables:
+                continue
+            res = compute_long(pa.concat_tables(tables, promote_options="default"), [name], device)
+            out.append(res[name])
+        return out
+
+    def cal_final_exposure(self, frequency, method: str, mode: str = "calendar", pool="full"):
+        """MF:114-245.  mode='days': per-code rolling over present rows on the GPU
+        (stage 2).  mode='calendar': the reference raises inside polars here
+        (group_by_dynamic without index_column, MF:145-178), so its semantics are
+        undefined; argument validation matches, then NotImplementedError."""
+        if mode == "calendar":
+            if frequency not in ("weekly", "monthly"):
+                raise ValueError(f"Unsupported frequency for calendar: {frequency}")
+            if pool != "full":
+                raise ValueError(f"不支持的股票池: {pool}")
+            if method not in ("o", "m", "z", "std"):
+                raise ValueError("Unknown method")
+            raise NotImplementedError(
+                "calendar resampling: the reference fails here (group_by_dynamic without "
+                "index_column, MinuteFrequentFactorCICC.py:145); use mode='days'")
+        if mode != "days":
+            raise ValueError(f"Unknown mode: {mode}")
+        if not isinstance(frequency, int):
+            raise ValueError(f"Unsupported frequency for days: {frequency}")
+        if method not in ("o", "m", "z", "std"):
+            raise ValueError("Unknown method")
+        import torch
+
+        from . import engine
+        from .factors import _device
+
+        name = f"{self.factor_name}_{frequency}_{method}"
+        val, state, codes, dates = frames.from_long(self.factor_exposure, self.factor_name)
+        dev = _device(None)
+        v = torch.from_numpy(val[None]).to(dev)
+        s = torch.from_numpy(state[None]).to(dev)
+        ov, os_ = engine.rolling(v, s, frequency, method)
+        torch.cuda.synchronize(dev)
+        return frames.to_long(ov[0].cpu().numpy(), os_[0].cpu().numpy(), codes, dates, name)
+
+
+def _arrow_float_mapper(t):
+    import pandas as pd
+    import pyarrow as pa
+
+    return pd.ArrowDtype(pa.float64()) if pa.types.is_floating(t) else None
+
+
+def _sort(df):
+    return df.sort_values(["date", "code"], kind="stable").reset_index(drop=True)

@@ -1,0 +1,158 @@
+"""Long <-> dense conversion at the drop-in boundary.
+
+The reference hands each `cal_*` a long day frame read from parquet
+(`pl.read_parquet(day file)`, MinuteFrequentFactorCICC.py:22) with columns
+code, date, time (HHMMSSmmm int), open, high, low, close, volume, and gets back rows
+[code, date, <name>] (absent rows for filtered stock-days, Float64 values that may be
+null or NaN).  The engine works on a dense [stock x day x 240-minute] panel; this module
+converts between the two.
+
+* Input frames may be pandas DataFrames, pyarrow Tables, dicts of arrays, or any object
+  with ``to_arrow()`` (e.g. a polars DataFrame, when polars is installed).
+* Bars must sit on the 240-bar grid 09:30-11:29, 13:00-14:59 (start-labelled, the grid
+  the reference's time filters assume: CM:18,33,69,84 and minute_in_trade CM:98-106);
+  anything else raises ValueError, as do duplicate (code, date, time) rows.
+* Rows are taken in (code, time) order, the frame order the reference relies on (C4).
+* Output values use pandas' pyarrow-backed float64 so polars null (pd.NA) and NaN stay
+  distinct.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+MINUTES = 240
+FIELDS = ("open", "high", "low", "close", "volume")
+
+
+def time_to_minute(time: np.ndarray) -> np.ndarray:
+    """HHMMSSmmm -> minute index 0..239, -1 when off the grid."""
+    t = np.asarray(time, dtype=np.int64)
+    hh, mm, rest = t // 10000000, (t // 100000) % 100, t % 100000
+    clock = hh * 60 + mm
+    m = np.where(clock < 720, clock - 570, clock - 660)
+    ok = (rest == 0) & (((clock >= 570) & (clock < 690)) | ((clock >= 780) & (clock < 900)))
+    return np.where(ok, m, -1)
+
+
+def minute_to_time(m: np.ndarray) -> np.ndarray:
+    m = np.asarray(m, dtype=np.int64)
+    clock = np.where(m < 120, 570 + m, 780 + (m - 120))
+    return (clock // 60) * 10000000 + (clock % 60) * 100000
+
+
+def _columns(df) -> Dict[str, np.ndarray]:
+    if hasattr(df, "to_arrow") and not hasattr(df, "to_pandas_dtype"):
+        df = df.to_arrow()
+    try:
+        import pyarrow as pa
+        if isinstance(df, pa.Table):
+            return {n: df.column(n).to_numpy(zero_copy_only=False) for n in df.column_names}
+    except ImportError:  # pragma: no cover
+        pass
+    if isinstance(df, dict):
+        return {k: np.asarray(v) for k, v in df.items()}
+    return {c: df[c].to_numpy() for c in df.columns}
+
+
+def _as_date(x):
+    if isinstance(x, _dt.datetime):
+        return x.date()
+    if isinstance(x, _dt.date):
+        return x
+    if isinstance(x, np.datetime64):
+        return x.astype("datetime64[D]").astype(object)
+    if hasattr(x, "date"):
+        return x.date()
+    if isinstance(x, str):
+        return _dt.date.fromisoformat(x[:10])
+    return x
+
+
+def to_dense(df, codes: Sequence[str] | None = None) -> Dict:
+    """Long frame -> host panel dict (see mff.synth): float32 planes [D][S][240], present
+    mask, sorted codes and dates."""
+    cols = _columns(df)
+    for k in ("code", "date", "time") + FIELDS:
+        if k not in cols:
+            raise ValueError(f"missing column {k!r}")
+    code = np.asarray(cols["code"]).astype(str)
+    date = np.array([_as_date(x) for x in cols["date"]], dtype=object)
+    minute = time_to_minute(cols["time"])
+    if (minute < 0).any():
+        bad = np.asarray(cols["time"])[minute < 0][:5]
+        raise ValueError(f"bars off the 240-minute grid (time={bad.tolist()})")
+    ucodes = sorted(set(code.tolist())) if codes is None else list(codes)
+    udates = sorted(set(date.tolist()))
+    ci = {c: i for i, c in enumerate(ucodes)}
+    di = {d: i for i, d in enumerate(udates)}
+    s = np.fromiter((ci[c] for c in code), dtype=np.int64, count=code.size)
+    d = np.fromiter((di[x] for x in date), dtype=np.int64, count=date.size)
+    D, S = len(udates), len(ucodes)
+    flat = (d * S + s) * MINUTES + minute
+    if np.unique(flat).size != flat.size:
+        raise ValueError("duplicate (code, date, time) rows")
+    panel = {}
+    for k in FIELDS:
+        arr = np.full(D * S * MINUTES, np.nan, dtype=np.float32)
+        arr[flat] = np.asarray(cols[k], dtype=np.float64).astype(np.float32)
+        panel[k] = arr.reshape(D, S, MINUTES)
+    pres = np.zeros(D * S * MINUTES, dtype=bool)
+    pres[flat] = True
+    panel["present"] = pres.reshape(D, S, MINUTES)
+    panel["codes"] = ucodes
+    panel["dates"] = udates
+    return panel
+
+
+def to_long(val: np.ndarray, state: np.ndarray, codes: Sequence[str], dates: Sequence,
+            name: str, first: str = "code"):
+    """Dense [D][S] (val, state) -> pandas frame [code, date, name] (or [date, code, name]
+    when first='date'), rows for non-ABSENT entries, sorted by (date, code) as the
+    reference driver does (MF:100)."""
+    import pandas as pd
+    import pyarrow as pa
+
+    state = np.asarray(state)
+    d_idx, s_idx = np.nonzero(state != 0)
+    vals = np.asarray(val)[d_idx, s_idx]
+    null = state[d_idx, s_idx] == 1
+    arr = pa.array(vals, type=pa.float64(), mask=null)
+    code_col = np.asarray(codes, dtype=object)[s_idx]
+    date_col = np.asarray(dates, dtype=object)[d_idx]
+    data = {"code": code_col, "date": date_col}
+    out = pd.DataFrame(data if first == "code" else {"date": date_col, "code": code_col})
+    out[name] = pd.array(arr, dtype=pd.ArrowDtype(pa.float64()))
+    return out.reset_index(drop=True)
+
+
+def from_long(df, name: str, codes: Sequence[str] | None = None,
+              dates: Sequence | None = None):
+    """Long exposure frame [code, date, name] -> dense (val, state, codes, dates)."""
+    import pandas as pd
+
+    code = df["code"].astype(str).to_numpy()
+    date = np.array([_as_date(x) for x in df["date"]], dtype=object)
+    ucodes = sorted(set(code.tolist())) if codes is None else list(codes)
+    udates = sorted(set(date.tolist())) if dates is None else list(dates)
+    ci = {c: i for i, c in enumerate(ucodes)}
+    di = {d: i for i, d in enumerate(udates)}
+    D, S = len(udates), len(ucodes)
+    val = np.zeros((D, S), dtype=np.float64)
+    state = np.zeros((D, S), dtype=np.uint8)
+    col = df[name]
+    if isinstance(col.dtype, pd.ArrowDtype):  # null and NaN kept apart
+        arr = col.array._pa_array.combine_chunks()
+        isnull = np.asarray(arr.is_null().to_numpy(zero_copy_only=False), dtype=bool)
+        x = np.asarray(arr.fill_null(0.0).to_numpy(zero_copy_only=False), dtype=np.float64)
+    else:  # numpy columns: None / pd.NA are nulls, NaN is a value
+        obj = col.to_numpy(dtype=object)
+        isnull = np.array([v is None or v is pd.NA for v in obj], dtype=bool)
+        x = np.array([0.0 if n else float(v) for v, n in zip(obj, isnull)], dtype=np.float64)
+    s = np.fromiter((ci[c] for c in code), dtype=np.int64, count=code.size)
+    d = np.fromiter((di[v] for v in date), dtype=np.int64, count=date.size)
+    state[d, s] = np.where(isnull, 1, 2)
+    val[d, s] = np.where(isnull, 0.0, x)
+    return val, state, ucodes, udates

@@ -1,0 +1,108 @@
+"""GPU: the drop-in surface (cal_* on long frames, MinFreqFactor over day files,
+cal_final_exposure) and the stock-sharded multi-rank path, against the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+from parity import compare
+from test_frames_factor import long_frame, write_day_files
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def panel_and_oracle():
+    import mff_oracle as O
+    from mff import synth
+    panel = synth.make_panel(30, 3, config=21, ragged=True)
+    return panel, O.oracle_stage1(panel)
+
+
+def _dense(df, name, panel):
+    from mff import frames
+    v, s, _, _ = frames.from_long(df, name, codes=panel["codes"], dates=panel["dates"])
+    return v, s
+
+
+def test_cal_functions_on_long_frames(dev, panel_and_oracle):
+    """Every cal_* through the reference calling convention (one long multi-day frame)."""
+    import MinuteFrequentFactorCalculateMethodsCICC as CM
+    from mff import catalog
+    panel, (ov, os_) = panel_and_oracle
+    df = long_frame(panel)
+    res = CM.compute_long(df)
+    bad = []
+    for i, nm in enumerate(catalog.NAMES):
+        out = res[nm]
+        assert list(out.columns) == (["date", "code", nm] if nm == "shape_skratio" else ["code", "date", nm])
+        v, s = _dense(out, nm, panel)
+        bad += compare(v, s, ov[i], os_[i], nm)
+    assert not bad, "\n".join(bad)
+    one = CM.cal_mmt_pm(long_frame(panel, 0))  # single day, single factor
+    v, s = _dense(one, "mmt_pm", {"codes": panel["codes"], "dates": panel["dates"][:1]})
+    assert not compare(v, s, ov[0][:1], os_[0][:1], "mmt_pm")
+
+
+def test_min_freq_factor_gpu_batches_and_rolling(dev, panel_and_oracle, tmp_path):
+    import mff_oracle as O
+    from MinuteFrequentFactorCICC import MinFreqFactor
+    import MinuteFrequentFactorCalculateMethodsCICC as CM
+    from mff import catalog
+    panel, (ov, os_) = panel_and_oracle
+    write_day_files(panel, str(tmp_path))
+    f = MinFreqFactor("doc_pdf80")
+    f.cal_exposure_by_min_data(CM.cal_doc_pdf80, path=str(tmp_path / "exp"), folder_path=str(tmp_path),
+                               batch_days=2)
+    i = catalog.ID["doc_pdf80"]
+    v, s = _dense(f.factor_exposure, "doc_pdf80", panel)
+    assert not compare(v, s, ov[i], os_[i], "doc_pdf80", rtol=0, atol=0)
+    assert f.factor_exposure["date"].is_monotonic_increasing
+    j = catalog.ID["vol_return1min"]
+    g = MinFreqFactor("vol_return1min")
+    g.cal_exposure_by_min_data("vol_return1min", path=str(tmp_path / "exp"), folder_path=str(tmp_path))
+    for meth in ("m", "z", "std", "o"):
+        out = g.cal_final_exposure(2, meth, mode="days")
+        name = f"vol_return1min_2_{meth}"
+        v, s = _dense(out, name, panel)
+        rv, rs = O.oracle_stage2(ov[j], os_[j], 2, meth)
+        assert not compare(v, s, rv, rs, name)
+
+
+@pytest.mark.parametrize("R", [2, 3])
+def test_sharded_ranks_match_unsharded_oracle(dev, panel_and_oracle, R):
+    """R ranks (threads sharing the device, mff.dist.ThreadComm) each own a contiguous
+    (uneven) stock shard: doc_pdf's frame-wide rank and stage 3 go through the same
+    collectives as the RCCL path; the gathered result must equal the unsharded oracle."""
+    import mff_oracle as O
+    from mff import catalog, dist, engine, synth
+    panel, (ov, os_) = panel_and_oracle
+    S = len(panel["codes"])
+
+    def rank_fn(comm):
+        s0, s1 = dist.shard_bounds(S, comm.world_size, comm.rank)
+        dp = engine.DevicePanel.from_host(synth.subpanel(panel, stocks=slice(s0, s1)), dev)
+        val, state, _ = engine.compute_factors(dp, comm=comm)
+        zv, zs = engine.cross_section(val, state, "z", comm=comm)
+        rv, rs = engine.cross_section(val, state, "rank", comm=comm)
+        torch.cuda.synchronize()
+        return [t.cpu().numpy() for t in (val, state, zv, zs, rv, rs)]
+
+    parts = dist.run_threads(R, rank_fn)
+    cat = [np.concatenate([p[k] for p in parts], axis=2) for k in range(6)]
+    bad = []
+    for i, nm in enumerate(catalog.NAMES):
+        bad += compare(cat[0][i], cat[1][i], ov[i], os_[i], nm)
+        for kind, (v, s) in (("z", (cat[2], cat[3])), ("rank", (cat[4], cat[5]))):
+            xv, xs = O.oracle_stage3(ov[i], os_[i], kind)
+            bad += compare(v[i], s[i], xv, xs, f"{nm}/xs-{kind}", rtol=1e-6 if kind == "z" else 0.0,
+                           atol=1e-9 if kind == "z" else 0.0)
+    assert not bad, "\n".join(bad[:20])
