@@ -63,11 +63,16 @@ const char* mff_factor_name(int id);
  * factor_ids (host, nf entries): catalogue ids in output-row order.
  * pdf_query: float64 [5][D][S] workspace, required when any doc_pdf* id is requested
  * (the doc_pdf values are then produced by mff_pdf_* below), else may be NULL.
+ * workspace: mff_stage1_workspace_bytes(S, D) bytes of device scratch (the list of
+ * stock-days the exact general path finishes; zeroed by the call itself).
+ * Environment MFF_STAGE1_IMPL=w64 selects the wave-per-stock-day kernel for everything.
  */
+size_t mff_stage1_workspace_bytes(int S, int D);
 int mff_stage1(const float* open, const float* high, const float* low,
                const float* close, const float* volume, const uint32_t* valid,
                int S, int D, const int32_t* factor_ids /* host */, int nf,
-               double* val, uint8_t* state, double* pdf_query, void* stream);
+               double* val, uint8_t* state, double* pdf_query, void* workspace,
+               void* stream);
 
 /*
  * doc_pdf60..95 frame-wide rank (CM:1015-1017: `.rank()` over ALL rows of the day

@@ -33,21 +33,29 @@ struct S1Args {
   double* val;             // [nf][D][S]
   uint8_t* state;          // [nf][D][S]
   double* pdfq;            // [5][D][S] or null
+  const int* list;         // list mode: stock-day indices d*S+s to process (else null)
+  const int* list_count;   // list mode: number of entries (device)
   int S, D, nf;
   uint32_t fam;
   int8_t row[NF];          // output row of each factor id, -1 = not requested
 };
 
 struct Out {
-  double* sv;
+  double* sv;        // LDS staging [nf][TILE] (tile mode) or global val (direct mode)
   uint8_t* ss;
   const int8_t* row;
-  int slot;
+  int slot;          // tile mode: stock slot; direct mode: -1
+  size_t sd, plane;  // direct mode: d*S+s and D*S
   __device__ __forceinline__ void put(int f, double v, uint8_t st) const {
     const int r = row[f];
     if (r >= 0 && lane_id() == 0) {
-      sv[r * TILE + slot] = v;
-      ss[r * TILE + slot] = st;
+      if (slot >= 0) {
+        sv[r * TILE + slot] = v;
+        ss[r * TILE + slot] = st;
+      } else {
+        sv[(size_t)r * plane + sd] = v;
+        ss[(size_t)r * plane + sd] = st;
+      }
     }
   }
   __device__ __forceinline__ void val(int f, double v) const { put(f, v, MFF_STATE_VALUE); }
@@ -161,36 +169,17 @@ __device__ __forceinline__ double msum(const double (&x)[4], const bool (&f)[4])
   return wsum(s);
 }
 
-// ------------------------------------------------------------------ kernel
-__global__ __launch_bounds__(256) void k_stage1(S1Args a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int nf = a.nf;
-  double* sv = reinterpret_cast<double*>(smem);                        // [nf][TILE]
-  float* vscr = reinterpret_cast<float*>(smem + (size_t)nf * TILE * 8);  // [WPB][256]
-  uint8_t* ss = smem + (size_t)nf * TILE * 8 + WPB * 256 * 4;            // [nf][TILE]
-
-  const int ntile = (a.S + TILE - 1) / TILE;
-  const int d = blockIdx.x / ntile;
-  const int s0 = (blockIdx.x % ntile) * TILE;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+// ------------------------------------------------------------------ one stock-day
+// The whole stock-day in one wavefront (lane l = bars 4l..4l+3).  Used as the exact
+// general path: the tile kernel below, and the list-mode fallback of the 16-lane kernel
+// (mff_stage1g.hip) for stock-days whose closes are not on the 0.01 tick grid or whose
+// doc_pdf threshold is an exact tie.
+__device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, float* vw) {
   const int lane = lane_id();
   const bool lv = lane < 60;
   const uint32_t fam = a.fam;
-
-  for (int i = threadIdx.x; i < nf * TILE; i += blockDim.x) {
-    sv[i] = 0.0;
-    ss[i] = MFF_STATE_ABSENT;
-  }
-  __syncthreads();
-
-  float* vw = vscr + wave * 256;
-
-  for (int j = 0; j < SPW; ++j) {
-    const int slot = wave * SPW + j;
-    const int s = s0 + slot;
-    if (s >= a.S) break;
+  {
     const size_t sd = (size_t)d * a.S + s;
-    const Out out{sv, ss, a.row, slot};
 
     // ---- presence
     const uint32_t mw = lv ? a.mask[sd * 8 + (lane >> 3)] : 0u;
@@ -204,7 +193,7 @@ __global__ __launch_bounds__(256) void k_stage1(S1Args a) {
       if (a.pdfq && (fam & F_PDF)) {
         if (lane < 5) a.pdfq[(size_t)lane * a.D * a.S + sd] = qnan();
       }
-      continue;  // every output stays ABSENT
+      return;  // every output stays ABSENT
     }
     const int mf = first_of(B), ml = last_of(B);
 
@@ -728,6 +717,43 @@ __global__ __launch_bounds__(256) void k_stage1(S1Args a) {
     }
   }
 
+}
+
+__global__ __launch_bounds__(256) void k_stage1(S1Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int nf = a.nf;
+  double* sv = reinterpret_cast<double*>(smem);                        // [nf][TILE]
+  float* vscr = reinterpret_cast<float*>(smem + (size_t)nf * TILE * 8);  // [WPB][256]
+  uint8_t* ss = smem + (size_t)nf * TILE * 8 + WPB * 256 * 4;            // [nf][TILE]
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float* vw = vscr + wave * 256;
+
+  if (a.list) {  // list mode: grid-stride over the listed stock-days, direct writes
+    const int cnt = *a.list_count;
+    const int nw = gridDim.x * WPB;
+    for (int w = blockIdx.x * WPB + wave; w < cnt; w += nw) {
+      const int sd = __builtin_amdgcn_readfirstlane(a.list[w]);
+      const Out out{a.val, a.state, a.row, -1, (size_t)sd, (size_t)a.D * a.S};
+      stock_day_w64(a, sd / a.S, sd % a.S, out, vw);
+    }
+    return;
+  }
+
+  const int ntile = (a.S + TILE - 1) / TILE;
+  const int d = blockIdx.x / ntile;
+  const int s0 = (blockIdx.x % ntile) * TILE;
+  for (int i = threadIdx.x; i < nf * TILE; i += blockDim.x) {
+    sv[i] = 0.0;
+    ss[i] = MFF_STATE_ABSENT;
+  }
+  __syncthreads();
+  for (int j = 0; j < SPW; ++j) {
+    const int slot = wave * SPW + j;
+    const int s = s0 + slot;
+    if (s >= a.S) break;
+    const Out out{sv, ss, a.row, slot, 0, 0};
+    stock_day_w64(a, d, s, out, vw);
+  }
   __syncthreads();
   // ---- write the tile: rows of 64 consecutive stocks
   const size_t plane = (size_t)a.D * a.S;
@@ -744,43 +770,36 @@ __global__ __launch_bounds__(256) void k_stage1(S1Args a) {
 
 }  // namespace mff
 
-using namespace mff;
+namespace mff {
 
-extern "C" int mff_stage1(const float* open, const float* high, const float* low,
-                          const float* close, const float* volume, const uint32_t* valid,
-                          int S, int D, const int32_t* factor_ids, int nf, double* val,
-                          uint8_t* state, double* pdf_query, void* stream) {
-  clear_error();
-  MFF_REQUIRE(S > 0 && D > 0, "mff_stage1: S=%d D=%d must be positive", S, D);
-  MFF_REQUIRE(nf > 0 && nf <= NF, "mff_stage1: nf=%d out of range", nf);
-  MFF_REQUIRE(factor_ids != nullptr, "mff_stage1: factor_ids is NULL");
-  MFF_REQUIRE(valid && val && state, "mff_stage1: NULL device buffer");
+// wave-per-stock-day launcher: tile mode (list == nullptr) or list mode (fallback of the
+// 16-lane kernel; `fam_mask` restricts the families recomputed, `list_grid` blocks)
+int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, const int32_t* ids, int nf,
+               double* val, uint8_t* state, double* pdfq, const int* list, const int* list_count,
+               uint32_t fam_mask, int list_grid, hipStream_t st) {
   S1Args a;
   memset(&a, 0, sizeof(a));
-  a.fld[0] = open; a.fld[1] = high; a.fld[2] = low; a.fld[3] = close; a.fld[4] = volume;
-  a.mask = valid; a.val = val; a.state = state; a.pdfq = pdf_query;
+  for (int f = 0; f < 5; ++f) a.fld[f] = fld[f];
+  a.mask = valid; a.val = val; a.state = state; a.pdfq = pdfq;
+  a.list = list; a.list_count = list_count;
   a.S = S; a.D = D; a.nf = nf;
   for (int i = 0; i < NF; ++i) a.row[i] = -1;
   for (int r = 0; r < nf; ++r) {
-    const int id = factor_ids[r];
-    MFF_REQUIRE(id >= 0 && id < NF, "mff_stage1: factor id %d out of range", id);
-    MFF_REQUIRE(a.row[id] < 0, "mff_stage1: factor id %d requested twice", id);
-    a.row[id] = (int8_t)r;
-    a.fam |= kFactorFamily[id];
+    a.row[ids[r]] = (int8_t)r;
+    a.fam |= kFactorFamily[ids[r]];
   }
-  const float* need[5] = {open, high, low, close, volume};
-  const uint32_t use[5] = {F_SEG | F_ORD | F_MOMR | F_TRD, F_OLS | F_MOMH, F_OLS | F_MOMH,
-                           F_SEG | F_ORD | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD,
-                           F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD};
-  for (int f = 0; f < 5; ++f)
-    MFF_REQUIRE(!(a.fam & use[f]) || need[f] != nullptr, "mff_stage1: field plane %d required", f);
-  MFF_REQUIRE(!(a.fam & F_PDF) || pdf_query != nullptr,
-              "mff_stage1: doc_pdf requested but pdf_query is NULL");
-  const long long ntile = (S + TILE - 1) / TILE;
-  const long long nblk = ntile * (long long)D;
-  MFF_REQUIRE(nblk < (1ll << 31), "mff_stage1: grid too large (%lld blocks)", nblk);
+  a.fam &= fam_mask;
   const size_t lds = (size_t)nf * TILE * 8 + WPB * 256 * 4 + (size_t)nf * TILE;
-  hipLaunchKernelGGL(k_stage1, dim3((unsigned)nblk), dim3(256), lds, as_stream(stream), a);
+  long long nblk;
+  if (list) {
+    nblk = list_grid;
+  } else {
+    nblk = (long long)((S + TILE - 1) / TILE) * D;
+    MFF_REQUIRE(nblk < (1ll << 31), "mff_stage1: grid too large (%lld blocks)", nblk);
+  }
+  hipLaunchKernelGGL(k_stage1, dim3((unsigned)nblk), dim3(256), lds, st, a);
   MFF_LAUNCH_CHECK();
   return 0;
 }
+
+}  // namespace mff

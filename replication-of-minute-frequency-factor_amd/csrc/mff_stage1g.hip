@@ -1,0 +1,972 @@
+// mff_stage1g.hip — stage 1, 16 lanes per stock-day (the default path).
+//
+// A wave64 computes FOUR stock-days at once, one per DPP row of 16 lanes; lane gi of a
+// row owns bars 16*gi .. 16*gi+15 of every plane (four float4 loads per plane, all
+// planes in flight together).  Per-lane work is a straight loop over 16 bars with
+// carries (previous present bar, running prefix sums); everything that crosses lanes
+// is a 4-step DPP row operation (mff_group.h).  Each group keeps its 58 results spread
+// over its 16 lanes (factor f lives in lane f%16, register f/16) and the lanes store
+// them in parallel at the end (val[row][d][s]: the 16 stocks a block handles per step
+// are consecutive, so each 128-byte line is filled by one block within one step).
+//
+// Per family (reference lines CM:<n>, semantics S*/C* in DESIGN.md §4):
+//  SEG   bar tests + DPP broadcasts of session endpoints             CM:10-90
+//  OLS   exact shifted prefix sums; window start (t-50) fetched from lane gi-3
+//        (slot k-2) or gi-4 (k<2) with one bpermute per quantity; betas through LDS
+//        for the two-pass std                                          CM:93-376
+//  ORD   bitonic sort of 256 volume keys (16 per lane), thresholds by index CM:379-480
+//  MOM   one pass of shifted raw sums (shift = a member of the set, so identical
+//        values give exact zeros, C3); up/down subsets use min == max     CM:483-729
+//  SUM/TRD masked sums, one reciprocal 1/v per bar                     CM:732-831,1203-1406
+//  CORR  six Pearson sums, shifts = each variant's first pair           CM:834-932
+//  LVL/PDF close levels through an LDS histogram over the 0.01-tick index (exact:
+//        closes round-trip through the tick; distinct closes <-> distinct ticks);
+//        level volumes exact integers; doc_pdf threshold by the exact comparison
+//        20*cum > k*sum(v).  Stock-days whose closes are off the tick grid, span more
+//        than 256 ticks, hit an exact doc_pdf tie, or carry non-integral volume are
+//        appended to a list that the wave64 kernel (mff_stage1.hip) finishes.  CM:935-1138
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/mff.h"
+#include "mff_group.h"
+#include "mff_internal.h"
+
+namespace mff {
+
+int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, const int32_t* ids, int nf,
+               double* val, uint8_t* state, double* pdfq, const int* list, const int* list_count,
+               uint32_t fam_mask, int list_grid, hipStream_t st);
+
+namespace g16 {
+
+constexpr int NB = 256;  // tick bins per stock-day (LDS, 8 B each)
+
+struct GArgs {
+  const float* fld[5];
+  const uint32_t* mask;
+  double* val;
+  uint8_t* state;
+  double* pdfq;
+  int* fb_list;
+  int* fb_count;
+  int S, D;
+  uint32_t fam;
+  int8_t row[NF];
+};
+
+// ---- result registers: factor f of the group lives in lane f%16, register f/16
+struct Res {
+  double r[4];
+  uint32_t st;
+  __device__ __forceinline__ void put(int f, double x, uint32_t s) {
+    if (gi() == (f & 15)) {
+      const int q = f >> 4;
+      r[q] = x;
+      st = (st & ~(0xFFu << (8 * q))) | (s << (8 * q));
+    }
+  }
+  __device__ __forceinline__ void val(int f, double x) { put(f, x, MFF_STATE_VALUE); }
+  __device__ __forceinline__ void null(int f) { put(f, 0.0, MFF_STATE_NULL); }
+};
+
+__device__ __forceinline__ double gmin_d(double x) {
+  x = fmin(x, dpp_d<QP_XOR1>(x));
+  x = fmin(x, dpp_d<QP_XOR2>(x));
+  x = fmin(x, dpp_d<ROW_HALF_MIRROR>(x));
+  x = fmin(x, dpp_d<ROW_MIRROR>(x));
+  return x;
+}
+__device__ __forceinline__ double gmax_d(double x) {
+  x = fmax(x, dpp_d<QP_XOR1>(x));
+  x = fmax(x, dpp_d<QP_XOR2>(x));
+  x = fmax(x, dpp_d<ROW_HALF_MIRROR>(x));
+  x = fmax(x, dpp_d<ROW_MIRROR>(x));
+  return x;
+}
+
+// Moments from shifted raw sums S_j = sum (x - x0)^j over n values.
+struct RawMom {
+  double s1, s2, s3, s4;
+  int n;
+};
+// sample std (ddof=1); false -> null (n < 2).  `exact0`: the set is constant.
+__device__ __forceinline__ bool std1_raw(const RawMom& m, bool exact0, double& out) {
+  if (m.n < 2) return false;
+  if (exact0) {
+    out = 0.0;
+    return true;
+  }
+  const double v = (m.s2 - m.s1 * m.s1 / (double)m.n) / (double)(m.n - 1);
+  out = sqrt(v);
+  return true;
+}
+// central m2, m3, m4 (biased); exact zeros when s1..s4 are all zero
+__device__ __forceinline__ void central(const RawMom& m, double& m2, double& m3, double& m4) {
+  const double n = (double)m.n;
+  const double mu = m.s1 / n, a2 = m.s2 / n, a3 = m.s3 / n, a4 = m.s4 / n;
+  m2 = a2 - mu * mu;
+  m3 = a3 - 3.0 * mu * a2 + 2.0 * mu * mu * mu;
+  m4 = a4 - 4.0 * mu * a3 + 6.0 * mu * mu * a2 - 3.0 * mu * mu * mu * mu;
+}
+// S2 skew / kurtosis from raw sums (x0 a member, so a constant set gives m2 == 0)
+__device__ __forceinline__ void skew_kurt(const RawMom& m, double& sk, double& ku) {
+  double m2, m3, m4;
+  central(m, m2, m3, m4);
+  if (__builtin_isnan(m2) || m2 == 0.0) {
+    sk = ku = qnan();
+    return;
+  }
+  sk = (m.n == 2) ? 0.0 : m3 / (m2 * sqrt(m2));
+  ku = m4 / (m2 * m2) - 3.0;
+}
+// S3 Pearson from shifted sums over n pairs (shift = a member pair)
+__device__ __forceinline__ double pearson_raw(int n, double sx, double sy, double sxx, double syy, double sxy) {
+  if (n < 2) return qnan();
+  const double dn = (double)n;
+  const double vx = sxx - sx * sx / dn, vy = syy - sy * sy / dn;
+  if (!(vx != 0.0) || !(vy != 0.0)) return (__builtin_isnan(vx) || __builtin_isnan(vy)) ? qnan() : qnan();
+  return (sxy - sx * sy / dn) / sqrt(vx * vy);
+}
+
+// a register value the optimiser must treat as new (no instruction emitted)
+__device__ __forceinline__ void opaque(float& x) { asm("" : "+v"(x)); }
+__device__ __forceinline__ void opaque(double& x) { asm("" : "+v"(x)); }
+__device__ __forceinline__ void opaque(uint32_t& x) { asm("" : "+v"(x)); }
+// every section starts from fresh names for the planes it reads, so the f32->f64
+// conversions and quotients of one section are recomputed, not kept live (CSE) into
+// the next one
+template <typename T>
+__device__ __forceinline__ void fresh(T (&x)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) opaque(x[k]);
+}
+
+__device__ __forceinline__ void lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ascending bitonic sort of the group's 256 u32 keys (bar order e = 16*gi + k)
+__device__ __forceinline__ void gsort256(uint32_t (&a)[K]) {
+  const int g = gi();
+#pragma unroll
+  for (int size = 2; size <= 256; size <<= 1) {
+#pragma unroll
+    for (int j = size >> 1; j > 0; j >>= 1) {
+      if (j >= 16) {
+        const int lj = j >> 4;
+        const bool lower = (g & lj) == 0;
+        const bool up = ((16 * g) & size) == 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const uint32_t p = (uint32_t)__shfl_xor((int)a[k], lj, 16);
+          const uint32_t mn = min(a[k], p), mx = max(a[k], p);
+          a[k] = (lower == up) ? mn : mx;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if ((k & j) == 0) {
+            const bool up = ((16 * g + k) & size) == 0;
+            const uint32_t x = a[k], y = a[k | j];
+            const uint32_t mn = min(x, y), mx = max(x, y);
+            a[k] = up ? mn : mx;
+            a[k | j] = up ? mx : mn;
+          }
+        }
+      }
+    }
+  }
+}
+
+// Family groups, one kernel instantiation each.  A group's registers are allocated for
+// that group alone (one kernel holding all 58 factors needs > 256 VGPRs); the planes a
+// group reads are re-read by the next group, which costs nothing measurable here: the
+// stage is ALU/latency bound at ~1/50 of the HBM roofline.
+constexpr uint32_t G_HL = F_OLS | F_MOMH;                                  // high, low
+constexpr uint32_t G_RET = F_SEG | F_ORD | F_ORDV | F_MOMR | F_TRD;         // open, close, volume
+constexpr uint32_t G_CV = F_MOMV | F_SUMV | F_SUMC | F_CORR;               // close, volume
+constexpr uint32_t G_LVL = F_LVL | F_PDF;                                  // close, volume
+constexpr uint32_t kGroups[4] = {G_HL, G_RET, G_CV, G_LVL};
+
+template <uint32_t SET>
+__global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
+  __shared__ __attribute__((aligned(16))) uint64_t scratch[16][NB];  // 2 KB per group
+  const int lane = lane_id();
+  const int wave = threadIdx.x >> 6;
+  const int grp = lane >> 4;
+  const int g = gi();
+  const int gb = gbase();
+  uint64_t* scr = scratch[wave * 4 + grp];
+  double* scr_d = reinterpret_cast<double*>(scr);
+  const uint32_t fam = a.fam & SET;
+  const int ntile = (a.S + 63) / 64;
+  const int d = blockIdx.x / ntile;
+  const int s0 = (blockIdx.x % ntile) * 64;
+  const size_t plane = (size_t)a.D * a.S;
+
+  for (int it = 0; it < 4; ++it) {
+    const int s = s0 + it * 16 + wave * 4 + grp;
+    const bool act = s < a.S;
+    const size_t sd = (size_t)d * a.S + (act ? s : 0);
+    const bool ln = act && g < 15;  // lane holds bars
+
+    uint32_t pb = 0;
+    if (ln) {
+      const uint32_t w = a.mask[sd * 8 + (g >> 1)];
+      pb = (w >> (16 * (g & 1))) & 0xFFFFu;
+    }
+    const int n = gcount(pb);
+    Res R;
+    R.r[0] = R.r[1] = R.r[2] = R.r[3] = 0.0;
+    R.st = 0u;
+    double qv[5] = {qnan(), qnan(), qnan(), qnan(), qnan()};
+
+    if (n > 0) {
+      // ---------------------------------------------------------------- loads
+      float o[K], h[K], lo[K], c[K], v[K];
+      auto load = [&](int f, float (&x)[K], float dflt) {
+        if (ln) {
+          const float4* p4 = reinterpret_cast<const float4*>(a.fld[f] + sd * NBAR + 16 * g);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 t = p4[q];
+            x[4 * q + 0] = t.x; x[4 * q + 1] = t.y; x[4 * q + 2] = t.z; x[4 * q + 3] = t.w;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < K; ++k) x[k] = dflt;
+        }
+      };
+      const uint32_t needO = F_SEG | F_ORD | F_MOMR | F_TRD;
+      const uint32_t needHL = F_OLS | F_MOMH;
+      const uint32_t needC = F_SEG | F_ORD | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD;
+      const uint32_t needV = F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD;
+      auto sanitize = [&](float (&x)[K], float dflt) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) x[k] = ((pb >> k) & 1u) ? x[k] + 0.0f : dflt;
+      };
+      // phase A planes: high, low (OLS, MOMH); later phases load the others
+      if (fam & needHL) {
+        load(1, h, 1.0f);
+        load(2, lo, 1.0f);
+        sanitize(h, 1.0f);
+        sanitize(lo, 1.0f);
+      }
+      const int fb = gfirst(pb), lb = glast(pb);
+
+      // ================================================================ OLS CM:93-376
+      if (fam & F_OLS) {
+        const double x0a = (double)gval(lo, fb), y0a = (double)gval(h, fb);
+        const float ln0 = dpp_f<ROW_SHL + 1>(lo[0]), hn0 = dpp_f<ROW_SHL + 1>(h[0]);
+        const uint32_t pn0 = dpp_u<ROW_SHL + 1>(pb) & 1u;
+        // lane totals -> carry-in of the prefix sums
+        double tx = 0, ty = 0, txx = 0, tyy = 0, txy = 0, q15x = 0, q15y = 0, q15xx = 0, q15yy = 0, q15xy = 0;
+        uint32_t tpk = 0, q15pk = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const bool pk = (pb >> k) & 1u;
+          const bool pnx = (k < 15) ? ((pb >> (k + 1)) & 1u) : (pn0 != 0u);
+          const float lnx = (k < 15) ? lo[k + 1] : ln0, hnx = (k < 15) ? h[k + 1] : hn0;
+          const double dx = pk ? (double)lo[k] - x0a : 0.0, dy = pk ? (double)h[k] - y0a : 0.0;
+          const uint32_t pkv = (pk ? 1u : 0u) | ((pk && pnx && lo[k] != lnx) ? 0x100u : 0u) |
+                               ((pk && pnx && h[k] != hnx) ? 0x10000u : 0u);
+          tx += dx; ty += dy; txx += dx * dx; tyy += dy * dy; txy += dx * dy; tpk += pkv;
+          if (k == 15) { q15x = dx; q15y = dy; q15xx = dx * dx; q15yy = dy * dy; q15xy = dx * dy; q15pk = pkv; }
+        }
+        double Rx = gscan_excl(tx), Ry = gscan_excl(ty), Rxx = gscan_excl(txx), Ryy = gscan_excl(tyy),
+               Rxy = gscan_excl(txy);
+        uint32_t Rpk = gscan_excl_u(tpk);
+        // prefix at slots 14 / 15 of this lane (read by lane gi+4 for its k = 0 / 1)
+        const double E15x = Rx + tx, E15y = Ry + ty, E15xx = Rxx + txx, E15yy = Ryy + tyy, E15xy = Rxy + txy;
+        const uint32_t E15pk = Rpk + tpk;
+        // fresh SSA names for the second walk: otherwise the 16 per-bar deviations and
+        // their 80 products from the first walk stay live (CSE) and the kernel spills
+        double x0 = x0a, y0 = y0a;
+        opaque(x0);
+        opaque(y0);
+#pragma unroll
+        for (int k = 0; k < K; ++k) { opaque(lo[k]); opaque(h[k]); }
+        double H1x = 0, H1y = 0, H1xx = 0, H1yy = 0, H1xy = 0, H2x = 0, H2y = 0, H2xx = 0, H2yy = 0, H2xy = 0;
+        uint32_t H1pk = 0, H2pk = 0;
+        double sq = 0, scs = 0, scr = 0, bsum = 0, blast = 0;
+        int lastT = -1, wq = 0;
+        uint32_t wmask = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const bool pk = (pb >> k) & 1u;
+          const bool pnx = (k < 15) ? ((pb >> (k + 1)) & 1u) : (pn0 != 0u);
+          const float lnx = (k < 15) ? lo[k + 1] : ln0, hnx = (k < 15) ? h[k + 1] : hn0;
+          const double dx = pk ? (double)lo[k] - x0 : 0.0, dy = pk ? (double)h[k] - y0 : 0.0;
+          const uint32_t chx = (pk && pnx && lo[k] != lnx) ? 1u : 0u;
+          const uint32_t chy = (pk && pnx && h[k] != hnx) ? 1u : 0u;
+          Rx += dx; Ry += dy; Rxx += dx * dx; Ryy += dy * dy; Rxy += dx * dy;
+          Rpk += (pk ? 1u : 0u) | (chx << 8) | (chy << 16);
+          // prefix at t-50: lane gi-3 slot k-2 (its H2 now) or lane gi-4 slot 14/15
+          double bx, by, bxx, byy, bxy;
+          uint32_t bpk;
+          if (k >= 2) {
+            const int src = gb + (g >= 3 ? g - 3 : 0);
+            bx = bpermd(src, H2x); by = bpermd(src, H2y); bxx = bpermd(src, H2xx);
+            byy = bpermd(src, H2yy); bxy = bpermd(src, H2xy); bpk = bpermu(src, H2pk);
+            if (g < 3) { bx = by = bxx = byy = bxy = 0.0; bpk = 0u; }
+          } else {
+            const int src = gb + (g >= 4 ? g - 4 : 0);
+            const double ex = (k == 0) ? E15x - q15x : E15x, ey = (k == 0) ? E15y - q15y : E15y;
+            const double exx = (k == 0) ? E15xx - q15xx : E15xx, eyy = (k == 0) ? E15yy - q15yy : E15yy;
+            const double exy = (k == 0) ? E15xy - q15xy : E15xy;
+            const uint32_t epk = (k == 0) ? E15pk - q15pk : E15pk;
+            bx = bpermd(src, ex); by = bpermd(src, ey); bxx = bpermd(src, exx);
+            byy = bpermd(src, eyy); bxy = bpermd(src, exy); bpk = bpermu(src, epk);
+            if (g < 4) { bx = by = bxx = byy = bxy = 0.0; bpk = 0u; }
+          }
+          H2x = H1x; H2y = H1y; H2xx = H1xx; H2yy = H1yy; H2xy = H1xy; H2pk = H1pk;
+          H1x = Rx; H1y = Ry; H1xx = Rxx; H1yy = Ryy; H1xy = Rxy; H1pk = Rpk;
+          const int t = 16 * g + k;
+          const uint32_t cnt = (Rpk & 0xffu) - (bpk & 0xffu);
+          const uint32_t cxw = ((Rpk >> 8) & 0xffu) - ((bpk >> 8) & 0xffu) - chx;
+          const uint32_t cyw = ((Rpk >> 16) & 0xffu) - ((bpk >> 16) & 0xffu) - chy;
+          const bool okw = ln && t >= 49 && cnt == 50u;
+          if (okw) {
+            const double Sx = Rx - bx, Sy = Ry - by, Sxx = Rxx - bxx, Syy = Ryy - byy, Sxy = Rxy - bxy;
+            const bool cx = cxw == 0u, cy = cyw == 0u;
+            const double vx = cx ? 0.0 : (Sxx - Sx * Sx * 0.02) * 0.02;
+            const double vy = cy ? 0.0 : (Syy - Sy * Sy * 0.02) * 0.02;
+            const double cv = (cx || cy) ? 0.0 : (Sxy - Sx * Sy * 0.02) * 0.02;
+            double beta;
+            if (vx != 0.0) beta = cv / vx;
+            else beta = (y0 + Sy * 0.02) / (x0 + Sx * 0.02);  // mean_y / mean_x
+            const double prod = vx * vy;
+            if (prod != 0.0) {
+              const double ip = 1.0 / prod;
+              sq += sqrt(cv) * ip;           // cov**0.5 / (vx*vy)   CM:137
+              scs += cv * cv * ip;           // cov**2 / (vx*vy)     CM:212
+              scr += cv * sqrt(prod) * ip;   // cov / (vx*vy)**0.5   CM:261
+              ++wq;
+            }
+            scr_d[t] = beta;
+            bsum += beta;
+            blast = beta;
+            lastT = t;
+            wmask |= 1u << k;
+          }
+          // keep the 16 steps in order: hoisting the bpermutes keeps 16 prefixes live
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const int W = gcount(wmask);
+        if (W > 0) {
+          lds_fence();
+          const int fT = gfirst(wmask), lT = gmax_i(lastT);
+          const double b0 = scr_d[fT];
+          const double bl = bpermd(gb + (lT >> 4), blast);
+          double d1 = 0.0, d2 = 0.0;
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+            if ((wmask >> k) & 1u) {
+              const double dd = scr_d[16 * g + k] - b0;
+              d1 += dd;
+              d2 += dd * dd;
+            }
+          d1 = gsum(d1);
+          d2 = gsum(d2);
+          const int Wq = gsum_i(wq);
+          const double Sq = gsum(sq), Scs = gsum(scs), Scr = gsum(scr);
+          const double bmean = b0 + d1 / (double)W;
+          double bstd = 0.0;
+          const bool has_std = W >= 2;
+          if (has_std) bstd = sqrt((d2 - d1 * d1 / (double)W) / (double)(W - 1));
+          (void)bsum;
+          if (has_std && tot_ne(bstd, 0.0) && Wq > 0)
+            R.val(5, (Sq / (double)Wq) * (bl - bmean) / bstd);  // mmt_ols_qrs CM:156-171
+          else
+            R.val(5, 0.0);
+          R.val(6, Wq > 0 ? Scs / (double)Wq : 0.0);
+          R.val(7, Wq > 0 ? Scr / (double)Wq : 0.0);
+          R.val(8, bmean);
+          R.val(9, (has_std && tot_gt(bstd, 0.0)) ? (bl - bmean) / bstd : bmean);
+          lds_fence();
+        }
+      }
+
+      __builtin_amdgcn_sched_barrier(0);
+      // ================================================================ MOMH CM:499-515
+      if (fam & F_MOMH) {
+        fresh(h);
+        fresh(lo);
+
+        const double x0 = (double)gval(h, fb) / (double)gval(lo, fb);
+        double s1 = 0, s2 = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if ((pb >> k) & 1u) {
+            const double dd = (double)h[k] / (double)lo[k] - x0;
+            s1 += dd;
+            s2 += dd * dd;
+          }
+        RawMom m{gsum(s1), gsum(s2), 0, 0, n};
+        double sdv;
+        if (std1_raw(m, m.s1 == 0.0 && m.s2 == 0.0, sdv)) R.val(15, sdv); else R.null(15);
+      }
+
+      __builtin_amdgcn_sched_barrier(0);
+      // phase B/C planes: volume, close, open
+      double sumv = 0.0;
+      if (fam & needV) {
+        load(4, v, 0.0f);
+        sanitize(v, 0.0f);
+        double t = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) t += (double)v[k];
+        sumv = gsum(t);
+      }
+      if (fam & needC) {
+        load(3, c, 1.0f);
+        sanitize(c, 1.0f);
+      }
+      if (fam & needO) {
+        load(0, o, 1.0f);
+        sanitize(o, 1.0f);
+      }
+
+      // ================================================================ ORD / ORDV sort
+      float th50 = 0.f, th20 = 0.f, tb50 = 0.f;
+      if (fam & (F_ORD | F_ORDV)) {
+        fresh(v);
+
+        uint32_t key[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) key[k] = ((pb >> k) & 1u) ? fbits(v[k]) : 0xffffffffu;
+        gsort256(key);
+        auto kth = [&](int e) { return bitsf(bpermu(gb + (e >> 4), pick(key, e & 15))); };
+        th50 = kth(n >= 50 ? n - 50 : 0);  // top_k(50).min()   CM:391-396
+        th20 = kth(n >= 20 ? n - 20 : 0);  // top_k(20).min()
+        tb50 = kth(n >= 50 ? 49 : n - 1);  // bottom_k(50).max() CM:417-422
+        if (fam & F_ORDV) {
+          double t10 = 0.0, t5 = 0.0;
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const int e = 16 * g + k;
+            const double x = (double)bitsf(key[k]);
+            if (e < n && e >= n - 10) t10 += x;
+            if (e < n && e >= n - 5) t5 += x;
+          }
+          t10 = gsum(t10);
+          t5 = gsum(t5);
+          R.val(47, t10 / sumv);  // doc_vol10_ratio
+          R.val(48, t5 / sumv);   // doc_vol5_ratio
+          R.val(49, t5 / sumv);   // doc_vol50_ratio: top_k(5) [sic CM:1196]
+        }
+      }
+
+      // ================================================================ RET: MOMR + TRD + ORD products
+      if (fam & (F_MOMR | F_TRD | F_ORD)) {
+        fresh(c);
+        fresh(o);
+        fresh(v);
+
+        const double x0 = (double)gval(c, fb) / (double)gval(o, fb) - 1.0;  // first return
+        double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+        double u1 = 0, u2 = 0, umn = __builtin_inf(), umx = -__builtin_inf();
+        double w1 = 0, w2 = 0, wmn = __builtin_inf(), wmx = -__builtin_inf();
+        uint32_t upm = 0, dnm = 0;
+        double p50 = 1.0, p20 = 1.0, pb50 = 1.0;
+        double vT20 = 0, vT50 = 0, rT20 = 0, rT50 = 0, vH20 = 0, vH50 = 0, a20 = 0, n20 = 0, q20 = 0, a50 = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const bool pk = (pb >> k) & 1u;
+          const int m = 16 * g + k;
+          const double q = (double)c[k] / (double)o[k];  // close / open
+          const double r = q - 1.0;                       // close / open - 1
+          if (pk) {
+            const double dd = r - x0, d2 = dd * dd;
+            s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
+            if (tot_gt(r, 0.0)) { upm |= 1u << k; u1 += dd; u2 += d2; umn = fmin(umn, r); umx = fmax(umx, r); }
+            if (tot_lt(r, 0.0)) { dnm |= 1u << k; w1 += dd; w2 += d2; wmn = fmin(wmn, r); wmx = fmax(wmx, r); }
+            if (v[k] >= th50) p50 *= q;
+            if (v[k] >= th20) p20 *= q;
+            if (v[k] <= tb50) pb50 *= q;
+            const double vk = (double)v[k];
+            if (m >= 220) { vT20 += vk; rT20 += vk * r; }
+            if (m >= 190) { vT50 += vk; rT50 += vk * r; }
+            if (m <= 50) {
+              const double iw = 1.0 / vk;  // inf when v = 0: r/0 semantics
+              const double ta = r * iw;
+              vH50 += vk; a50 += ta;
+              if (m <= 20) {
+                vH20 += vk; a20 += ta;
+                n20 += (r < 0.0 ? -r : 0.0) * iw;
+                q20 += (r > 0.0 ? r : 0.0) * iw;
+              }
+            }
+          }
+        }
+        if (fam & F_MOMR) {
+          RawMom m{gsum(s1), gsum(s2), gsum(s3), gsum(s4), n};
+          double sdr;
+          const bool has_sdr = std1_raw(m, m.s1 == 0.0 && m.s2 == 0.0, sdr);
+          if (has_sdr) R.val(16, sdr); else R.null(16);  // vol_return1min
+          const int nu = gcount(upm), nd = gcount(dnm);
+          const double U1 = gsum(u1), U2 = gsum(u2), Umn = gmin_d(umn), Umx = gmax_d(umx);
+          const double D1 = gsum(w1), D2 = gsum(w2), Dmn = gmin_d(wmn), Dmx = gmax_d(wmx);
+          double sup = 0.0, sdn = 0.0;  // fill_null(0)
+          std1_raw(RawMom{U1, U2, 0, 0, nu}, Umn == Umx, sup);
+          std1_raw(RawMom{D1, D2, 0, 0, nd}, Dmn == Dmx, sdn);
+          R.val(17, sup);  // vol_upVol
+          R.val(19, sdn);  // vol_downVol
+          if (has_sdr) { R.val(18, sup / sdr); R.val(20, sdn / sdr); }
+          else { R.null(18); R.null(20); }
+          double sk, ku;
+          skew_kurt(m, sk, ku);
+          R.val(21, sk);
+          R.val(22, ku);
+          R.val(23, sk / ku);
+        }
+        if (fam & F_ORD) {
+          const double pbb = gprod(pb50) - 1.0;
+          R.val(10, gprod(p50) - 1.0);
+          R.val(11, pbb);
+          R.val(12, gprod(p20) - 1.0);
+          R.val(13, pbb);  // bottom_k(50) [sic CM:471]
+        }
+        if (fam & F_TRD) {
+          if (gany((pb & rmask(220, 239)) != 0u)) R.val(50, gsum(rT20) / (gsum(vT20) + 1.0));
+          if (gany((pb & rmask(190, 239)) != 0u)) {
+            double den = gsum(vT50);
+            if (den == 0.0) den = 1.0;
+            R.val(51, gsum(rT50) / den);
+          }
+          const int nh20 = gcount(pb & rmask(0, 20)), nh50 = gcount(pb & rmask(0, 50));
+          if (nh20 > 0) {
+            const double sH = gsum(vH20);
+            R.val(54, sH * gsum(a20) / (double)nh20);
+            R.val(56, sH * gsum(n20) / (double)nh20);
+            R.val(57, sH * gsum(q20) / (double)nh20);
+          }
+          if (nh50 > 0) R.val(55, gsum(vH50) * gsum(a50) / (double)nh50);
+        }
+      }
+
+      // ================================================================ SEG CM:10-90
+      if (fam & F_SEG) {
+        fresh(c);
+        fresh(o);
+
+        auto seg = [&](int f, int ma, int mb, float ca, float cb, float oa, float ob) {
+          const bool pa = gpres(pb, ma), pbb = gpres(pb, mb);
+          if (!pa && !pbb) return;
+          R.val(f, (double)(pbb ? cb : ca) / (double)(pa ? oa : ob));
+        };
+        seg(0, 120, 239, gvalc<120>(c), gvalc<239>(c), gvalc<120>(o), gvalc<239>(o));  // mmt_pm
+        seg(1, 210, 239, gvalc<210>(c), gvalc<239>(c), gvalc<210>(o), gvalc<239>(o));  // mmt_last30
+        seg(3, 0, 119, gvalc<0>(c), gvalc<119>(c), gvalc<0>(o), gvalc<119>(o));        // mmt_am
+        seg(4, 30, 209, gvalc<30>(c), gvalc<209>(c), gvalc<30>(o), gvalc<209>(o));     // mmt_between
+        // mmt_paratio CM:42-60, C1: g(PM) - g(AM); one session gives g - g
+        const uint32_t am = pb & rmask(0, 119), pm = pb & rmask(120, 239);
+        const int af = gfirst(am), al = glast(am), pf = gfirst(pm), pl = glast(pm);
+        double gA = 0.0, gP = 0.0;
+        if (af >= 0) gA = (double)gval(c, al) / (double)gval(o, af) - 1.0;
+        if (pf >= 0) gP = (double)gval(c, pl) / (double)gval(o, pf) - 1.0;
+        R.val(2, (af >= 0 && pf >= 0) ? gP - gA : (af >= 0 ? gA - gA : gP - gP));
+      }
+
+      // ================================================================ MOMV CM:485-496, 690-729
+      if (fam & F_MOMV) {
+        fresh(v);
+
+        const double x0 = (double)gval(v, fb);
+        double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+          if ((pb >> k) & 1u) {
+            const double dd = (double)v[k] - x0, d2 = dd * dd;
+            s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
+          }
+        RawMom m{gsum(s1), gsum(s2), gsum(s3), gsum(s4), n};
+        double sdv;
+        if (std1_raw(m, m.s1 == 0.0 && m.s2 == 0.0, sdv)) R.val(14, sdv); else R.null(14);
+        // skew/kurt of v / sum(v) == of v (scale-free); sum(v) = 0 -> shares NaN
+        double sk, ku;
+        skew_kurt(m, sk, ku);
+        if (sumv == 0.0) sk = ku = qnan();
+        R.val(24, sk);
+        R.val(25, ku);
+        R.val(26, sk / ku);
+      }
+
+      // ================================================================ SUMV CM:764-831, 1251-1306
+      if (fam & F_SUMV) {
+        fresh(v);
+
+        const uint32_t mpre = pb & rmask(0, 236), mcls = pb & rmask(237, 239);
+        const uint32_t mhead = pb & rmask(0, 30), mtail = pb & rmask(210, 239);
+        double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const double vk = (double)v[k];
+          if ((mpre >> k) & 1u) a0 += vk;
+          if ((mcls >> k) & 1u) a1 += vk;
+          if ((mhead >> k) & 1u) a2 += vk;
+          if ((mtail >> k) & 1u) a3 += vk;
+        }
+        const double spre = gsum(a0), scls = gsum(a1), shead = gsum(a2), stail = gsum(a3);
+        if (gany(mpre != 0u)) R.val(28, spre);
+        if (gany(mcls != 0u)) R.val(29, scls);
+        const double vfirst = (double)gval(v, fb);
+        R.val(30, vfirst / sumv);
+        R.val(31, scls / sumv);
+        R.val(32, vfirst);
+        R.val(52, sumv > 0.0 ? shead / sumv : 0.125);
+        R.val(53, sumv > 0.0 ? stail / sumv : 0.125);
+      }
+
+      // ================================================================ SUMC + CORR CM:734-761, 834-932
+      if (fam & (F_SUMC | F_CORR)) {
+        fresh(c);
+        fresh(v);
+
+        // last present close / volume of this lane -> carries from the left
+        float lc = 1.f, lvv = 0.f, lcz = 1.f, lvz = 0.f;
+        const uint32_t pz = pb & 0xFFFFu;
+        uint32_t nzm = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if ((pb >> k) & 1u) { lc = c[k]; lvv = v[k]; }
+          if (((pb >> k) & 1u) && v[k] != 0.0f) { lcz = c[k]; lvz = v[k]; nzm |= 1u << k; }
+        }
+        (void)pz;
+        float cpv, vpv, cpz, vpz;
+        bool hp, hz, hpv, hzv;
+        carry_left(lc, pb != 0u, cpv, hp);
+        carry_left(lvv, pb != 0u, vpv, hpv);
+        carry_left(lcz, nzm != 0u, cpz, hz);
+        carry_left(lvz, nzm != 0u, vpz, hzv);
+        if (fam & F_SUMC) {
+          double am = 0.0;
+          float cp = cpv;
+          bool h_ = hp;
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+            if ((pb >> k) & 1u) {
+              if (h_ && v[k] > 0.0f) am += fabs((double)c[k] - (double)cp) / ((double)cp * (double)v[k]);
+              cp = c[k];
+              h_ = true;
+            }
+          R.val(27, gsum(am));  // liq_amihud_1min
+        }
+        if (fam & F_CORR) {
+          // first two present bars f1, f2 and first two non-zero-volume bars z1, z2
+          const int f1 = fb;
+          uint32_t pb2 = pb;
+          if (f1 >= 0 && (f1 >> 4) == g) pb2 &= ~(1u << (f1 & 15));
+          const int f2 = gfirst(pb2);
+          const int z1 = gfirst(nzm);
+          uint32_t nz2 = nzm;
+          if (z1 >= 0 && (z1 >> 4) == g) nz2 &= ~(1u << (z1 & 15));
+          const int z2 = gfirst(nz2);
+          const double cf1 = (double)gval(c, f1), vf1 = (double)gval(v, f1);
+          const double cf2 = f2 >= 0 ? (double)gval(c, f2) : 0.0, vf2 = f2 >= 0 ? (double)gval(v, f2) : 0.0;
+          const double cz1 = z1 >= 0 ? (double)gval(c, z1) : 1.0, vz1 = z1 >= 0 ? (double)gval(v, z1) : 1.0;
+          const double cz2 = z2 >= 0 ? (double)gval(c, z2) : 1.0, vz2 = z2 >= 0 ? (double)gval(v, z2) : 1.0;
+          // shifts = first pair of each variant (exact zeros for constant sides)
+          const double x1 = (cf2 - cf1) / cf1, y1 = vf2;   // prv: (pct_change(close), volume)
+          const double x2 = cf1, y2 = vf1;                 // pv
+          const double x3 = cf2, y3 = vf1;                 // pvd: (close, volume.shift(1))
+          const double x4 = cf1, y4 = vf2;                 // pvl: (close, volume.shift(-1))
+          const double x5 = (cz2 - cz1) / cz1, y5 = (vz2 - vz1) / vz1;  // prvr
+          const double x6 = cz2;                           // pvr (y shift = y5)
+          const int nzc = gcount(nzm);
+          auto fin = [&](int fidx, int np, double a0, double a1, double a2, double a3, double a4) {
+            R.val(fidx, pearson_raw(np, gsum(a0), gsum(a1), gsum(a2), gsum(a3), gsum(a4)));
+          };
+          // pass 1: pv, prv, pvd (previous present bar)
+          {
+            double P[3][5];
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+              for (int j = 0; j < 5; ++j) P[i][j] = 0.0;
+            float cp = cpv, vp = vpv;
+            bool h_ = hp;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              if ((pb >> k) & 1u) {
+                const double ck = (double)c[k], vk = (double)v[k];
+                double dx = ck - x2, dy = vk - y2;
+                P[0][0] += dx; P[0][1] += dy; P[0][2] += dx * dx; P[0][3] += dy * dy; P[0][4] += dx * dy;
+                if (h_) {
+                  const double pc = (ck - (double)cp) / (double)cp;
+                  dx = pc - x1; dy = vk - y1;
+                  P[1][0] += dx; P[1][1] += dy; P[1][2] += dx * dx; P[1][3] += dy * dy; P[1][4] += dx * dy;
+                  dx = ck - x3; dy = (double)vp - y3;
+                  P[2][0] += dx; P[2][1] += dy; P[2][2] += dx * dx; P[2][3] += dy * dy; P[2][4] += dx * dy;
+                }
+                cp = c[k]; vp = v[k]; h_ = true;
+              }
+            }
+            fin(35, n, P[0][0], P[0][1], P[0][2], P[0][3], P[0][4]);          // corr_pv
+            fin(33, n - 1, P[1][0], P[1][1], P[1][2], P[1][3], P[1][4]);      // corr_prv
+            fin(36, n - 1, P[2][0], P[2][1], P[2][2], P[2][3], P[2][4]);      // corr_pvd
+          }
+          // pass 2: prvr, pvr over rows with volume != 0 (CM:855-866, 924-930)
+          if (nzc > 0) {
+            double P[2][5];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+              for (int j = 0; j < 5; ++j) P[i][j] = 0.0;
+            float czp = cpz, vzp = vpz;
+            bool hz_ = hz;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              if (((nzm >> k) & 1u)) {
+                const double ck = (double)c[k], vk = (double)v[k];
+                if (hz_) {
+                  const double pcz = (ck - (double)czp) / (double)czp;
+                  const double pvz = (vk - (double)vzp) / (double)vzp;
+                  double dx = pcz - x5, dy = pvz - y5;
+                  P[0][0] += dx; P[0][1] += dy; P[0][2] += dx * dx; P[0][3] += dy * dy; P[0][4] += dx * dy;
+                  dx = ck - x6;
+                  P[1][0] += dx; P[1][1] += dy; P[1][2] += dx * dx; P[1][3] += dy * dy; P[1][4] += dx * dy;
+                }
+                czp = c[k]; vzp = v[k]; hz_ = true;
+              }
+            }
+            fin(34, nzc - 1, P[0][0], P[0][1], P[0][2], P[0][3], P[0][4]);  // corr_prvr
+            fin(38, nzc - 1, P[1][0], P[1][1], P[1][2], P[1][3], P[1][4]);  // corr_pvr
+          }
+          // pass 3: pvl, right-to-left with the next present volume (CM:905-916)
+          {
+            double a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0;
+            float fvv = 0.f;
+#pragma unroll
+            for (int k = K - 1; k >= 0; --k)
+              if ((pb >> k) & 1u) fvv = v[k];
+            float vn;
+            bool hn;
+            carry_right(fvv, pb != 0u, vn, hn);
+#pragma unroll
+            for (int k = K - 1; k >= 0; --k)
+              if ((pb >> k) & 1u) {
+                if (hn) {
+                  const double dx = (double)c[k] - x4, dy = (double)vn - y4;
+                  a0 += dx; a1 += dy; a2 += dx * dx; a3 += dy * dy; a4 += dx * dy;
+                }
+                vn = v[k];
+                hn = true;
+              }
+            fin(37, n - 1, a0, a1, a2, a3, a4);  // corr_pvl
+          }
+        }
+      }
+
+      // ================================================================ LVL / PDF: tick levels
+      if (fam & (F_LVL | F_PDF)) {
+        fresh(c);
+        fresh(v);
+
+        // tick index round trip and integral volume (the exact fast-path contract)
+        int tk[K];
+        bool ok = true;
+        int tmin = 0x7fffffff, tmax = -0x7fffffff;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const double tt = rint((double)c[k] * 100.0);
+          tk[k] = (int)tt;
+          if ((pb >> k) & 1u) {
+            ok = ok && (tt < 2.0e9) && ((float)(tt * 0.01) == c[k]) && (v[k] == rintf(v[k])) &&
+                 (v[k] <= 16777216.0f);
+            tmin = min(tmin, tk[k]);
+            tmax = max(tmax, tk[k]);
+          }
+        }
+        tmin = gmin_i(tmin);
+        tmax = gmax_i(tmax);
+        bool fast = !gany(!ok) && (tmax - tmin) < NB;
+        double q[5] = {qnan(), qnan(), qnan(), qnan(), qnan()};
+        if (fast) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) scr[16 * g + k] = 0ull;
+          lds_fence();
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+            if ((pb >> k) & 1u)
+              atomicAdd(reinterpret_cast<unsigned long long*>(&scr[tmax - tk[k]]),
+                        (unsigned long long)((1ull << 40) | (uint64_t)v[k]));
+          lds_fence();
+          // bins 16g..16g+15 in descending-close order: count, volume, running cum
+          uint64_t bins[K];
+          uint32_t lanevol = 0, lcnt = 0;
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            bins[k] = scr[16 * g + k];
+            lanevol += (uint32_t)(bins[k] & 0xFFFFFFFFFFull);
+            lcnt |= ((bins[k] >> 40) != 0ull) ? (1u << k) : 0u;
+          }
+          const uint32_t carry = gscan_excl_u(lanevol);
+          const uint32_t Sv = (uint32_t)sumv;
+          if (fam & F_LVL) {
+            // level shares V_l / sum(v) (C7: equal volumes -> identical shares)
+            const double inv = 1.0 / sumv;
+            const int fl_ = gfirst(lcnt);
+            const double x0 = (double)(uint32_t)(bpermu(gb + (fl_ >> 4), (uint32_t)pick(bins, fl_ & 15)) & 0xFFFFFFFFull) * inv;
+            double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+              if ((lcnt >> k) & 1u) {
+                const double dd = (double)(uint32_t)(bins[k] & 0xFFFFFFFFFFull) * inv - x0, d2 = dd * dd;
+                s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
+              }
+            const int L = gcount(lcnt);
+            RawMom m{gsum(s1), gsum(s2), gsum(s3), gsum(s4), L};
+            double sk, ku;
+            skew_kurt(m, sk, ku);
+            if (!(sumv > 0.0)) sk = ku = qnan();
+            R.val(39, ku);  // doc_kurt
+            R.val(40, sk);  // doc_skew
+            R.val(41, sk);  // doc_std: .skew() [sic CM:999]
+          }
+          if (fam & F_PDF) {
+            const double kk[5] = {12.0, 14.0, 16.0, 18.0, 19.0};
+            int ep[5], et[5];
+#pragma unroll
+            for (int t = 0; t < 5; ++t) { ep[t] = 1 << 20; et[t] = 1 << 20; }
+            uint32_t cum = carry;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              cum += (uint32_t)(bins[k] & 0xFFFFFFFFFFull);
+              if ((lcnt >> k) & 1u) {
+                const double lhs = 20.0 * (double)cum;
+#pragma unroll
+                for (int t = 0; t < 5; ++t) {
+                  const double rhs = kk[t] * (double)Sv;
+                  if (lhs > rhs && ep[t] == (1 << 20)) ep[t] = 16 * g + k;
+                  if (lhs == rhs && et[t] == (1 << 20)) et[t] = 16 * g + k;
+                }
+              }
+            }
+            bool tie = false;
+            const int first_level = gfirst(lcnt);
+#pragma unroll
+            for (int t = 0; t < 5; ++t) {
+              int e = gmin_i(ep[t]);
+              const int te = gmin_i(et[t]);
+              if (Sv == 0u) e = first_level;  // shares NaN: NaN > p (S11)
+              else if (te < e) tie = true;
+              if (e < (1 << 20)) {
+                const float cstar = (float)((double)(tmax - e) * 0.01);
+                q[t] = (double)gval(c, lb) / (double)cstar;
+              }
+            }
+            if (tie) fast = false;  // exact tie: the reference's float order decides
+          }
+        }
+        if (!fast) {
+          if (g == 0) {
+            const int idx = atomicAdd(a.fb_count, 1);
+            a.fb_list[idx] = (int)sd;
+          }
+        }
+        if (fam & F_PDF) {
+#pragma unroll
+          for (int t = 0; t < 5; ++t) {
+            qv[t] = q[t];
+            R.null(PDF0 + t);  // filled by mff_pdf_finalize (or the fallback)
+          }
+        }
+      }
+    }
+
+    // ---------------------------------------------------------------- stores
+    if (act) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int f = 16 * q + g;
+        if (f < NF) {
+          const int row = a.row[f];
+          if (row >= 0) {
+            a.val[(size_t)row * plane + sd] = R.r[q];
+            a.state[(size_t)row * plane + sd] = (uint8_t)((R.st >> (8 * q)) & 0xFFu);
+          }
+        }
+      }
+      if (a.pdfq && g < 5) {
+        const double qq = (g == 0) ? qv[0] : (g == 1) ? qv[1] : (g == 2) ? qv[2] : (g == 3) ? qv[3] : qv[4];
+        a.pdfq[(size_t)g * plane + sd] = qq;
+      }
+    }
+  }
+}
+
+}  // namespace g16
+}  // namespace mff
+
+using namespace mff;
+
+extern "C" size_t mff_stage1_workspace_bytes(int S, int D) {
+  return 256 + (size_t)S * (size_t)D * sizeof(int);
+}
+
+extern "C" int mff_stage1(const float* open, const float* high, const float* low, const float* close,
+                          const float* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
+                          int nf, double* val, uint8_t* state, double* pdf_query, void* workspace,
+                          void* stream) {
+  clear_error();
+  MFF_REQUIRE(S > 0 && D > 0, "mff_stage1: S=%d D=%d must be positive", S, D);
+  MFF_REQUIRE((long long)S * D < (1ll << 31), "mff_stage1: S*D must be < 2^31");
+  MFF_REQUIRE(nf > 0 && nf <= NF, "mff_stage1: nf=%d out of range", nf);
+  MFF_REQUIRE(factor_ids != nullptr, "mff_stage1: factor_ids is NULL");
+  MFF_REQUIRE(valid && val && state, "mff_stage1: NULL device buffer");
+  MFF_REQUIRE(workspace != nullptr, "mff_stage1: workspace is NULL (mff_stage1_workspace_bytes)");
+  const float* fld[5] = {open, high, low, close, volume};
+  g16::GArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int f = 0; f < 5; ++f) a.fld[f] = fld[f];
+  a.mask = valid; a.val = val; a.state = state; a.pdfq = pdf_query;
+  a.S = S; a.D = D;
+  for (int i = 0; i < NF; ++i) a.row[i] = -1;
+  for (int r = 0; r < nf; ++r) {
+    const int id = factor_ids[r];
+    MFF_REQUIRE(id >= 0 && id < NF, "mff_stage1: factor id %d out of range", id);
+    MFF_REQUIRE(a.row[id] < 0, "mff_stage1: factor id %d requested twice", id);
+    a.row[id] = (int8_t)r;
+    a.fam |= kFactorFamily[id];
+  }
+  const uint32_t use[5] = {F_SEG | F_ORD | F_MOMR | F_TRD, F_OLS | F_MOMH, F_OLS | F_MOMH,
+                           F_SEG | F_ORD | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD,
+                           F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD};
+  for (int f = 0; f < 5; ++f)
+    MFF_REQUIRE(!(a.fam & use[f]) || fld[f] != nullptr, "mff_stage1: field plane %d required", f);
+  MFF_REQUIRE(!(a.fam & F_PDF) || pdf_query != nullptr, "mff_stage1: doc_pdf requested but pdf_query is NULL");
+  hipStream_t st = as_stream(stream);
+  const char* impl = getenv("MFF_STAGE1_IMPL");
+  if (impl && strcmp(impl, "w64") == 0)  // the wave-per-stock-day kernel for everything
+    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, nullptr, nullptr, ~0u, 0, st);
+  int* cnt = reinterpret_cast<int*>(workspace);
+  a.fb_count = cnt;
+  a.fb_list = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + 256);
+  MFF_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
+  const long long nblk = (long long)((S + 63) / 64) * D;
+  for (int gi = 0; gi < 4; ++gi) {
+    const uint32_t set = g16::kGroups[gi];
+    if (!(a.fam & set)) continue;
+    g16::GArgs b = a;  // this launch stores its own group's rows (and the queries) only
+    for (int i = 0; i < NF; ++i)
+      if (!(kFactorFamily[i] & set)) b.row[i] = -1;
+    if (!(set & F_PDF)) b.pdfq = nullptr;
+    switch (gi) {
+      case 0: hipLaunchKernelGGL(g16::k_stage1g<g16::G_HL>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
+      case 1: hipLaunchKernelGGL(g16::k_stage1g<g16::G_RET>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
+      case 2: hipLaunchKernelGGL(g16::k_stage1g<g16::G_CV>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
+      default: hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
+    }
+    MFF_LAUNCH_CHECK();
+  }
+  if (a.fam & (F_LVL | F_PDF)) {
+    // exact general path for the listed stock-days (LVL + PDF only)
+    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt,
+                      F_LVL | F_PDF, 1024, st);
+  }
+  return 0;
+}

@@ -96,18 +96,32 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
     need_pdf = any(i in catalog.PDF_IDS for i in ids)
     pdfq = torch.empty((5, D, S), dtype=torch.float64, device=dev) if need_pdf else None
     b = panel.bars
+    ws = _workspace(dev, lib.mff_stage1_workspace_bytes(S, D))
     if events is not None:
         events[0].record()
     _lib.check(lib.mff_stage1(_lib.ptr(b[0]), _lib.ptr(b[1]), _lib.ptr(b[2]), _lib.ptr(b[3]),
                               _lib.ptr(b[4]), _lib.ptr(panel.mask), S, D,
                               _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
-                              _lib.ptr(pdfq), _stream(dev)), "mff_stage1")
+                              _lib.ptr(pdfq), _lib.ptr(ws), _stream(dev)), "mff_stage1")
     if events is not None:
         events[1].record()
     if need_pdf:
         rows = [ids.index(i) if i in ids else -1 for i in catalog.PDF_IDS]
         pdf_ranks(panel, pdfq, rows, val, state, comm=comm, day_batch=pdf_day_batch)
     return val, state, ids
+
+
+_WS = {}
+
+
+def _workspace(dev, nbytes: int) -> torch.Tensor:
+    """Per-device scratch reused across calls (grown on demand)."""
+    key = str(dev)
+    t = _WS.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=dev)
+        _WS[key] = t
+    return t
 
 
 def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, rows: List[int], val, state, comm=None,
