@@ -17,13 +17,14 @@
 #include "../../include/mff.h"
 #include "mff_internal.h"
 #include "mff_sort.h"
+#include "mff_group.h"
 #include "mff_wave.h"
 
 namespace mff {
 
-constexpr int PDF_CHUNK = 256;  // stocks per count workgroup: <= 61,440 keys < 2^16
-constexpr int PDF_SPL = 32;     // queries per LDS splitter
-constexpr int PDF_MAXM = 32767; // bins (M+1) u32 must fit 128 KiB of LDS
+constexpr int PDF_MAXM = 32767;  // queries per day (all ranks)
+constexpr int PDF_ZQ = 8192;     // sorted queries per count workgroup (LDS: 16 B each)
+constexpr int PDF_NBK = 2048;    // bucket table over the workgroup's query range
 
 struct QLoader {
   const double* q;  // [R][5][D][S_loc]
@@ -45,107 +46,128 @@ __global__ __launch_bounds__(SORT_THREADS) void k_pdf_sort(const double* q_all, 
   segment_sort(ld, M, q_sorted + (size_t)dd * M, tmp + (size_t)dd * M, sk);
 }
 
+// One workgroup per (day, slice of <= PDF_ZQ consecutive sorted queries): the slice and
+// its predecessor Q[P0-1] sit in LDS with a bucket table over the slice's key range, so
+// a key's lower_bound is a table lookup plus a short LDS binary search.  Every key of
+// the day is formed in every slice's workgroup (the slices of a day share the close
+// plane through L2: their blocks are mapped onto one XCD); a key at or below Q[P0-1]
+// only bumps the slice's `below` count, a key above the slice is dropped.  The slice
+// then writes (n_less, n_eq) at its positions: below + exclusive scan + own lt.
 __global__ __launch_bounds__(1024) void k_pdf_count(const float* close, const uint32_t* valid, int S,
-                                                    int D, int d0, const uint64_t* q_sorted, int M,
-                                                    uint32_t* slab) {
+                                                    int d0, int nd, const uint64_t* q_sorted, int M,
+                                                    int Z, int Mz, uint32_t* counts) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* bins = reinterpret_cast<uint32_t*>(smem);  // [M+1]
-  const int nspl = (M + PDF_SPL - 1) / PDF_SPL;
-  uint64_t* spl = reinterpret_cast<uint64_t*>(smem + (((size_t)(M + 1) * 4 + 15) & ~(size_t)15));
-  const int dd = blockIdx.x;
-  const int chunk = blockIdx.y;
-  const int nchunk = gridDim.y;
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t below_s;
+  // XCD-aware block order: hardware dispatches block b to XCD b % 8; the Z slices of a
+  // day get consecutive logical ids on one XCD
+  const int nb = gridDim.x;
+  const int per_xcd = nb >> 3;  // host pads the grid to a multiple of 8
+  const int lid = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int dd = lid / Z, z = lid % Z;
+  if (dd >= nd) return;
   const int d = d0 + dd;
   const uint64_t* Q = q_sorted + (size_t)dd * M;
-  for (int i = threadIdx.x; i <= M; i += blockDim.x) bins[i] = 0u;
-  for (int i = threadIdx.x; i < nspl; i += blockDim.x) spl[i] = Q[i * PDF_SPL];
+  const int P0 = z * Mz, P1 = min(M, P0 + Mz);
+  uint32_t* out = counts + ((size_t)dd * M) * 2;
+
+  uint64_t* L = reinterpret_cast<uint64_t*>(smem);      // [Mz + 1]: Q[P0-1], Q[P0..P1)
+  uint32_t* lt = reinterpret_cast<uint32_t*>(L + Mz + 1);  // [Mz]
+  uint32_t* eqc = lt + Mz;                                // [Mz]
+  uint16_t* T = reinterpret_cast<uint16_t*>(eqc + Mz);     // [PDF_NBK + 1]
+
+  // valid (non-NaN) part of the slice: NaN queries sort last as ~0 and are never read
+  const int nq = P1 - P0;
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+    L[1 + i] = Q[P0 + i];
+    lt[i] = 0u;
+    eqc[i] = 0u;
+  }
+  if (threadIdx.x == 0) {
+    L[0] = P0 > 0 ? Q[P0 - 1] : 0ull;
+    below_s = 0u;
+  }
+  __syncthreads();
+  int nv = lower_bound_u64(L + 1, 0, nq, ~0ull);  // first sentinel
+  const uint64_t qmin = nv > 0 ? L[1] : 0ull, qmax = nv > 0 ? L[nv] : 0ull;
+  int sh = 0;
+  while (nv > 0 && ((qmax - qmin) >> sh) >= (uint64_t)PDF_NBK) ++sh;
+  for (int b = threadIdx.x; b <= PDF_NBK; b += blockDim.x) {
+    int v = nv;
+    if (nv > 0 && b < PDF_NBK) {
+      const uint64_t edge = qmin + ((uint64_t)b << sh);
+      v = (edge > qmax || edge < qmin) ? nv : lower_bound_u64(L + 1, 0, nv, edge);
+    }
+    T[b] = (uint16_t)v;
+  }
   __syncthreads();
 
-  const int lane = lane_id();
-  const int wave = threadIdx.x >> 6;
-  const int nw = blockDim.x >> 6;
-  const bool lv = lane < 60;
-  for (int j = wave; j < PDF_CHUNK; j += nw) {
-    const int s = chunk * PDF_CHUNK + j;
-    if (s >= S) break;
-    const size_t sd = (size_t)d * S + s;
-    const uint32_t mw = lv ? valid[sd * 8 + (lane >> 3)] : 0u;
-    const uint32_t pb = (mw >> ((lane & 7) * 4)) & 0xFu;
-    bool p[4];
+  if (nv > 0) {
+    const int lane = lane_id();
+    const int g = lane & 15;
+    const int grp = (threadIdx.x >> 4);  // 64 groups of 16 lanes
+    const uint64_t L0 = L[0];
+    uint32_t below = 0u;
+    for (int s = grp; s < S; s += 64) {  // one stock per 16-lane group
+      const size_t sd = (size_t)d * S + s;
+      uint32_t pb = 0u;
+      if (g < 15) pb = (valid[sd * 8 + (g >> 1)] >> (16 * (g & 1))) & 0xFFFFu;
+      if (g16::gmax_i((int)pb) == 0) continue;  // absent stock-day (group-uniform)
+      float c[16];
+      if (g < 15) {
+        const float4* p4 = reinterpret_cast<const float4*>(close + sd * NBAR + 16 * g);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) p[k] = (pb >> k) & 1u;
-    const Bits B = ballot4(p);
-    if (!any(B)) continue;
-    float c[4] = {1.f, 1.f, 1.f, 1.f};
-    if (lv) {
-      const float4 t = reinterpret_cast<const float4*>(close + sd * NBAR)[lane];
-      c[0] = t.x; c[1] = t.y; c[2] = t.z; c[3] = t.w;
-    }
-    const double clast = (double)elem(c, last_of(B));
+        for (int q = 0; q < 4; ++q) {
+          const float4 t = p4[q];
+          c[4 * q] = t.x; c[4 * q + 1] = t.y; c[4 * q + 2] = t.z; c[4 * q + 3] = t.w;
+        }
+      } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (!p[k]) continue;
-      const uint64_t key = ord64(clast / (double)c[k]);
-      // level 1: splitters in LDS
-      int lo = 0, hi = nspl;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (spl[mid] < key) lo = mid + 1; else hi = mid;
+        for (int k = 0; k < 16; ++k) c[k] = 1.f;
       }
-      // answer in (32(b-1), 32b]
-      const int b = lo;
-      int a0 = (b == 0) ? 0 : (b - 1) * PDF_SPL + 1;
-      int a1 = min(b * PDF_SPL, M);
-      if (b == 0) a1 = 0;
-      const int jpos = lower_bound_u64(Q, a0, a1, key);
-      const bool eq = jpos < M && Q[jpos] == key;
-      atomicAdd(&bins[jpos], eq ? 0x10000u : 1u);
+      const int lb = g16::glast(pb);
+      const double clast = (double)g16::gval(c, lb);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        if (!((pb >> k) & 1u)) continue;
+        const uint64_t key = ord64(clast / (double)c[k]);
+        if (key <= L0) { ++below; continue; }
+        if (key > qmax) continue;
+        int lo = 0, hi = 0;
+        if (key > qmin) {
+          const int b = (int)((key - qmin) >> sh);
+          lo = T[b];
+          hi = T[b + 1];
+        }
+        const int j = lower_bound_u64(L + 1, lo, hi, key);
+        atomicAdd(L[1 + j] == key ? &eqc[j] : &lt[j], 1u);
+      }
     }
+    below = (uint32_t)__reduce_add_sync(~0ull, (int)below);
+    if (lane_id() == 0) atomicAdd(&below_s, below);
   }
   __syncthreads();
-  uint32_t* dst = slab + ((size_t)dd * nchunk + chunk) * (size_t)(M + 1);
-  for (int i = threadIdx.x; i <= M; i += blockDim.x) dst[i] = bins[i];
-}
 
-// per day: sum chunk histograms, prefix -> (n_less, n_eq) at every query position
-__global__ __launch_bounds__(1024) void k_pdf_reduce(const uint32_t* slab, int nchunk, int M,
-                                                     uint32_t* counts) {
-  __shared__ uint32_t part[1024];
-  const int dd = blockIdx.x;
-  const uint32_t* sl = slab + (size_t)dd * nchunk * (M + 1);
-  const int per = (M + blockDim.x - 1) / blockDim.x;
-  const int i0 = threadIdx.x * per, i1 = min(M, i0 + per);
-  uint32_t tot = 0;
-  for (int i = i0; i < i1; ++i) {
-    uint32_t lt = 0, eq = 0;
-    for (int cc = 0; cc < nchunk; ++cc) {
-      const uint32_t x = sl[(size_t)cc * (M + 1) + i];
-      lt += x & 0xffffu;
-      eq += x >> 16;
-    }
-    tot += lt + eq;
+  // (n_less, n_eq) at P0 + i: below + sum_{i' < i} (lt + eq) + lt[i]
+  const int per = (nq + 1023) >> 10;
+  const int i0 = min(nq, (int)threadIdx.x * per), i1 = min(nq, i0 + per);
+  uint32_t tot = 0u;
+  for (int i = i0; i < i1; ++i) tot += lt[i] + eqc[i];
+  const int lane = lane_id(), wave = threadIdx.x >> 6;
+  uint32_t incl = tot;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+    if (lane >= o) incl += y;
   }
-  part[threadIdx.x] = tot;
+  if (lane == 63) wsum[wave] = incl;
   __syncthreads();
-  // exclusive scan of part (Hillis-Steele on 1024 entries)
-  for (int o = 1; o < 1024; o <<= 1) {
-    const uint32_t y = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0u;
-    __syncthreads();
-    part[threadIdx.x] += y;
-    __syncthreads();
-  }
-  uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
-  uint32_t* out = counts + (size_t)dd * M * 2;
+  uint32_t run = below_s + incl - tot;
+  for (int w = 0; w < wave; ++w) run += wsum[w];
   for (int i = i0; i < i1; ++i) {
-    uint32_t lt = 0, eq = 0;
-    for (int cc = 0; cc < nchunk; ++cc) {
-      const uint32_t x = sl[(size_t)cc * (M + 1) + i];
-      lt += x & 0xffffu;
-      eq += x >> 16;
-    }
-    out[2 * i] = run + lt;  // keys below Q[i]
-    out[2 * i + 1] = eq;    // keys equal to Q[i]
-    run += lt + eq;
+    out[2 * (P0 + i)] = run + lt[i];
+    out[2 * (P0 + i) + 1] = eqc[i];
+    run += lt[i] + eqc[i];
   }
 }
 
@@ -187,8 +209,7 @@ extern "C" {
 
 size_t mff_pdf_workspace_bytes(int S_loc, int R, int nd) {
   const size_t M = (size_t)R * 5 * S_loc;
-  const size_t nchunk = (S_loc + PDF_CHUNK - 1) / PDF_CHUNK;
-  return align256(M * nd * 8) + align256(nchunk * nd * (M + 1) * 4);
+  return align256(M * nd * 8);  // merge-sort ping-pong buffer
 }
 
 int mff_pdf_sort(const double* q_all, int R, int S_loc, int D, int d0, int nd, uint64_t* q_sorted,
@@ -211,15 +232,14 @@ int mff_pdf_count(const float* close, const uint32_t* valid, int S_loc, int D, i
               "mff_pdf_count: bad sizes");
   MFF_REQUIRE(M <= PDF_MAXM, "mff_pdf_count: %d queries per day exceed %d (R*5*S_loc)", M, PDF_MAXM);
   MFF_REQUIRE(close && valid && q_sorted && counts && workspace, "mff_pdf_count: NULL buffer");
-  const int nchunk = (S_loc + PDF_CHUNK - 1) / PDF_CHUNK;
-  uint32_t* slab = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(workspace) +
-                                               align256((size_t)M * nd * 8));
-  const int nspl = (M + PDF_SPL - 1) / PDF_SPL;
-  const size_t lds = (((size_t)(M + 1) * 4 + 15) & ~(size_t)15) + (size_t)nspl * 8;
-  hipLaunchKernelGGL(k_pdf_count, dim3(nd, nchunk), dim3(1024), lds, as_stream(stream), close, valid,
-                     S_loc, D, d0, q_sorted, M, slab);
-  MFF_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_pdf_reduce, dim3(nd), dim3(1024), 0, as_stream(stream), slab, nchunk, M, counts);
+  (void)workspace;
+  const int Z = (M + PDF_ZQ - 1) / PDF_ZQ;
+  const int Mz = (M + Z - 1) / Z;
+  const size_t lds = (size_t)(Mz + 1) * 8 + (size_t)Mz * 8 + (size_t)(PDF_NBK + 1) * 2;
+  const long long nblk = ((long long)Z * nd + 7) / 8 * 8;
+  MFF_REQUIRE(nblk < (1ll << 31), "mff_pdf_count: too many days in one call");
+  hipLaunchKernelGGL(k_pdf_count, dim3((unsigned)nblk), dim3(1024), lds, as_stream(stream), close, valid,
+                     S_loc, d0, nd, q_sorted, M, Z, Mz, counts);
   MFF_LAUNCH_CHECK();
   return 0;
 }

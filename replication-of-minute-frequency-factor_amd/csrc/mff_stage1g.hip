@@ -19,12 +19,11 @@
 //        values give exact zeros, C3); up/down subsets use min == max     CM:483-729
 //  SUM/TRD masked sums, one reciprocal 1/v per bar                     CM:732-831,1203-1406
 //  CORR  six Pearson sums, shifts = each variant's first pair           CM:834-932
-//  LVL/PDF close levels through an LDS histogram over the 0.01-tick index (exact:
-//        closes round-trip through the tick; distinct closes <-> distinct ticks);
-//        level volumes exact integers; doc_pdf threshold by the exact comparison
-//        20*cum > k*sum(v).  Stock-days whose closes are off the tick grid, span more
-//        than 256 ticks, hit an exact doc_pdf tie, or carry non-integral volume are
-//        appended to a list that the wave64 kernel (mff_stage1.hip) finishes.  CM:935-1138
+//  LVL/PDF close levels by a bitonic sort of (close descending, volume) keys: a level is
+//        a run of equal closes, its volume an exact u32 segment sum; doc_pdf's
+//        threshold by the exact comparison 20*cum > k*sum(v).  Stock-days that hit an
+//        exact doc_pdf tie or carry non-integral volume are appended to a list that the
+//        wave64 kernel (mff_stage1.hip) finishes.                       CM:935-1138
 #include <stdlib.h>
 #include <string.h>
 
@@ -40,7 +39,7 @@ int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, c
 
 namespace g16 {
 
-constexpr int NB = 256;  // tick bins per stock-day (LDS, 8 B each)
+constexpr int NB = 256;  // OLS betas per stock-day (LDS, 8 B each)
 
 struct GArgs {
   const float* fld[5];
@@ -148,8 +147,15 @@ __device__ __forceinline__ void lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ascending bitonic sort of the group's 256 u32 keys (bar order e = 16*gi + k)
-__device__ __forceinline__ void gsort256(uint32_t (&a)[K]) {
+__device__ __forceinline__ uint32_t xor_lane(uint32_t x, int lj) { return (uint32_t)__shfl_xor((int)x, lj, 16); }
+__device__ __forceinline__ uint64_t xor_lane(uint64_t x, int lj) {
+  const uint32_t lo = xor_lane((uint32_t)x, lj), hi = xor_lane((uint32_t)(x >> 32), lj);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// ascending bitonic sort of the group's 256 keys (bar order e = 16*gi + k)
+template <typename T>
+__device__ __forceinline__ void gsort256(T (&a)[K]) {
   const int g = gi();
 #pragma unroll
   for (int size = 2; size <= 256; size <<= 1) {
@@ -161,8 +167,8 @@ __device__ __forceinline__ void gsort256(uint32_t (&a)[K]) {
         const bool up = ((16 * g) & size) == 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          const uint32_t p = (uint32_t)__shfl_xor((int)a[k], lj, 16);
-          const uint32_t mn = min(a[k], p), mx = max(a[k], p);
+          const T p = xor_lane(a[k], lj);
+          const T mn = a[k] < p ? a[k] : p, mx = a[k] < p ? p : a[k];
           a[k] = (lower == up) ? mn : mx;
         }
       } else {
@@ -170,8 +176,8 @@ __device__ __forceinline__ void gsort256(uint32_t (&a)[K]) {
         for (int k = 0; k < K; ++k) {
           if ((k & j) == 0) {
             const bool up = ((16 * g + k) & size) == 0;
-            const uint32_t x = a[k], y = a[k | j];
-            const uint32_t mn = min(x, y), mx = max(x, y);
+            const T x = a[k], y = a[k | j];
+            const T mn = x < y ? x : y, mx = x < y ? y : x;
             a[k] = up ? mn : mx;
             a[k | j] = up ? mx : mn;
           }
@@ -761,64 +767,83 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
         }
       }
 
-      // ================================================================ LVL / PDF: tick levels
+      // ================================================================ LVL / PDF: close levels
       if (fam & (F_LVL | F_PDF)) {
         fresh(c);
         fresh(v);
-
-        // tick index round trip and integral volume (the exact fast-path contract)
-        int tk[K];
+        // (close descending, volume) keys: ~bits(close) in the high word (closes are > 0,
+        // so the float order is the bit order), the integral volume in the low word;
+        // absent bars sort last as ~0.  After the sort, element e < n is a bar, and a
+        // level (distinct close) is a run of equal high words.
         bool ok = true;
-        int tmin = 0x7fffffff, tmax = -0x7fffffff;
+        uint64_t key[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          const double tt = rint((double)c[k] * 100.0);
-          tk[k] = (int)tt;
-          if ((pb >> k) & 1u) {
-            ok = ok && (tt < 2.0e9) && ((float)(tt * 0.01) == c[k]) && (v[k] == rintf(v[k])) &&
-                 (v[k] <= 16777216.0f);
-            tmin = min(tmin, tk[k]);
-            tmax = max(tmax, tk[k]);
-          }
+          const bool pk = (pb >> k) & 1u;
+          if (pk) ok = ok && (v[k] == rintf(v[k])) && (v[k] >= 0.0f) && (v[k] <= 16777216.0f);
+          key[k] = pk ? (((uint64_t)~fbits(c[k]) << 32) | (uint64_t)(uint32_t)v[k]) : ~0ull;
         }
-        tmin = gmin_i(tmin);
-        tmax = gmax_i(tmax);
-        bool fast = !gany(!ok) && (tmax - tmin) < NB;
+        const double clast = (double)gval(c, lb);
+        bool fast = !gany(!ok);
         double q[5] = {qnan(), qnan(), qnan(), qnan(), qnan()};
         if (fast) {
-#pragma unroll
-          for (int k = 0; k < K; ++k) scr[16 * g + k] = 0ull;
-          lds_fence();
-#pragma unroll
-          for (int k = 0; k < K; ++k)
-            if ((pb >> k) & 1u)
-              atomicAdd(reinterpret_cast<unsigned long long*>(&scr[tmax - tk[k]]),
-                        (unsigned long long)((1ull << 40) | (uint64_t)v[k]));
-          lds_fence();
-          // bins 16g..16g+15 in descending-close order: count, volume, running cum
-          uint64_t bins[K];
-          uint32_t lanevol = 0, lcnt = 0;
+          gsort256(key);
+          const int e0 = 16 * g;
+          // close word of the neighbours across the lane boundary
+          const uint32_t prevw = dpp_u<ROW_SHR + 1>((uint32_t)(key[K - 1] >> 32));
+          const uint32_t nextw = dpp_u<ROW_SHL + 1>((uint32_t)(key[0] >> 32));
+          uint32_t endm = 0u, startm = 0u, tv = 0u;
 #pragma unroll
           for (int k = 0; k < K; ++k) {
-            bins[k] = scr[16 * g + k];
-            lanevol += (uint32_t)(bins[k] & 0xFFFFFFFFFFull);
-            lcnt |= ((bins[k] >> 40) != 0ull) ? (1u << k) : 0u;
+            const int e = e0 + k;
+            const uint32_t w = (uint32_t)(key[k] >> 32);
+            const uint32_t wp = k > 0 ? (uint32_t)(key[k - 1] >> 32) : prevw;
+            const uint32_t wn = k < K - 1 ? (uint32_t)(key[k + 1] >> 32) : nextw;
+            if (e < n) {
+              tv += (uint32_t)key[k];
+              if (e == 0 || wp != w) startm |= 1u << k;
+              if (e == n - 1 || wn != w) endm |= 1u << k;
+            }
           }
-          const uint32_t carry = gscan_excl_u(lanevol);
+          // exact u32 prefix sums: sum(v) <= 240 * 2^24 < 2^32
+          const uint32_t carry = gscan_excl_u(tv);
+          // running prefix at the last level start of the lane -> start prefix carried in
+          uint32_t lastS = 0u, run = carry;
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            if ((startm >> k) & 1u) lastS = run;
+            if (e0 + k < n) run += (uint32_t)key[k];
+          }
+          uint32_t sc;
+          bool hs;
+          carry_left(lastS, startm != 0u, sc, hs);
           const uint32_t Sv = (uint32_t)sumv;
           if (fam & F_LVL) {
             // level shares V_l / sum(v) (C7: equal volumes -> identical shares)
             const double inv = 1.0 / sumv;
-            const int fl_ = gfirst(lcnt);
-            const double x0 = (double)(uint32_t)(bpermu(gb + (fl_ >> 4), (uint32_t)pick(bins, fl_ & 15)) & 0xFFFFFFFFull) * inv;
-            double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+            uint32_t cum = carry, st0 = sc, V0 = 0u;
+            bool got = false;
 #pragma unroll
-            for (int k = 0; k < K; ++k)
-              if ((lcnt >> k) & 1u) {
-                const double dd = (double)(uint32_t)(bins[k] & 0xFFFFFFFFFFull) * inv - x0, d2 = dd * dd;
+            for (int k = 0; k < K; ++k) {
+              if ((startm >> k) & 1u) st0 = cum;
+              if (e0 + k < n) cum += (uint32_t)key[k];
+              if (((endm >> k) & 1u) && !got) { V0 = cum - st0; got = true; }
+            }
+            const int fe = gfirst(endm);
+            const double x0 = (double)bpermu(gb + (fe >> 4), V0) * inv;
+            double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+            cum = carry;
+            st0 = sc;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              if ((startm >> k) & 1u) st0 = cum;
+              if (e0 + k < n) cum += (uint32_t)key[k];
+              if ((endm >> k) & 1u) {
+                const double dd = (double)(cum - st0) * inv - x0, d2 = dd * dd;
                 s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
               }
-            const int L = gcount(lcnt);
+            }
+            const int L = gcount(endm);
             RawMom m{gsum(s1), gsum(s2), gsum(s3), gsum(s4), L};
             double sk, ku;
             skew_kurt(m, sk, ku);
@@ -828,6 +853,8 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             R.val(41, sk);  // doc_std: .skew() [sic CM:999]
           }
           if (fam & F_PDF) {
+            // first level (descending close) whose cumulative share exceeds k/20:
+            // 20*cum > k*sum(v), exact in f64 (both sides < 2^37)
             const double kk[5] = {12.0, 14.0, 16.0, 18.0, 19.0};
             int ep[5], et[5];
 #pragma unroll
@@ -835,28 +862,27 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             uint32_t cum = carry;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-              cum += (uint32_t)(bins[k] & 0xFFFFFFFFFFull);
-              if ((lcnt >> k) & 1u) {
+              if (e0 + k < n) cum += (uint32_t)key[k];
+              if ((endm >> k) & 1u) {
                 const double lhs = 20.0 * (double)cum;
 #pragma unroll
                 for (int t = 0; t < 5; ++t) {
                   const double rhs = kk[t] * (double)Sv;
-                  if (lhs > rhs && ep[t] == (1 << 20)) ep[t] = 16 * g + k;
-                  if (lhs == rhs && et[t] == (1 << 20)) et[t] = 16 * g + k;
+                  if (lhs > rhs && ep[t] == (1 << 20)) ep[t] = e0 + k;
+                  if (lhs == rhs && et[t] == (1 << 20)) et[t] = e0 + k;
                 }
               }
             }
             bool tie = false;
-            const int first_level = gfirst(lcnt);
 #pragma unroll
             for (int t = 0; t < 5; ++t) {
               int e = gmin_i(ep[t]);
               const int te = gmin_i(et[t]);
-              if (Sv == 0u) e = first_level;  // shares NaN: NaN > p (S11)
+              if (Sv == 0u) e = 0;  // shares NaN: NaN > p (S11) -> the first level
               else if (te < e) tie = true;
               if (e < (1 << 20)) {
-                const float cstar = (float)((double)(tmax - e) * 0.01);
-                q[t] = (double)gval(c, lb) / (double)cstar;
+                const uint32_t w = bpermu(gb + (e >> 4), (uint32_t)(pick(key, e & 15) >> 32));
+                q[t] = clast / (double)bitsf(~w);
               }
             }
             if (tie) fast = false;  // exact tie: the reference's float order decides

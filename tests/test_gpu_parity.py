@@ -78,12 +78,57 @@ def test_stage1_live_oracle_new_seed(dev):
     _check_all(gv, gs, ov, os_, catalog.NAMES)
 
 
+def test_stage1_w64_kernel_golden(dev, monkeypatch):
+    """MFF_STAGE1_IMPL=w64: the wave-per-stock-day kernel (the LVL/PDF fallback) for all 58."""
+    monkeypatch.setenv("MFF_STAGE1_IMPL", "w64")
+    panel, z = _golden("panel_ragged.npz")
+    gv, gs, ids = _run_stage1(panel, dev)
+    from mff import catalog
+    _check_all(gv, gs, z["val"], z["state"], catalog.NAMES)
+
+
+def test_stage1_level_fallback_and_off_tick(dev):
+    """Levels off the 0.01 grid and wide intraday ranges go through the sorted-level path;
+    stock-days with non-integral volume go through the listed wave64 fallback.  The
+    DevicePanel is built directly (the host validator would refuse fractional volume)."""
+    import mff_oracle as O
+    from mff import synth, catalog, engine
+    panel = synth.make_panel(41, 3, config=14, ragged=True)
+    rng = np.random.default_rng(5)
+    c = panel["close"]
+    c[:, :10] = (c[:, :10] * np.float32(1.0 + 1e-4 * rng.random(c[:, :10].shape))).astype(np.float32)
+    c[:, 10:15] = (c[:, 10:15] * np.linspace(0.8, 1.25, c.shape[2], dtype=np.float32)).astype(np.float32)
+    v = panel["volume"]
+    v[:, 20:25] = v[:, 20:25] + np.float32(0.5)
+    ov, os_ = O.oracle_stage1(panel)
+    bars = torch.from_numpy(np.ascontiguousarray(synth.stack_fields(panel))).to(dev)
+    mask = torch.from_numpy(synth.pack_mask(panel["present"]).view(np.int32)).to(dev)
+    val, state, ids = engine.compute_factors(engine.DevicePanel(bars, mask))
+    torch.cuda.synchronize()
+    _check_all(val.cpu().numpy(), state.cpu().numpy(), ov, os_, catalog.NAMES)
+
+
 def test_doc_pdf_merge_path(dev):
     """M = 5*S = 8,500 > 8,192 queries per day: the sort finishes with a global merge pass."""
     import mff_oracle as O
     from mff import synth
     panel = synth.make_panel(1700, 1, config=12)
     names = ["doc_pdf60", "doc_pdf95"]
+    ov, os_ = O.oracle_stage1(panel, names)
+    gv, gs, _ = _run_stage1(panel, dev, names)
+    bad = []
+    for r, nm in enumerate(names):
+        bad += compare(gv[r], gs[r], ov[r], os_[r], nm, atol=0.0, rtol=0.0)
+    assert not bad, "\n".join(bad)
+
+
+def test_doc_pdf_four_slices(dev):
+    """M = 5*S = 25,000 queries per day: four LDS query slices in mff_pdf_count, with the
+    bench's stock count (ranks exact, tolerance 0)."""
+    import mff_oracle as O
+    from mff import synth
+    panel = synth.make_panel(5000, 1, config=13)
+    names = ["doc_pdf70", "doc_pdf80", "doc_pdf90"]
     ov, os_ = O.oracle_stage1(panel, names)
     gv, gs, _ = _run_stage1(panel, dev, names)
     bad = []
