@@ -81,7 +81,7 @@ def main():
     ap.add_argument("--stocks", type=int, default=5000)
     ap.add_argument("--days", type=int, default=2500)
     ap.add_argument("--cpu-days", type=int, default=16)
-    ap.add_argument("--cpu-stocks", type=int, default=40)
+    ap.add_argument("--cpu-stocks", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
     args = ap.parse_args()

@@ -63,40 +63,50 @@ const char* mff_factor_name(int id);
  * factor_ids (host, nf entries): catalogue ids in output-row order.
  * pdf_query: float64 [5][D][S] workspace, required when any doc_pdf* id is requested
  * (the doc_pdf values are then produced by mff_pdf_* below), else may be NULL.
+ * pdf_levels: mff_pdf_levels_bytes(S, D) bytes, required with doc_pdf (else NULL): the
+ * per-stock-day level list (distinct closes, descending, with cumulative bar counts)
+ * that mff_pdf_count / mff_pdf_rank_local bin against the sorted queries.
  * workspace: mff_stage1_workspace_bytes(S, D) bytes of device scratch (the list of
  * stock-days the exact general path finishes; zeroed by the call itself).
  * Environment MFF_STAGE1_IMPL=w64 selects the wave-per-stock-day kernel for everything.
  */
 size_t mff_stage1_workspace_bytes(int S, int D);
+size_t mff_pdf_levels_bytes(int S, int D);
 int mff_stage1(const float* open, const float* high, const float* low,
                const float* close, const float* volume, const uint32_t* valid,
                int S, int D, const int32_t* factor_ids /* host */, int nf,
-               double* val, uint8_t* state, double* pdf_query, void* workspace,
-               void* stream);
+               double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
+               void* workspace, void* stream);
 
 /*
  * doc_pdf60..95 frame-wide rank (CM:1015-1017: `.rank()` over ALL rows of the day
- * frame, every code).  Three device phases; between count and finalize a multi-GPU
- * caller sums `counts` over ranks (all-reduce), see INTEGRATION.md.
- * Each phase works on days [d0, d0+nd) of arrays laid out over all D days.
+ * frame, every code).  Device phases; each works on days [d0, d0+nd) of arrays laid
+ * out over all D days.
  *   sort:     queries of R ranks, float64 [R][5][D][S_all] (NaN = none; each rank's
  *             [5][D][S_loc] padded to S_all with NaN)
  *             -> q_sorted uint64 [nd][M], M = R*5*S_all <= 32767 (total-order keys)
- *   count:    this rank's keys c_last/c_b against q_sorted
+ *   count:    this rank's keys c_last/c_b (from stage 1's pdf_levels: one key per
+ *             distinct close, weighted by its bar count) against q_sorted
  *             -> counts uint32 [nd][M][2] (n_less, n_eq) over local keys
- *   finalize: own queries [5][D][S_loc] -> val/state rows pdf_rows[5] (host)
- * workspace: mff_pdf_workspace_bytes(S_loc, R, nd) bytes of device scratch.
+ *   [R > 1: the caller sums `counts` over ranks (all-reduce), see INTEGRATION.md]
+ *   finalize: own queries [5][D][S_loc] -> val/state rows pdf_rows[5] (host, -1 = skip)
+ *   rank_local: count + finalize in one pass, for a single rank (R = 1: no exchange)
+ * workspace: mff_pdf_workspace_bytes(S_loc, R, nd) bytes of device scratch (sort).
  */
 size_t mff_pdf_workspace_bytes(int S_loc, int R, int nd);
 int mff_pdf_sort(const double* q_all, int R, int S_all, int D, int d0, int nd,
                  uint64_t* q_sorted, void* workspace, void* stream);
-int mff_pdf_count(const float* close, const uint32_t* valid, int S_loc, int D, int d0,
-                  int nd, const uint64_t* q_sorted, int M, uint32_t* counts,
-                  void* workspace, void* stream);
+int mff_pdf_count(const void* pdf_levels, int S_loc, int D, int d0, int nd,
+                  const uint64_t* q_sorted, int M, uint32_t* counts, void* workspace,
+                  void* stream);
 int mff_pdf_finalize(const double* q_local, const uint64_t* q_sorted,
                      const uint32_t* counts, int S_loc, int D, int d0, int nd, int M,
                      const int32_t* pdf_rows /* host, 5 entries, -1 = skip */,
                      double* val, uint8_t* state, void* stream);
+int mff_pdf_rank_local(const void* pdf_levels, const double* q_local,
+                       int S, int D, int d0, int nd, const uint64_t* q_sorted, int M,
+                       const int32_t* pdf_rows /* host, 5 entries */, double* val,
+                       uint8_t* state, void* stream);
 
 /*
  * Stage 2: N-day rolling post-processing over present days, per stock.

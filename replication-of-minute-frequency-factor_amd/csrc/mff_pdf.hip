@@ -7,13 +7,16 @@
 // keys is n_less(q) + (n_eq(q) + 1) / 2 (S6 'average'), computed here without sorting
 // the day's ~240*S keys:
 //   1. sort    — per day, the 5*S (x R ranks) queries as total-order u64 (mff_sort.h);
-//   2. count   — per (day, chunk of 256 stocks) workgroup, every local key c_last/c_b
-//                finds its bin among the sorted queries (lower_bound: LDS splitters,
-//                then 32 keys in L2) and bumps a packed (eq<<16 | lt) LDS counter; the
-//                chunk histograms are summed and prefix-scanned per day -> (n_less, n_eq)
-//                per sorted query position, over THIS rank's keys;
+//   2. count   — per (day, slice of <= PDF_ZQ sorted queries) workgroup, every local key
+//                c_last/c_b finds its position among the slice's queries (LDS bucket
+//                table + fixed-depth LDS binary search, 16 keys of a lane in lockstep) and
+//                bumps a packed (n_eq << 32 | n_less) LDS counter; a scan turns the
+//                counters into (n_less, n_eq) per sorted query position, over THIS
+//                rank's keys;
 //   [multi-GPU: counts are summed over ranks with one all-reduce]
-//   3. finalize — each own query looks its position up and writes the rank.
+//   3. finalize — each own query looks its position up in its slice (LDS) and writes the
+//                rank.  With one rank, 2 and 3 run as one kernel (mff_pdf_rank_local):
+//                the slice's counters never leave LDS.
 #include "../../include/mff.h"
 #include "mff_internal.h"
 #include "mff_sort.h"
@@ -22,9 +25,11 @@
 
 namespace mff {
 
+size_t pdf_levels_split(int S, int D, size_t* off_cum, size_t* off_meta);  // mff_stage1g.hip
+
 constexpr int PDF_MAXM = 32767;  // queries per day (all ranks)
-constexpr int PDF_ZQ = 8192;     // sorted queries per count workgroup (LDS: 16 B each)
-constexpr int PDF_NBK = 2048;    // bucket table over the workgroup's query range
+constexpr int PDF_ZQ = 9200;     // sorted queries per count workgroup (LDS: 16 B each)
+constexpr int PDF_NBK = 8192;    // bucket table over the workgroup's distinct query values
 
 struct QLoader {
   const double* q;  // [R][5][D][S_loc]
@@ -46,115 +51,37 @@ __global__ __launch_bounds__(SORT_THREADS) void k_pdf_sort(const double* q_all, 
   segment_sort(ld, M, q_sorted + (size_t)dd * M, tmp + (size_t)dd * M, sk);
 }
 
-// One workgroup per (day, slice of <= PDF_ZQ consecutive sorted queries): the slice and
-// its predecessor Q[P0-1] sit in LDS with a bucket table over the slice's key range, so
-// a key's lower_bound is a table lookup plus a short LDS binary search.  Every key of
-// the day is formed in every slice's workgroup (the slices of a day share the close
-// plane through L2: their blocks are mapped onto one XCD); a key at or below Q[P0-1]
-// only bumps the slice's `below` count, a key above the slice is dropped.  The slice
-// then writes (n_less, n_eq) at its positions: below + exclusive scan + own lt.
-__global__ __launch_bounds__(1024) void k_pdf_count(const float* close, const uint32_t* valid, int S,
-                                                    int d0, int nd, const uint64_t* q_sorted, int M,
-                                                    int Z, int Mz, uint32_t* counts) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t below_s;
-  // XCD-aware block order: hardware dispatches block b to XCD b % 8; the Z slices of a
-  // day get consecutive logical ids on one XCD
-  const int nb = gridDim.x;
-  const int per_xcd = nb >> 3;  // host pads the grid to a multiple of 8
-  const int lid = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  const int dd = lid / Z, z = lid % Z;
-  if (dd >= nd) return;
-  const int d = d0 + dd;
-  const uint64_t* Q = q_sorted + (size_t)dd * M;
-  const int P0 = z * Mz, P1 = min(M, P0 + Mz);
-  uint32_t* out = counts + ((size_t)dd * M) * 2;
-
-  uint64_t* L = reinterpret_cast<uint64_t*>(smem);      // [Mz + 1]: Q[P0-1], Q[P0..P1)
-  uint32_t* lt = reinterpret_cast<uint32_t*>(L + Mz + 1);  // [Mz]
-  uint32_t* eqc = lt + Mz;                                // [Mz]
-  uint16_t* T = reinterpret_cast<uint16_t*>(eqc + Mz);     // [PDF_NBK + 1]
-
-  // valid (non-NaN) part of the slice: NaN queries sort last as ~0 and are never read
-  const int nq = P1 - P0;
-  for (int i = threadIdx.x; i < nq; i += blockDim.x) {
-    L[1 + i] = Q[P0 + i];
-    lt[i] = 0u;
-    eqc[i] = 0u;
-  }
-  if (threadIdx.x == 0) {
-    L[0] = P0 > 0 ? Q[P0 - 1] : 0ull;
-    below_s = 0u;
-  }
-  __syncthreads();
-  int nv = lower_bound_u64(L + 1, 0, nq, ~0ull);  // first sentinel
-  const uint64_t qmin = nv > 0 ? L[1] : 0ull, qmax = nv > 0 ? L[nv] : 0ull;
-  int sh = 0;
-  while (nv > 0 && ((qmax - qmin) >> sh) >= (uint64_t)PDF_NBK) ++sh;
-  for (int b = threadIdx.x; b <= PDF_NBK; b += blockDim.x) {
-    int v = nv;
-    if (nv > 0 && b < PDF_NBK) {
-      const uint64_t edge = qmin + ((uint64_t)b << sh);
-      v = (edge > qmax || edge < qmin) ? nv : lower_bound_u64(L + 1, 0, nv, edge);
+// One workgroup per (day, slice of <= PDF_ZQ consecutive sorted queries).  The slice,
+// its predecessor Q[P0-1] and a bucket table over the slice's key range sit in LDS.
+// Every 16-lane group walks the day's stocks (the next stock's closes are loaded while
+// the current one is binned); a stock's 16x16 keys are binned together: all lookups of
+// one search step are independent LDS reads issued back to back, and the step count is
+// the table's worst bucket occupancy (block-uniform), so there is no divergent loop.
+// A key at or below Q[P0-1] only bumps the slice's `below` count, a key above the slice
+// is dropped (a later slice bins it).  Counters are one packed u64 per query position
+// (n_less in the low word, n_eq in the high word): one ds_add_u64 per binned key.
+// The slice then turns them into (n_less, n_eq) at its positions: below + exclusive scan.
+struct PdfSlice {
+  const uint64_t* L;  // LDS [nq + 2]: Q[P0-1], Q[P0..P1), ~0
+  const uint16_t* T;  // LDS [PDF_NBK + 1]
+  uint64_t L0, qmin, qmax;
+  int nv, sh, steps;
+  // lower_bound of `key` inside the slice (key in (L0, qmax]); position relative to P0
+  __device__ __forceinline__ void range(uint64_t key, int& lo, int& hi) const {
+    lo = hi = 0;
+    if (key > qmin) {
+      const int b = (int)((key - qmin) >> sh);
+      lo = T[b];
+      hi = T[b + 1];
     }
-    T[b] = (uint16_t)v;
   }
-  __syncthreads();
+};
 
-  if (nv > 0) {
-    const int lane = lane_id();
-    const int g = lane & 15;
-    const int grp = (threadIdx.x >> 4);  // 64 groups of 16 lanes
-    const uint64_t L0 = L[0];
-    uint32_t below = 0u;
-    for (int s = grp; s < S; s += 64) {  // one stock per 16-lane group
-      const size_t sd = (size_t)d * S + s;
-      uint32_t pb = 0u;
-      if (g < 15) pb = (valid[sd * 8 + (g >> 1)] >> (16 * (g & 1))) & 0xFFFFu;
-      if (g16::gmax_i((int)pb) == 0) continue;  // absent stock-day (group-uniform)
-      float c[16];
-      if (g < 15) {
-        const float4* p4 = reinterpret_cast<const float4*>(close + sd * NBAR + 16 * g);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 t = p4[q];
-          c[4 * q] = t.x; c[4 * q + 1] = t.y; c[4 * q + 2] = t.z; c[4 * q + 3] = t.w;
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) c[k] = 1.f;
-      }
-      const int lb = g16::glast(pb);
-      const double clast = (double)g16::gval(c, lb);
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        if (!((pb >> k) & 1u)) continue;
-        const uint64_t key = ord64(clast / (double)c[k]);
-        if (key <= L0) { ++below; continue; }
-        if (key > qmax) continue;
-        int lo = 0, hi = 0;
-        if (key > qmin) {
-          const int b = (int)((key - qmin) >> sh);
-          lo = T[b];
-          hi = T[b + 1];
-        }
-        const int j = lower_bound_u64(L + 1, lo, hi, key);
-        atomicAdd(L[1 + j] == key ? &eqc[j] : &lt[j], 1u);
-      }
-    }
-    below = (uint32_t)__reduce_add_sync(~0ull, (int)below);
-    if (lane_id() == 0) atomicAdd(&below_s, below);
-  }
-  __syncthreads();
-
-  // (n_less, n_eq) at P0 + i: below + sum_{i' < i} (lt + eq) + lt[i]
-  const int per = (nq + 1023) >> 10;
-  const int i0 = min(nq, (int)threadIdx.x * per), i1 = min(nq, i0 + per);
-  uint32_t tot = 0u;
-  for (int i = i0; i < i1; ++i) tot += lt[i] + eqc[i];
-  const int lane = lane_id(), wave = threadIdx.x >> 6;
-  uint32_t incl = tot;
+// block-wide exclusive scan of one u32 per thread (wsum: 16 words of LDS); returns the
+// thread's offset, *total = the block sum.  Ends synced.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, uint32_t* total) {
+  const int lane = lane_id(), wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t incl = x;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
@@ -162,41 +89,293 @@ __global__ __launch_bounds__(1024) void k_pdf_count(const float* close, const ui
   }
   if (lane == 63) wsum[wave] = incl;
   __syncthreads();
-  uint32_t run = below_s + incl - tot;
-  for (int w = 0; w < wave; ++w) run += wsum[w];
+  uint32_t off = incl - x, tot = 0u;
+  for (int w = 0; w < nw; ++w) {
+    if (w < wave) off += wsum[w];
+    tot += wsum[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return off;
+}
+
+// Load the slice, keep its DISTINCT values above Q[P0-1] (duplicated queries -- many
+// stock-days share e.g. the key 1.0 -- would otherwise deepen every search), build the
+// bucket table and the search depth.  Block-wide; ends synced.
+//   L[0] = Q[P0-1], L[1..nv] = distinct slice values > L[0], L[nv+1] = ~0
+__device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, int P0, int P1,
+                                                    uint64_t* L, uint64_t* C, uint16_t* T,
+                                                    uint32_t* wsum, int* occ_s) {
+  const int nq = P1 - P0;
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) L[1 + i] = Q[P0 + i];
+  if (threadIdx.x == 0) {
+    L[0] = P0 > 0 ? Q[P0 - 1] : 0ull;
+    *occ_s = 0;
+  }
+  __syncthreads();
+  // compaction: a thread's contiguous chunk -> distinct values into C, then back to L
+  const int per = (nq + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int i0 = min(nq, (int)threadIdx.x * per), i1 = min(nq, i0 + per);
+  const uint64_t L0 = L[0];
+  uint32_t cnt = 0u;
   for (int i = i0; i < i1; ++i) {
-    out[2 * (P0 + i)] = run + lt[i];
-    out[2 * (P0 + i) + 1] = eqc[i];
-    run += lt[i] + eqc[i];
+    const uint64_t x = L[1 + i];
+    cnt += (x != ~0ull && x > L0 && x != L[i]) ? 1u : 0u;
+  }
+  uint32_t nu;
+  uint32_t off = block_excl_scan(cnt, wsum, &nu);
+  for (int i = i0; i < i1; ++i) {
+    const uint64_t x = L[1 + i];
+    if (x != ~0ull && x > L0 && x != L[i]) C[off++] = x;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < (int)nu; i += blockDim.x) L[1 + i] = C[i];
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) C[i] = 0ull;
+  if (threadIdx.x == 0) L[1 + nu] = ~0ull;
+  __syncthreads();
+  PdfSlice sl;
+  sl.L = L;
+  sl.T = T;
+  sl.L0 = L0;
+  sl.nv = (int)nu;
+  sl.qmin = nu > 0 ? L[1] : 0ull;
+  sl.qmax = nu > 0 ? L[nu] : 0ull;
+  int sh = 0;
+  while (sl.nv > 0 && ((sl.qmax - sl.qmin) >> sh) >= (uint64_t)PDF_NBK) ++sh;
+  sl.sh = sh;
+  for (int b = threadIdx.x; b <= PDF_NBK; b += blockDim.x) {
+    int v = sl.nv;
+    if (sl.nv > 0 && b < PDF_NBK) {
+      const uint64_t edge = sl.qmin + ((uint64_t)b << sh);
+      v = (edge > sl.qmax || edge < sl.qmin) ? sl.nv : lower_bound_u64(L + 1, 0, sl.nv, edge);
+    }
+    T[b] = (uint16_t)v;
+  }
+  __syncthreads();
+  int occ = 0;
+  for (int b = threadIdx.x; b < PDF_NBK; b += blockDim.x) occ = max(occ, (int)T[b + 1] - (int)T[b]);
+  occ = __reduce_max_sync(~0ull, occ);
+  if (lane_id() == 0) atomicMax(occ_s, occ);
+  __syncthreads();
+  const int mo = *occ_s;
+  sl.steps = mo > 0 ? 32 - __builtin_clz((unsigned)mo) : 0;  // ceil(log2(mo + 1))
+  return sl;
+}
+
+// packed counters -> final (n_less | n_eq << 32) per distinct value (block-wide)
+__device__ __forceinline__ void pdf_slice_scan(uint64_t* C, int nv, uint32_t below, uint32_t* wsum) {
+  const int per = (nv + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int i0 = min(nv, (int)threadIdx.x * per), i1 = min(nv, i0 + per);
+  uint32_t tot = 0u;
+  for (int i = i0; i < i1; ++i) tot += (uint32_t)C[i] + (uint32_t)(C[i] >> 32);
+  uint32_t all;
+  uint32_t run = below + block_excl_scan(tot, wsum, &all);
+  for (int i = i0; i < i1; ++i) {
+    const uint32_t lt = (uint32_t)C[i], eq = (uint32_t)(C[i] >> 32);
+    C[i] = (uint64_t)(run + lt) | ((uint64_t)eq << 32);
+    run += lt + eq;
+  }
+  __syncthreads();
+}
+
+// own queries [5][D][S] of day d that fall in this slice -> rank (S6 average)
+__device__ __forceinline__ void pdf_slice_resolve(const PdfSlice& sl, const uint64_t* C, const double* q_local,
+                                                  int S, int D, int d, const int (&rows)[5], double* val,
+                                                  uint8_t* state) {
+  if (sl.nv == 0) return;
+  const size_t plane = (size_t)D * S;
+  for (int i = threadIdx.x; i < 5 * S; i += blockDim.x) {
+    const int t = i / S, s = i - t * S;
+    if (rows[t] < 0) continue;
+    const double q = q_local[(size_t)t * plane + (size_t)d * S + s];
+    if (__builtin_isnan(q)) continue;  // no level passed (null) or absent stock-day
+    const uint64_t key = ord64(q);
+    if (key <= sl.L0 || key > sl.qmax) continue;  // another slice owns its first copy
+    int lo, hi;
+    sl.range(key, lo, hi);
+    const int j = lower_bound_u64(sl.L + 1, lo, hi, key);
+    const uint64_t cn = C[j];
+    const double rank = (double)(uint32_t)cn + ((double)(uint32_t)(cn >> 32) + 1.0) * 0.5;
+    const size_t o = (size_t)rows[t] * plane + (size_t)d * S + s;
+    val[o] = rank;
+    state[o] = MFF_STATE_VALUE;
   }
 }
 
-struct PdfRows {
-  int r[5];
+struct PdfArgs {
+  const float* lvl_close;  // level side channel written by stage 1 (mff_pdf_levels_bytes)
+  const uint8_t* lvl_cum;
+  const uint64_t* lvl_meta;
+  const uint64_t* q_sorted;
+  uint32_t* counts;       // [nd][M][2] (count phase) or NULL (fused finalize)
+  const double* q_local;  // fused finalize: own queries [5][D][S]
+  double* val;
+  uint8_t* state;
+  int rows[5];
+  int S, D, d0, nd, M, Z, Mz;
 };
 
-__global__ void k_pdf_finalize(const double* q_local, const uint64_t* q_sorted, const uint32_t* counts,
-                               int S, int D, int d0, int nd, int M, PdfRows rows, double* val,
-                               uint8_t* state) {
-  const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long tot = 5ll * nd * S;
-  if (gid >= tot) return;
-  const int s = (int)(gid % S);
-  const int dd = (int)((gid / S) % nd);
-  const int t = (int)(gid / ((long long)S * nd));
-  const int row = rows.r[t];
-  if (row < 0) return;
-  const int d = d0 + dd;
-  const double q = q_local[((size_t)t * D + d) * S + s];
-  if (__builtin_isnan(q)) return;  // no level passed (null) or absent stock-day
-  const uint64_t key = ord64(q);
-  const uint64_t* Q = q_sorted + (size_t)dd * M;
-  const int j = lower_bound_u64(Q, 0, M, key);
-  const uint32_t* cn = counts + ((size_t)dd * M + j) * 2;
-  const double rank = (double)cn[0] + ((double)cn[1] + 1.0) * 0.5;
-  const size_t o = (size_t)row * D * S + (size_t)d * S + s;
-  val[o] = rank;
-  state[o] = MFF_STATE_VALUE;
+template <bool FUSED>
+__global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t below_s;
+  __shared__ int occ_s;
+  // XCD-aware block order: hardware dispatches block b to XCD b % 8; the Z slices of a
+  // day get consecutive logical ids on one XCD (they share the day's close plane in L2)
+  const int per_xcd = gridDim.x >> 3;  // host pads the grid to a multiple of 8
+  const int lid = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int dd = lid / a.Z, z = lid % a.Z;
+  if (dd >= a.nd) return;
+  const int d = a.d0 + dd;
+  const int S = a.S;
+  const uint64_t* Q = a.q_sorted + (size_t)dd * a.M;
+  const int P0 = z * a.Mz, P1 = min(a.M, P0 + a.Mz);
+  const int nq = P1 - P0;
+
+  uint64_t* L = reinterpret_cast<uint64_t*>(smem);  // [Mz + 2]
+  uint64_t* C = L + a.Mz + 2;                       // [Mz]
+  uint16_t* T = reinterpret_cast<uint16_t*>(C + a.Mz);
+  if (threadIdx.x == 0) below_s = 0u;
+  const PdfSlice sl = pdf_slice_setup(Q, a.M, P0, P1, L, C, T, wsum, &occ_s);
+
+  uint32_t below = 0u;
+  if (sl.nv > 0) {
+    const int g = lane_id() & 15;
+    const int grp = threadIdx.x >> 4;  // 64 groups of 16 lanes, one stock each
+    // One stock-day per 16-lane group; its levels (distinct closes, ascending key
+    // c_last/c) 64 at a time, lane g holding levels 4g..4g+3 (one float4 + one u32 of
+    // cumulative counts), each binned with its bar count as weight.  The next
+    // stock-day's first 64 levels are loaded while this one is binned (slots past the
+    // level count are read but ignored: the side channel holds 240 per stock-day).
+    // Search: binary lifting from T[b]-1 (L1[T[b]-1] < key <= L1[T[b+1]]), so a step
+    // is one LDS read, one compare and one select.
+    const uint64_t* L1 = L + 1;
+    const int nvc = sl.nv;  // L1[nv] = ~0 stops every probe past the end
+    auto load = [&](int s, int j0, float4& c4, uint32_t& cu) {
+      const size_t sd = (size_t)d * S + s;
+      const int i0 = min(j0 + 4 * g, NBAR - 4);  // lanes past slot 240 re-read (ignored)
+      c4 = *reinterpret_cast<const float4*>(a.lvl_close + sd * NBAR + i0);
+      cu = *reinterpret_cast<const uint32_t*>(a.lvl_cum + sd * NBAR + i0);
+    };
+    // bin levels j0 + 4g .. j0 + 4g + 3 of one stock-day
+    auto bin = [&](double clast, int nl, int j0, uint32_t cprev, const float4& c4, uint32_t cu) {
+      // bars at each level: cum - cum of the previous level (lane g-1's last byte)
+      const uint32_t left = g16::dpp_u<g16::ROW_SHR + 1>(cu) >> 24;
+      const uint32_t pc = (g == 0) ? cprev : left;
+      uint32_t w[4];
+      w[0] = (cu & 0xFFu) - pc;
+      w[1] = ((cu >> 8) & 0xFFu) - (cu & 0xFFu);
+      w[2] = ((cu >> 16) & 0xFFu) - ((cu >> 8) & 0xFFu);
+      w[3] = (cu >> 24) - ((cu >> 16) & 0xFFu);
+      const float cl[4] = {c4.x, c4.y, c4.z, c4.w};
+      uint64_t key[4];
+      int j[4];
+      uint32_t inm = 0u;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool v = j0 + 4 * g + u < nl;
+        key[u] = ord64(clast / (double)cl[u]);
+        const bool bl = v && key[u] <= sl.L0;
+        const bool in = v && !bl && key[u] <= sl.qmax;
+        below += bl ? w[u] : 0u;
+        inm |= (in ? 1u : 0u) << u;
+        const bool gtmin = key[u] > sl.qmin;
+        const int bk = (in && gtmin) ? (int)((key[u] - sl.qmin) >> sl.sh) : 0;
+        j[u] = (in && gtmin) ? (int)sl.T[bk] - 1 : -1;
+      }
+      for (int bb = (1 << sl.steps) >> 1; bb > 0; bb >>= 1) {
+        uint64_t x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = L1[min(j[u] + bb, nvc)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) j[u] = x[u] < key[u] ? j[u] + bb : j[u];
+      }
+      uint64_t x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = L1[j[u] + 1];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if ((inm >> u) & 1u)
+          atomicAdd((unsigned long long*)&C[j[u] + 1],
+                    x[u] == key[u] ? ((uint64_t)w[u] << 32) : (uint64_t)w[u]);
+    };
+    const int slast = S - 1;
+    uint64_t meta_n = a.lvl_meta[(size_t)d * S + min(grp, slast)];
+    float4 c4_n;
+    uint32_t cu_n;
+    load(min(grp, slast), 0, c4_n, cu_n);
+    for (int s = grp; s < S; s += 64) {  // group-uniform trip count
+      const uint64_t meta = meta_n;
+      const float4 c4 = c4_n;
+      const uint32_t cu = cu_n;
+      const int sn = min(s + 64, slast);  // prefetch (the last one is a harmless re-read)
+      meta_n = a.lvl_meta[(size_t)d * S + sn];
+      load(sn, 0, c4_n, cu_n);
+      const int nl = (int)(meta & 0xFFFFu);
+      if (nl == 0) continue;  // absent stock-day (group-uniform)
+      const double clast = (double)bitsf((uint32_t)(meta >> 32));
+      bin(clast, nl, 0, 0u, c4, cu);
+      for (int j0 = 64; j0 < nl; j0 += 64) {  // more than 64 levels (group-uniform)
+        float4 c4b;
+        uint32_t cub;
+        load(s, j0, c4b, cub);
+        const uint32_t cprev = a.lvl_cum[((size_t)d * S + s) * NBAR + j0 - 1];
+        bin(clast, nl, j0, cprev, c4b, cub);
+      }
+    }
+    below = (uint32_t)__reduce_add_sync(~0ull, (int)below);
+    if (lane_id() == 0) atomicAdd(&below_s, below);
+  }
+  __syncthreads();
+  pdf_slice_scan(C, sl.nv, below_s, wsum);
+  if (FUSED) {
+    pdf_slice_resolve(sl, C, a.q_local, S, a.D, d, a.rows, a.val, a.state);
+  } else {
+    // per sorted position: the counts of its distinct value (positions holding Q[P0-1]
+    // or NaN are never looked up)
+    uint32_t* out = a.counts + ((size_t)dd * a.M + P0) * 2;
+    for (int i = threadIdx.x; i < nq; i += blockDim.x) {
+      const uint64_t x = Q[P0 + i];
+      uint64_t cn = 0ull;
+      if (x > sl.L0 && x <= sl.qmax) {
+        int lo, hi;
+        sl.range(x, lo, hi);
+        cn = C[lower_bound_u64(L + 1, lo, hi, x)];
+      }
+      out[2 * i] = (uint32_t)cn;
+      out[2 * i + 1] = (uint32_t)(cn >> 32);
+    }
+  }
+}
+
+// multi-rank finalize: counts summed over ranks -> per (day, slice) LDS lookup of own queries
+__global__ __launch_bounds__(1024) void k_pdf_finalize(PdfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int occ_s;
+  __shared__ uint32_t wsum[16];
+  const int dd = blockIdx.x / a.Z, z = blockIdx.x % a.Z;
+  if (dd >= a.nd) return;
+  const int d = a.d0 + dd;
+  const uint64_t* Q = a.q_sorted + (size_t)dd * a.M;
+  const int P0 = z * a.Mz, P1 = min(a.M, P0 + a.Mz);
+  uint64_t* L = reinterpret_cast<uint64_t*>(smem);
+  uint64_t* C = L + a.Mz + 2;
+  uint16_t* T = reinterpret_cast<uint16_t*>(C + a.Mz);
+  const PdfSlice sl = pdf_slice_setup(Q, a.M, P0, P1, L, C, T, wsum, &occ_s);
+  // counts of each distinct value, from its first sorted position
+  const uint32_t* cn = a.counts + ((size_t)dd * a.M + P0) * 2;
+  for (int i = threadIdx.x; i < P1 - P0; i += blockDim.x) {
+    const uint64_t x = Q[P0 + i];
+    const uint64_t xp = i > 0 ? Q[P0 + i - 1] : sl.L0;
+    if (x > sl.L0 && x <= sl.qmax && x != xp) {
+      int lo, hi;
+      sl.range(x, lo, hi);
+      C[lower_bound_u64(L + 1, lo, hi, x)] = (uint64_t)cn[2 * i] | ((uint64_t)cn[2 * i + 1] << 32);
+    }
+  }
+  __syncthreads();
+  pdf_slice_resolve(sl, C, a.q_local, a.S, a.D, d, a.rows, a.val, a.state);
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -225,40 +404,88 @@ int mff_pdf_sort(const double* q_all, int R, int S_loc, int D, int d0, int nd, u
   return 0;
 }
 
-int mff_pdf_count(const float* close, const uint32_t* valid, int S_loc, int D, int d0, int nd,
+static void pdf_slices(int M, int& Z, int& Mz, size_t& lds) {
+  Z = (M + PDF_ZQ - 1) / PDF_ZQ;
+  Mz = (M + Z - 1) / Z;
+  lds = (size_t)(Mz + 2) * 8 + (size_t)Mz * 8 + (size_t)(PDF_NBK + 1) * 2;
+}
+
+static int pdf_launch(PdfArgs& a, const uint64_t* q_sorted, int M, hipStream_t st, int mode) {
+  size_t lds;
+  pdf_slices(M, a.Z, a.Mz, lds);
+  a.q_sorted = q_sorted;
+  a.M = M;
+  if (mode == 2) {
+    const long long nblk = (long long)a.Z * a.nd;
+    MFF_REQUIRE(nblk < (1ll << 31), "mff_pdf_finalize: too many days in one call");
+    hipLaunchKernelGGL(k_pdf_finalize, dim3((unsigned)nblk), dim3(1024), lds, st, a);
+  } else {
+    const long long nblk = ((long long)a.Z * a.nd + 7) / 8 * 8;
+    MFF_REQUIRE(nblk < (1ll << 31), "mff_pdf_count: too many days in one call");
+    if (mode == 1)
+      hipLaunchKernelGGL(k_pdf_count<true>, dim3((unsigned)nblk), dim3(1024), lds, st, a);
+    else
+      hipLaunchKernelGGL(k_pdf_count<false>, dim3((unsigned)nblk), dim3(1024), lds, st, a);
+  }
+  MFF_LAUNCH_CHECK();
+  return 0;
+}
+
+static void pdf_levels_args(PdfArgs& a, const void* pdf_levels, int S, int D) {
+  size_t oc, om;
+  pdf_levels_split(S, D, &oc, &om);
+  const char* base = reinterpret_cast<const char*>(pdf_levels);
+  a.lvl_close = reinterpret_cast<const float*>(base);
+  a.lvl_cum = reinterpret_cast<const uint8_t*>(base + oc);
+  a.lvl_meta = reinterpret_cast<const uint64_t*>(base + om);
+}
+
+int mff_pdf_count(const void* pdf_levels, int S_loc, int D, int d0, int nd,
                   const uint64_t* q_sorted, int M, uint32_t* counts, void* workspace, void* stream) {
   clear_error();
   MFF_REQUIRE(S_loc > 0 && D > 0 && nd > 0 && d0 >= 0 && d0 + nd <= D && M > 0,
               "mff_pdf_count: bad sizes");
   MFF_REQUIRE(M <= PDF_MAXM, "mff_pdf_count: %d queries per day exceed %d (R*5*S_loc)", M, PDF_MAXM);
-  MFF_REQUIRE(close && valid && q_sorted && counts && workspace, "mff_pdf_count: NULL buffer");
-  (void)workspace;
-  const int Z = (M + PDF_ZQ - 1) / PDF_ZQ;
-  const int Mz = (M + Z - 1) / Z;
-  const size_t lds = (size_t)(Mz + 1) * 8 + (size_t)Mz * 8 + (size_t)(PDF_NBK + 1) * 2;
-  const long long nblk = ((long long)Z * nd + 7) / 8 * 8;
-  MFF_REQUIRE(nblk < (1ll << 31), "mff_pdf_count: too many days in one call");
-  hipLaunchKernelGGL(k_pdf_count, dim3((unsigned)nblk), dim3(1024), lds, as_stream(stream), close, valid,
-                     S_loc, d0, nd, q_sorted, M, Z, Mz, counts);
-  MFF_LAUNCH_CHECK();
-  return 0;
+  MFF_REQUIRE(pdf_levels && q_sorted && counts && workspace, "mff_pdf_count: NULL buffer");
+  PdfArgs a;
+  memset(&a, 0, sizeof(a));
+  pdf_levels_args(a, pdf_levels, S_loc, D);
+  a.counts = counts;
+  a.S = S_loc; a.D = D; a.d0 = d0; a.nd = nd;
+  return pdf_launch(a, q_sorted, M, as_stream(stream), 0);
 }
 
 int mff_pdf_finalize(const double* q_local, const uint64_t* q_sorted, const uint32_t* counts, int S_loc,
                      int D, int d0, int nd, int M, const int32_t* pdf_rows, double* val, uint8_t* state,
                      void* stream) {
   clear_error();
-  MFF_REQUIRE(S_loc > 0 && D > 0 && nd > 0 && d0 >= 0 && d0 + nd <= D && M > 0,
+  MFF_REQUIRE(S_loc > 0 && D > 0 && nd > 0 && d0 >= 0 && d0 + nd <= D && M > 0 && M <= PDF_MAXM,
               "mff_pdf_finalize: bad sizes");
   MFF_REQUIRE(q_local && q_sorted && counts && pdf_rows && val && state, "mff_pdf_finalize: NULL buffer");
-  PdfRows rows;
-  for (int t = 0; t < 5; ++t) rows.r[t] = pdf_rows[t];
-  const long long tot = 5ll * nd * S_loc;
-  const int thr = 256;
-  hipLaunchKernelGGL(k_pdf_finalize, dim3((unsigned)((tot + thr - 1) / thr)), dim3(thr), 0,
-                     as_stream(stream), q_local, q_sorted, counts, S_loc, D, d0, nd, M, rows, val, state);
-  MFF_LAUNCH_CHECK();
-  return 0;
+  PdfArgs a;
+  memset(&a, 0, sizeof(a));
+  a.counts = const_cast<uint32_t*>(counts);
+  a.q_local = q_local; a.val = val; a.state = state;
+  for (int t = 0; t < 5; ++t) a.rows[t] = pdf_rows[t];
+  a.S = S_loc; a.D = D; a.d0 = d0; a.nd = nd;
+  return pdf_launch(a, q_sorted, M, as_stream(stream), 2);
+}
+
+int mff_pdf_rank_local(const void* pdf_levels, const double* q_local, int S, int D,
+                       int d0, int nd, const uint64_t* q_sorted, int M, const int32_t* pdf_rows,
+                       double* val, uint8_t* state, void* stream) {
+  clear_error();
+  MFF_REQUIRE(S > 0 && D > 0 && nd > 0 && d0 >= 0 && d0 + nd <= D && M > 0 && M <= PDF_MAXM,
+              "mff_pdf_rank_local: bad sizes");
+  MFF_REQUIRE(pdf_levels && q_local && q_sorted && pdf_rows && val && state,
+              "mff_pdf_rank_local: NULL buffer");
+  PdfArgs a;
+  memset(&a, 0, sizeof(a));
+  pdf_levels_args(a, pdf_levels, S, D);
+  a.q_local = q_local; a.val = val; a.state = state;
+  for (int t = 0; t < 5; ++t) a.rows[t] = pdf_rows[t];
+  a.S = S; a.D = D; a.d0 = d0; a.nd = nd;
+  return pdf_launch(a, q_sorted, M, as_stream(stream), 1);
 }
 
 }  // extern "C"

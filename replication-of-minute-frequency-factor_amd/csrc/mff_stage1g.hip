@@ -47,8 +47,12 @@ struct GArgs {
   double* val;
   uint8_t* state;
   double* pdfq;
+  float* lvl_close;     // doc_pdf level side channel (mff_pdf_levels_bytes), or null
+  uint8_t* lvl_cum;
+  uint64_t* lvl_meta;
   int* fb_list;
   int* fb_count;
+  uint32_t fam_exact;  // families whose non-fast stock-days go to the exact list
   int S, D;
   uint32_t fam;
   int8_t row[NF];
@@ -229,6 +233,8 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
     R.r[0] = R.r[1] = R.r[2] = R.r[3] = 0.0;
     R.st = 0u;
     double qv[5] = {qnan(), qnan(), qnan(), qnan(), qnan()};
+    uint32_t lvl_n = 0u;
+    float lvl_clast = 0.f;
 
     if (n > 0) {
       // ---------------------------------------------------------------- loads
@@ -774,37 +780,43 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
         // (close descending, volume) keys: ~bits(close) in the high word (closes are > 0,
         // so the float order is the bit order), the integral volume in the low word;
         // absent bars sort last as ~0.  After the sort, element e < n is a bar, and a
-        // level (distinct close) is a run of equal high words.
+        // level (distinct close) is a run of equal high words.  A stock-day with a
+        // non-integral volume still sorts (volume word 0) for the level list, and its
+        // LVL/PDF values go to the exact path.
         bool ok = true;
         uint64_t key[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const bool pk = (pb >> k) & 1u;
-          if (pk) ok = ok && (v[k] == rintf(v[k])) && (v[k] >= 0.0f) && (v[k] <= 16777216.0f);
-          key[k] = pk ? (((uint64_t)~fbits(c[k]) << 32) | (uint64_t)(uint32_t)v[k]) : ~0ull;
+          const bool vok = (v[k] == rintf(v[k])) && (v[k] >= 0.0f) && (v[k] <= 16777216.0f);
+          if (pk) ok = ok && vok;
+          key[k] = pk ? (((uint64_t)~fbits(c[k]) << 32) | (uint64_t)(vok ? (uint32_t)v[k] : 0u)) : ~0ull;
         }
         const double clast = (double)gval(c, lb);
         bool fast = !gany(!ok);
         double q[5] = {qnan(), qnan(), qnan(), qnan(), qnan()};
-        if (fast) {
-          gsort256(key);
-          const int e0 = 16 * g;
-          // close word of the neighbours across the lane boundary
-          const uint32_t prevw = dpp_u<ROW_SHR + 1>((uint32_t)(key[K - 1] >> 32));
-          const uint32_t nextw = dpp_u<ROW_SHL + 1>((uint32_t)(key[0] >> 32));
-          uint32_t endm = 0u, startm = 0u, tv = 0u;
+        gsort256(key);
+        const int e0 = 16 * g;
+        // close word of the neighbours across the lane boundary
+        const uint32_t prevw = dpp_u<ROW_SHR + 1>((uint32_t)(key[K - 1] >> 32));
+        const uint32_t nextw = dpp_u<ROW_SHL + 1>((uint32_t)(key[0] >> 32));
+        uint32_t endm = 0u, startm = 0u, tv = 0u;
 #pragma unroll
-          for (int k = 0; k < K; ++k) {
-            const int e = e0 + k;
-            const uint32_t w = (uint32_t)(key[k] >> 32);
-            const uint32_t wp = k > 0 ? (uint32_t)(key[k - 1] >> 32) : prevw;
-            const uint32_t wn = k < K - 1 ? (uint32_t)(key[k + 1] >> 32) : nextw;
-            if (e < n) {
-              tv += (uint32_t)key[k];
-              if (e == 0 || wp != w) startm |= 1u << k;
-              if (e == n - 1 || wn != w) endm |= 1u << k;
-            }
+        for (int k = 0; k < K; ++k) {
+          const int e = e0 + k;
+          const uint32_t w = (uint32_t)(key[k] >> 32);
+          const uint32_t wp = k > 0 ? (uint32_t)(key[k - 1] >> 32) : prevw;
+          const uint32_t wn = k < K - 1 ? (uint32_t)(key[k + 1] >> 32) : nextw;
+          if (e < n) {
+            tv += (uint32_t)key[k];
+            if (e == 0 || wp != w) startm |= 1u << k;
+            if (e == n - 1 || wn != w) endm |= 1u << k;
           }
+        }
+        const int L = gcount(endm);
+        lvl_n = (uint32_t)L;
+        lvl_clast = (float)clast;
+        if (fast) {
           // exact u32 prefix sums: sum(v) <= 240 * 2^24 < 2^32
           const uint32_t carry = gscan_excl_u(tv);
           // running prefix at the last level start of the lane -> start prefix carried in
@@ -843,7 +855,6 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
                 s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
               }
             }
-            const int L = gcount(endm);
             RawMom m{gsum(s1), gsum(s2), gsum(s3), gsum(s4), L};
             double sk, ku;
             skew_kurt(m, sk, ku);
@@ -888,7 +899,21 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             if (tie) fast = false;  // exact tie: the reference's float order decides
           }
         }
-        if (!fast) {
+        int li = (int)gscan_excl_u((uint32_t)__builtin_popcount(endm));
+        if (a.lvl_close && ln) {
+          // level list for doc_pdf's frame-wide rank: level i (descending close) at its
+          // run end e: close, and e + 1 = bars in levels 0..i (mff_pdf.hip)
+          float* lc = a.lvl_close + sd * NBAR;
+          uint8_t* lu = a.lvl_cum + sd * NBAR;
+#pragma unroll
+          for (int k = 0; k < K; ++k)
+            if ((endm >> k) & 1u) {
+              lc[li] = bitsf(~(uint32_t)(key[k] >> 32));
+              lu[li] = (uint8_t)(e0 + k + 1);
+              ++li;
+            }
+        }
+        if (!fast && (fam & (a.fam_exact))) {
           if (g == 0) {
             const int idx = atomicAdd(a.fb_count, 1);
             a.fb_list[idx] = (int)sd;
@@ -917,6 +942,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           }
         }
       }
+      if (a.lvl_meta && g == 0) a.lvl_meta[sd] = (uint64_t)lvl_n | ((uint64_t)fbits(lvl_clast) << 32);
       if (a.pdfq && g < 5) {
         const double qq = (g == 0) ? qv[0] : (g == 1) ? qv[1] : (g == 2) ? qv[2] : (g == 3) ? qv[3] : qv[4];
         a.pdfq[(size_t)g * plane + sd] = qq;
@@ -934,10 +960,25 @@ extern "C" size_t mff_stage1_workspace_bytes(int S, int D) {
   return 256 + (size_t)S * (size_t)D * sizeof(int);
 }
 
+namespace mff {
+// doc_pdf level side channel: closes f32 [D][S][240] | cum u8 [D][S][240] | meta u64 [D][S]
+size_t pdf_levels_split(int S, int D, size_t* off_cum, size_t* off_meta) {
+  const size_t sd = (size_t)S * (size_t)D;
+  *off_cum = sd * NBAR * 4;
+  *off_meta = ((*off_cum + sd * NBAR) + 255) & ~(size_t)255;
+  return *off_meta + sd * 8;
+}
+}  // namespace mff
+
+extern "C" size_t mff_pdf_levels_bytes(int S, int D) {
+  size_t a, b;
+  return pdf_levels_split(S, D, &a, &b);
+}
+
 extern "C" int mff_stage1(const float* open, const float* high, const float* low, const float* close,
                           const float* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
-                          int nf, double* val, uint8_t* state, double* pdf_query, void* workspace,
-                          void* stream) {
+                          int nf, double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
+                          void* workspace, void* stream) {
   clear_error();
   MFF_REQUIRE(S > 0 && D > 0, "mff_stage1: S=%d D=%d must be positive", S, D);
   MFF_REQUIRE((long long)S * D < (1ll << 31), "mff_stage1: S*D must be < 2^31");
@@ -951,6 +992,7 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
   for (int f = 0; f < 5; ++f) a.fld[f] = fld[f];
   a.mask = valid; a.val = val; a.state = state; a.pdfq = pdf_query;
   a.S = S; a.D = D;
+  a.fam_exact = ~0u;
   for (int i = 0; i < NF; ++i) a.row[i] = -1;
   for (int r = 0; r < nf; ++r) {
     const int id = factor_ids[r];
@@ -964,16 +1006,35 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
                            F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD};
   for (int f = 0; f < 5; ++f)
     MFF_REQUIRE(!(a.fam & use[f]) || fld[f] != nullptr, "mff_stage1: field plane %d required", f);
-  MFF_REQUIRE(!(a.fam & F_PDF) || pdf_query != nullptr, "mff_stage1: doc_pdf requested but pdf_query is NULL");
+  MFF_REQUIRE(!(a.fam & F_PDF) || (pdf_query != nullptr && pdf_levels != nullptr),
+              "mff_stage1: doc_pdf requested but pdf_query / pdf_levels is NULL");
+  if (a.fam & F_PDF) {
+    size_t oc, om;
+    pdf_levels_split(S, D, &oc, &om);
+    char* base = reinterpret_cast<char*>(pdf_levels);
+    a.lvl_close = reinterpret_cast<float*>(base);
+    a.lvl_cum = reinterpret_cast<uint8_t*>(base + oc);
+    a.lvl_meta = reinterpret_cast<uint64_t*>(base + om);
+  }
   hipStream_t st = as_stream(stream);
-  const char* impl = getenv("MFF_STAGE1_IMPL");
-  if (impl && strcmp(impl, "w64") == 0)  // the wave-per-stock-day kernel for everything
-    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, nullptr, nullptr, ~0u, 0, st);
   int* cnt = reinterpret_cast<int*>(workspace);
   a.fb_count = cnt;
   a.fb_list = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + 256);
   MFF_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
   const long long nblk = (long long)((S + 63) / 64) * D;
+  const char* impl = getenv("MFF_STAGE1_IMPL");
+  if (impl && strcmp(impl, "w64") == 0) {  // the wave-per-stock-day kernel for everything
+    const int rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, nullptr, nullptr, ~0u, 0, st);
+    if (rc != 0 || !(a.fam & F_PDF)) return rc;
+    g16::GArgs b = a;  // doc_pdf level lists only (no rows, no queries, no exact list)
+    for (int i = 0; i < NF; ++i) b.row[i] = -1;
+    b.pdfq = nullptr;
+    b.fam = F_PDF;
+    b.fam_exact = 0u;
+    hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b);
+    MFF_LAUNCH_CHECK();
+    return 0;
+  }
   for (int gi = 0; gi < 4; ++gi) {
     const uint32_t set = g16::kGroups[gi];
     if (!(a.fam & set)) continue;

@@ -25,11 +25,13 @@ SIGNATURES = {
     "mff_num_factors": (c_int, []),
     "mff_factor_name": (c_char_p, [c_int]),
     "mff_stage1_workspace_bytes": (c_size_t, [c_int, c_int]),
-    "mff_stage1": (c_int, [P, P, P, P, P, P, c_int, c_int, IP, c_int, P, P, P, P, P]),
+    "mff_pdf_levels_bytes": (c_size_t, [c_int, c_int]),
+    "mff_stage1": (c_int, [P, P, P, P, P, P, c_int, c_int, IP, c_int, P, P, P, P, P, P]),
     "mff_pdf_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mff_pdf_sort": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
-    "mff_pdf_count": (c_int, [P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
+    "mff_pdf_count": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
     "mff_pdf_finalize": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, IP, P, P, P]),
+    "mff_pdf_rank_local": (c_int, [P, P, c_int, c_int, c_int, c_int, P, c_int, IP, P, P, P]),
     "mff_stage2": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
     "mff_xs_moments": (c_int, [P, P, c_int, c_int, c_int, P, P]),
     "mff_xs_zscore": (c_int, [P, P, c_int, c_int, c_int, P, c_int, P, P, P]),

@@ -95,36 +95,27 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
     state = torch.empty((nf, D, S), dtype=torch.uint8, device=dev)
     need_pdf = any(i in catalog.PDF_IDS for i in ids)
     pdfq = torch.empty((5, D, S), dtype=torch.float64, device=dev) if need_pdf else None
+    levels = (torch.empty(lib.mff_pdf_levels_bytes(S, D), dtype=torch.uint8, device=dev)
+              if need_pdf else None)
     b = panel.bars
-    ws = _workspace(dev, lib.mff_stage1_workspace_bytes(S, D))
+    ws = torch.empty(lib.mff_stage1_workspace_bytes(S, D), dtype=torch.uint8, device=dev)
     if events is not None:
         events[0].record()
     _lib.check(lib.mff_stage1(_lib.ptr(b[0]), _lib.ptr(b[1]), _lib.ptr(b[2]), _lib.ptr(b[3]),
                               _lib.ptr(b[4]), _lib.ptr(panel.mask), S, D,
                               _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
-                              _lib.ptr(pdfq), _lib.ptr(ws), _stream(dev)), "mff_stage1")
+                              _lib.ptr(pdfq), _lib.ptr(levels), _lib.ptr(ws), _stream(dev)),
+               "mff_stage1")
     if events is not None:
         events[1].record()
     if need_pdf:
         rows = [ids.index(i) if i in ids else -1 for i in catalog.PDF_IDS]
-        pdf_ranks(panel, pdfq, rows, val, state, comm=comm, day_batch=pdf_day_batch)
+        pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
     return val, state, ids
 
 
-_WS = {}
-
-
-def _workspace(dev, nbytes: int) -> torch.Tensor:
-    """Per-device scratch reused across calls (grown on demand)."""
-    key = str(dev)
-    t = _WS.get(key)
-    if t is None or t.numel() < nbytes:
-        t = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=dev)
-        _WS[key] = t
-    return t
-
-
-def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, rows: List[int], val, state, comm=None,
+def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows: List[int], val, state,
+              comm=None,
               day_batch: Optional[int] = None, workspace_budget: int = 2 << 30):
     """doc_pdf frame-wide ranks (CM:1015-1017) for all days, in day batches."""
     lib = _lib.load()
@@ -145,14 +136,19 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, rows: List[int], val, stat
         nd = min(day_batch, D - d0)
         ws = torch.empty(lib.mff_pdf_workspace_bytes(S, R, nd), dtype=torch.uint8, device=dev)
         q_sorted = torch.empty((nd, M), dtype=torch.int64, device=dev)
-        counts = torch.empty((nd, M, 2), dtype=torch.int32, device=dev)
         _lib.check(lib.mff_pdf_sort(_lib.ptr(q_all), R, S_all, D, d0, nd, _lib.ptr(q_sorted),
                                     _lib.ptr(ws), st), "mff_pdf_sort")
-        _lib.check(lib.mff_pdf_count(_lib.ptr(panel.bars[3]), _lib.ptr(panel.mask), S, D, d0, nd,
+        if comm is None:  # single rank: count + finalize fused, no exchange
+            _lib.check(lib.mff_pdf_rank_local(_lib.ptr(levels), _lib.ptr(pdfq), S, D, d0, nd,
+                                              _lib.ptr(q_sorted), M,
+                                              _lib.int_array(rows), _lib.ptr(val), _lib.ptr(state), st),
+                       "mff_pdf_rank_local")
+            continue
+        counts = torch.empty((nd, M, 2), dtype=torch.int32, device=dev)
+        _lib.check(lib.mff_pdf_count(_lib.ptr(levels), S, D, d0, nd,
                                      _lib.ptr(q_sorted), M, _lib.ptr(counts), _lib.ptr(ws), st),
                    "mff_pdf_count")
-        if comm is not None:
-            comm.all_reduce_sum(counts)
+        comm.all_reduce_sum(counts)
         _lib.check(lib.mff_pdf_finalize(_lib.ptr(pdfq), _lib.ptr(q_sorted), _lib.ptr(counts), S, D,
                                         d0, nd, M, _lib.int_array(rows), _lib.ptr(val),
                                         _lib.ptr(state), st), "mff_pdf_finalize")
