@@ -14,8 +14,6 @@
 namespace mff {
 namespace g16 {
 
-constexpr int K = 16;  // bars per lane
-
 __device__ __forceinline__ int gi() { return (int)(threadIdx.x & 15u); }
 __device__ __forceinline__ int gbase() { return (int)(threadIdx.x & 48u); }
 
@@ -26,6 +24,7 @@ constexpr int ROW_SHR = 0x110;  // + n
 constexpr int ROW_SHL = 0x100;  // + n
 constexpr int ROW_MIRROR = 0x140;
 constexpr int ROW_HALF_MIRROR = 0x141;
+constexpr int K = 16;  // bars per lane
 
 template <int CTRL>
 __device__ __forceinline__ int dpp_i(int x) {
@@ -222,6 +221,94 @@ __device__ __forceinline__ int glast(uint32_t m) {
   return gmax_i(m ? 16 * gi() + 31 - (int)__builtin_clz(m) : -1);
 }
 __device__ __forceinline__ int gcount(uint32_t m) { return gsum_i(__builtin_popcount(m)); }
+__device__ __forceinline__ uint32_t gmax_u(uint32_t x) {
+  x = max(x, dpp_u<QP_XOR1>(x));
+  x = max(x, dpp_u<QP_XOR2>(x));
+  x = max(x, dpp_u<ROW_HALF_MIRROR>(x));
+  x = max(x, dpp_u<ROW_MIRROR>(x));
+  return x;
+}
+__device__ __forceinline__ uint32_t gmin_u(uint32_t x) {
+  x = min(x, dpp_u<QP_XOR1>(x));
+  x = min(x, dpp_u<QP_XOR2>(x));
+  x = min(x, dpp_u<ROW_HALF_MIRROR>(x));
+  x = min(x, dpp_u<ROW_MIRROR>(x));
+  return x;
+}
+
+// ---- ascending sort of the group's 256 u32 keys (element e = 16*gi + k), bitonic with
+// the "flip" merge: every merge of size s starts by comparing e with e ^ (s-1), then
+// half-cleans with e ^ j; every compare-exchange is ascending, so in-lane steps are a
+// bare v_min_u32 / v_max_u32 pair with compile-time register indices.  Cross-lane
+// partners are DPP patterns inside the 16-lane row (xor 1, 2, 3 quad_perm; xor 7
+// row_half_mirror; xor 15 row_mirror; xor 8 row_ror:8) except xor 4 (ds_swizzle).
+constexpr int QP_XOR3 = 0x1B;   // quad_perm [3,2,1,0]
+constexpr int ROW_ROR8 = 0x128;
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_full(uint32_t x) {
+  // every source lane is inside the row, so `old` is never used
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t swz_xor4(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (4 << 10));
+}
+// partner value for lane xor M (M in {1,2,3,4,7,8,15}) of element register x
+template <int M>
+__device__ __forceinline__ uint32_t gpartner(uint32_t x) {
+  if constexpr (M == 1) return dpp_full<QP_XOR1>(x);
+  else if constexpr (M == 2) return dpp_full<QP_XOR2>(x);
+  else if constexpr (M == 3) return dpp_full<QP_XOR3>(x);
+  else if constexpr (M == 4) return swz_xor4(x);
+  else if constexpr (M == 7) return dpp_full<ROW_HALF_MIRROR>(x);
+  else if constexpr (M == 8) return dpp_full<ROW_ROR8>(x);
+  else return dpp_full<ROW_MIRROR>(x);
+}
+// one cross-lane step: lane partner g ^ M, register k paired with partner register
+// FLIP ? 15-k : k; the lane whose bit LB is clear keeps the minimum
+template <int M, int LB, bool FLIP>
+__device__ __forceinline__ void gcross(uint32_t (&a)[K]) {
+  const bool lower = (gi() & LB) == 0;
+  uint32_t p[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = gpartner<M>(a[FLIP ? K - 1 - k : k]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) a[k] = lower ? min(a[k], p[k]) : max(a[k], p[k]);
+}
+template <int J, bool FLIP>
+__device__ __forceinline__ void glocal(uint32_t (&a)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int o = FLIP ? (k ^ (2 * J - 1)) : (k ^ J);
+    if (o > k) {
+      const uint32_t x = a[k], y = a[o];
+      a[k] = min(x, y);
+      a[o] = max(x, y);
+    }
+  }
+}
+__device__ __forceinline__ void glocal_tail(uint32_t (&a)[K]) {
+  glocal<8, false>(a);
+  glocal<4, false>(a);
+  glocal<2, false>(a);
+  glocal<1, false>(a);
+}
+__device__ __forceinline__ void gsort256u(uint32_t (&a)[K]) {
+  // sizes 2..16 inside the lane
+  glocal<1, true>(a);
+  glocal<2, true>(a); glocal<1, false>(a);
+  glocal<4, true>(a); glocal<2, false>(a); glocal<1, false>(a);
+  glocal<8, true>(a); glocal<4, false>(a); glocal<2, false>(a); glocal<1, false>(a);
+  // size 32: flip with lane ^ 1
+  gcross<1, 1, true>(a); glocal_tail(a);
+  // size 64: flip lane ^ 3, then lane ^ 1
+  gcross<3, 2, true>(a); gcross<1, 1, false>(a); glocal_tail(a);
+  // size 128: flip lane ^ 7, then ^ 2, ^ 1
+  gcross<7, 4, true>(a); gcross<2, 2, false>(a); gcross<1, 1, false>(a); glocal_tail(a);
+  // size 256: flip lane ^ 15, then ^ 4, ^ 2, ^ 1
+  gcross<15, 8, true>(a); gcross<4, 4, false>(a); gcross<2, 2, false>(a); gcross<1, 1, false>(a);
+  glocal_tail(a);
+}
 
 }  // namespace g16
 }  // namespace mff

@@ -450,7 +450,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
         uint32_t key[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) key[k] = ((pb >> k) & 1u) ? fbits(v[k]) : 0xffffffffu;
-        gsort256(key);
+        gsort256u(key);
         auto kth = [&](int e) { return bitsf(bpermu(gb + (e >> 4), pick(key, e & 15))); };
         th50 = kth(n >= 50 ? n - 50 : 0);  // top_k(50).min()   CM:391-396
         th20 = kth(n >= 20 ? n - 20 : 0);  // top_k(20).min()
@@ -777,38 +777,82 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
       if (fam & (F_LVL | F_PDF)) {
         fresh(c);
         fresh(v);
-        // (close descending, volume) keys: ~bits(close) in the high word (closes are > 0,
-        // so the float order is the bit order), the integral volume in the low word;
-        // absent bars sort last as ~0.  After the sort, element e < n is a bar, and a
-        // level (distinct close) is a run of equal high words.  A stock-day with a
-        // non-integral volume still sorts (volume word 0) for the level list, and its
-        // LVL/PDF values go to the exact path.
+        // Levels (distinct closes) in descending close order: after an ascending sort,
+        // element e < n is a bar with close word cw[e] (ascending = close descending,
+        // close = bitsf(cbase - cw)) and volume vv[e]; a level is a run of equal cw.
+        //  * narrow days (closes within 2^24 float steps, i.e. a high/low close ratio
+        //    below 2: every real A-share day): u32 keys (bits(cmax) - bits(c)) << 8 | bar,
+        //    the bar's volume read back from LDS after the sort;
+        //  * otherwise u64 keys ~bits(close) << 32 | volume.
+        // Closes are > 0, so the float order is the bit order; absent bars sort last.
+        // A stock-day with a non-integral volume still sorts (volume 0) for the level
+        // list, and its LVL/PDF values go to the exact path.
         bool ok = true;
-        uint64_t key[K];
+        uint32_t cmx = 0u, cmn = 0xffffffffu;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const bool pk = (pb >> k) & 1u;
           const bool vok = (v[k] == rintf(v[k])) && (v[k] >= 0.0f) && (v[k] <= 16777216.0f);
-          if (pk) ok = ok && vok;
-          key[k] = pk ? (((uint64_t)~fbits(c[k]) << 32) | (uint64_t)(vok ? (uint32_t)v[k] : 0u)) : ~0ull;
+          if (pk) {
+            ok = ok && vok;
+            cmx = max(cmx, fbits(c[k]));
+            cmn = min(cmn, fbits(c[k]));
+          }
         }
+        cmx = gmax_u(cmx);
+        cmn = gmin_u(cmn);
         const double clast = (double)gval(c, lb);
         bool fast = !gany(!ok);
         double q[5] = {qnan(), qnan(), qnan(), qnan(), qnan()};
-        gsort256(key);
         const int e0 = 16 * g;
+        uint32_t cw[K], vv[K], cbase;
+        if (cmx - cmn < (1u << 24)) {  // uniform inside the group
+          uint32_t* sv = reinterpret_cast<uint32_t*>(scr);  // 256 volumes of this group
+          uint32_t key[K];
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const bool pk = (pb >> k) & 1u;
+            const bool vok = (v[k] == rintf(v[k])) && (v[k] >= 0.0f) && (v[k] <= 16777216.0f);
+            sv[e0 + k] = (pk && vok) ? (uint32_t)v[k] : 0u;
+            key[k] = pk ? ((cmx - fbits(c[k])) << 8) | (uint32_t)(e0 + k) : 0xffffffffu;
+          }
+          gsort256u(key);
+          lds_fence();
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            cw[k] = key[k] >> 8;
+            vv[k] = (e0 + k < n) ? sv[key[k] & 0xffu] : 0u;
+          }
+          lds_fence();
+          cbase = cmx;
+        } else {
+          uint64_t key[K];
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const bool pk = (pb >> k) & 1u;
+            const bool vok = (v[k] == rintf(v[k])) && (v[k] >= 0.0f) && (v[k] <= 16777216.0f);
+            key[k] = pk ? (((uint64_t)~fbits(c[k]) << 32) | (uint64_t)(vok ? (uint32_t)v[k] : 0u)) : ~0ull;
+          }
+          gsort256(key);
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            cw[k] = (uint32_t)(key[k] >> 32);
+            vv[k] = (uint32_t)key[k];
+          }
+          cbase = 0xffffffffu;
+        }
         // close word of the neighbours across the lane boundary
-        const uint32_t prevw = dpp_u<ROW_SHR + 1>((uint32_t)(key[K - 1] >> 32));
-        const uint32_t nextw = dpp_u<ROW_SHL + 1>((uint32_t)(key[0] >> 32));
+        const uint32_t prevw = dpp_u<ROW_SHR + 1>(cw[K - 1]);
+        const uint32_t nextw = dpp_u<ROW_SHL + 1>(cw[0]);
         uint32_t endm = 0u, startm = 0u, tv = 0u;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const int e = e0 + k;
-          const uint32_t w = (uint32_t)(key[k] >> 32);
-          const uint32_t wp = k > 0 ? (uint32_t)(key[k - 1] >> 32) : prevw;
-          const uint32_t wn = k < K - 1 ? (uint32_t)(key[k + 1] >> 32) : nextw;
+          const uint32_t w = cw[k];
+          const uint32_t wp = k > 0 ? cw[k - 1] : prevw;
+          const uint32_t wn = k < K - 1 ? cw[k + 1] : nextw;
           if (e < n) {
-            tv += (uint32_t)key[k];
+            tv += vv[k];
             if (e == 0 || wp != w) startm |= 1u << k;
             if (e == n - 1 || wn != w) endm |= 1u << k;
           }
@@ -824,7 +868,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
 #pragma unroll
           for (int k = 0; k < K; ++k) {
             if ((startm >> k) & 1u) lastS = run;
-            if (e0 + k < n) run += (uint32_t)key[k];
+            if (e0 + k < n) run += vv[k];
           }
           uint32_t sc;
           bool hs;
@@ -838,7 +882,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
 #pragma unroll
             for (int k = 0; k < K; ++k) {
               if ((startm >> k) & 1u) st0 = cum;
-              if (e0 + k < n) cum += (uint32_t)key[k];
+              if (e0 + k < n) cum += vv[k];
               if (((endm >> k) & 1u) && !got) { V0 = cum - st0; got = true; }
             }
             const int fe = gfirst(endm);
@@ -849,7 +893,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
 #pragma unroll
             for (int k = 0; k < K; ++k) {
               if ((startm >> k) & 1u) st0 = cum;
-              if (e0 + k < n) cum += (uint32_t)key[k];
+              if (e0 + k < n) cum += vv[k];
               if ((endm >> k) & 1u) {
                 const double dd = (double)(cum - st0) * inv - x0, d2 = dd * dd;
                 s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
@@ -873,7 +917,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             uint32_t cum = carry;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-              if (e0 + k < n) cum += (uint32_t)key[k];
+              if (e0 + k < n) cum += vv[k];
               if ((endm >> k) & 1u) {
                 const double lhs = 20.0 * (double)cum;
 #pragma unroll
@@ -892,8 +936,8 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
               if (Sv == 0u) e = 0;  // shares NaN: NaN > p (S11) -> the first level
               else if (te < e) tie = true;
               if (e < (1 << 20)) {
-                const uint32_t w = bpermu(gb + (e >> 4), (uint32_t)(pick(key, e & 15) >> 32));
-                q[t] = clast / (double)bitsf(~w);
+                const uint32_t w = bpermu(gb + (e >> 4), pick(cw, e & 15));
+                q[t] = clast / (double)bitsf(cbase - w);
               }
             }
             if (tie) fast = false;  // exact tie: the reference's float order decides
@@ -908,7 +952,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
 #pragma unroll
           for (int k = 0; k < K; ++k)
             if ((endm >> k) & 1u) {
-              lc[li] = bitsf(~(uint32_t)(key[k] >> 32));
+              lc[li] = bitsf(cbase - cw[k]);
               lu[li] = (uint8_t)(e0 + k + 1);
               ++li;
             }

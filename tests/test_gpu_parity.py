@@ -98,6 +98,8 @@ def test_stage1_level_fallback_and_off_tick(dev):
     c = panel["close"]
     c[:, :10] = (c[:, :10] * np.float32(1.0 + 1e-4 * rng.random(c[:, :10].shape))).astype(np.float32)
     c[:, 10:15] = (c[:, 10:15] * np.linspace(0.8, 1.25, c.shape[2], dtype=np.float32)).astype(np.float32)
+    # closes spanning more than 2^24 float steps (ratio > 2): the u64-key level sort
+    c[:, 15:18] = (c[:, 15:18] * np.linspace(0.6, 2.4, c.shape[2], dtype=np.float32)).astype(np.float32)
     v = panel["volume"]
     v[:, 20:25] = v[:, 20:25] + np.float32(0.5)
     ov, os_ = O.oracle_stage1(panel)
