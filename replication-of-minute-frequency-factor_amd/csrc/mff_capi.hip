@@ -37,18 +37,13 @@ const char* const kFactorNames[NF] = {
     "trade_topNeg20retRatio", "trade_topPos20retRatio",
 };
 
-const uint32_t kFactorFamily[NF] = {
-    F_SEG, F_SEG, F_SEG, F_SEG, F_SEG,
-    F_OLS, F_OLS, F_OLS, F_OLS, F_OLS,
-    F_ORD, F_ORD, F_ORD, F_ORD,
-    F_MOMV, F_MOMH, F_MOMR, F_MOMR, F_MOMR, F_MOMR, F_MOMR,
-    F_MOMR, F_MOMR, F_MOMR, F_MOMV, F_MOMV, F_MOMV,
-    F_SUMC, F_SUMV, F_SUMV, F_SUMV, F_SUMV, F_SUMV,
-    F_CORR, F_CORR, F_CORR, F_CORR, F_CORR, F_CORR,
-    F_LVL, F_LVL, F_LVL, F_PDF, F_PDF, F_PDF, F_PDF, F_PDF,
-    F_ORDV, F_ORDV, F_ORDV,
-    F_TRD, F_TRD, F_SUMV, F_SUMV, F_TRD, F_TRD, F_TRD, F_TRD,
-};
+
+
+static_assert([] {  // the table in mff_internal.h and the device lookup agree
+  for (int f = 0; f < NF; ++f)
+    if (kFactorFamily[f] != kFamOf(f)) return false;
+  return true;
+}(), "kFamOf (device) disagrees with kFactorFamily");
 
 }  // namespace mff
 

@@ -56,9 +56,26 @@ enum Fam : uint32_t {
 
 constexpr int NF = 58;
 extern const char* const kFactorNames[NF];
-extern const uint32_t kFactorFamily[NF];
 // first catalogue id of doc_pdf60..95
 constexpr int PDF0 = 42;
+inline constexpr uint32_t kFactorFamily[NF] = {
+    F_SEG, F_SEG, F_SEG, F_SEG, F_SEG,
+    F_OLS, F_OLS, F_OLS, F_OLS, F_OLS,
+    F_ORD, F_ORD, F_ORD, F_ORD,
+    F_MOMV, F_MOMH, F_MOMR, F_MOMR, F_MOMR, F_MOMR, F_MOMR,
+    F_MOMR, F_MOMR, F_MOMR, F_MOMV, F_MOMV, F_MOMV,
+    F_SUMC, F_SUMV, F_SUMV, F_SUMV, F_SUMV, F_SUMV,
+    F_CORR, F_CORR, F_CORR, F_CORR, F_CORR, F_CORR,
+    F_LVL, F_LVL, F_LVL, F_PDF, F_PDF, F_PDF, F_PDF, F_PDF,
+    F_ORDV, F_ORDV, F_ORDV,
+    F_TRD, F_TRD, F_SUMV, F_SUMV, F_TRD, F_TRD, F_TRD, F_TRD,
+};
+// kFactorFamily[f] as a constant expression for device code (catalogue order, CM:12-1381)
+__host__ __device__ constexpr uint32_t kFamOf(int f) {
+  return f < 5 ? F_SEG : f < 10 ? F_OLS : f < 14 ? F_ORD : f == 14 ? F_MOMV : f == 15 ? F_MOMH
+       : f < 24 ? F_MOMR : f < 27 ? F_MOMV : f == 27 ? F_SUMC : f < 33 ? F_SUMV : f < 39 ? F_CORR
+       : f < 42 ? F_LVL : f < 47 ? F_PDF : f < 50 ? F_ORDV : f < 52 ? F_TRD : f < 54 ? F_SUMV : F_TRD;
+}
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

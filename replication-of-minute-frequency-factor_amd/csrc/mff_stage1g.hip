@@ -29,6 +29,7 @@
 
 #include "../../include/mff.h"
 #include "mff_group.h"
+#include "mff_stats.h"
 #include "mff_internal.h"
 
 namespace mff {
@@ -36,6 +37,8 @@ namespace mff {
 int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, const int32_t* ids, int nf,
                double* val, uint8_t* state, double* pdfq, const int* list, const int* list_count,
                uint32_t fam_mask, int list_grid, hipStream_t st);
+int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
+                  uint32_t fam, double* val, uint8_t* state, hipStream_t st);
 
 namespace g16 {
 
@@ -86,50 +89,6 @@ __device__ __forceinline__ double gmax_d(double x) {
   x = fmax(x, dpp_d<ROW_HALF_MIRROR>(x));
   x = fmax(x, dpp_d<ROW_MIRROR>(x));
   return x;
-}
-
-// Moments from shifted raw sums S_j = sum (x - x0)^j over n values.
-struct RawMom {
-  double s1, s2, s3, s4;
-  int n;
-};
-// sample std (ddof=1); false -> null (n < 2).  `exact0`: the set is constant.
-__device__ __forceinline__ bool std1_raw(const RawMom& m, bool exact0, double& out) {
-  if (m.n < 2) return false;
-  if (exact0) {
-    out = 0.0;
-    return true;
-  }
-  const double v = (m.s2 - m.s1 * m.s1 / (double)m.n) / (double)(m.n - 1);
-  out = sqrt(v);
-  return true;
-}
-// central m2, m3, m4 (biased); exact zeros when s1..s4 are all zero
-__device__ __forceinline__ void central(const RawMom& m, double& m2, double& m3, double& m4) {
-  const double n = (double)m.n;
-  const double mu = m.s1 / n, a2 = m.s2 / n, a3 = m.s3 / n, a4 = m.s4 / n;
-  m2 = a2 - mu * mu;
-  m3 = a3 - 3.0 * mu * a2 + 2.0 * mu * mu * mu;
-  m4 = a4 - 4.0 * mu * a3 + 6.0 * mu * mu * a2 - 3.0 * mu * mu * mu * mu;
-}
-// S2 skew / kurtosis from raw sums (x0 a member, so a constant set gives m2 == 0)
-__device__ __forceinline__ void skew_kurt(const RawMom& m, double& sk, double& ku) {
-  double m2, m3, m4;
-  central(m, m2, m3, m4);
-  if (__builtin_isnan(m2) || m2 == 0.0) {
-    sk = ku = qnan();
-    return;
-  }
-  sk = (m.n == 2) ? 0.0 : m3 / (m2 * sqrt(m2));
-  ku = m4 / (m2 * m2) - 3.0;
-}
-// S3 Pearson from shifted sums over n pairs (shift = a member pair)
-__device__ __forceinline__ double pearson_raw(int n, double sx, double sy, double sxx, double syy, double sxy) {
-  if (n < 2) return qnan();
-  const double dn = (double)n;
-  const double vx = sxx - sx * sx / dn, vy = syy - sy * sy / dn;
-  if (!(vx != 0.0) || !(vy != 0.0)) return (__builtin_isnan(vx) || __builtin_isnan(vy)) ? qnan() : qnan();
-  return (sxy - sx * sy / dn) / sqrt(vx * vy);
 }
 
 // a register value the optimiser must treat as new (no instruction emitted)
@@ -191,15 +150,16 @@ __device__ __forceinline__ void gsort256(T (&a)[K]) {
   }
 }
 
-// Family groups, one kernel instantiation each.  A group's registers are allocated for
-// that group alone (one kernel holding all 58 factors needs > 256 VGPRs); the planes a
-// group reads are re-read by the next group, which costs nothing measurable here: the
-// stage is ALU/latency bound at ~1/50 of the HBM roofline.
-constexpr uint32_t G_HL = F_OLS | F_MOMH;                                  // high, low
-constexpr uint32_t G_RET = F_SEG | F_ORD | F_ORDV | F_MOMR | F_TRD;         // open, close, volume
-constexpr uint32_t G_CV = F_MOMV | F_SUMV | F_SUMC | F_CORR;               // close, volume
-constexpr uint32_t G_LVL = F_LVL | F_PDF;                                  // close, volume
-constexpr uint32_t kGroups[4] = {G_HL, G_RET, G_CV, G_LVL};
+// Family groups of the 16-lane kernel, one instantiation each: the families that need
+// order statistics (sorts).  Everything else (SEG, OLS, MOM*, SUM*, CORR, TRD) runs one
+// lane per stock-day in mff_stage1s.hip; G_HL (OLS, MOMH) stays instantiable here for
+// the family-cost tools.  A group's registers
+// are allocated for that group alone; the planes a group reads are re-read by the next
+// launch, which costs little here: the stage is VALU bound.
+[[maybe_unused]] constexpr uint32_t G_HL = F_OLS | F_MOMH;  // high, low
+constexpr uint32_t G_ORD = F_ORD | F_ORDV;   // open, close, volume
+constexpr uint32_t G_LVL = F_LVL | F_PDF;    // close, volume
+constexpr uint32_t kGroups[2] = {G_ORD, G_LVL};
 
 template <uint32_t SET>
 __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
@@ -1079,7 +1039,11 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
     MFF_LAUNCH_CHECK();
     return 0;
   }
-  for (int gi = 0; gi < 4; ++gi) {
+  {
+    const int rc = launch_serial(fld, valid, S, D, a.row, a.fam, val, state, st);
+    if (rc != 0) return rc;
+  }
+  for (int gi = 0; gi < 2; ++gi) {
     const uint32_t set = g16::kGroups[gi];
     if (!(a.fam & set)) continue;
     g16::GArgs b = a;  // this launch stores its own group's rows (and the queries) only
@@ -1087,9 +1051,7 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
       if (!(kFactorFamily[i] & set)) b.row[i] = -1;
     if (!(set & F_PDF)) b.pdfq = nullptr;
     switch (gi) {
-      case 0: hipLaunchKernelGGL(g16::k_stage1g<g16::G_HL>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
-      case 1: hipLaunchKernelGGL(g16::k_stage1g<g16::G_RET>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
-      case 2: hipLaunchKernelGGL(g16::k_stage1g<g16::G_CV>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
+      case 0: hipLaunchKernelGGL(g16::k_stage1g<g16::G_ORD>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
       default: hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
     }
     MFF_LAUNCH_CHECK();

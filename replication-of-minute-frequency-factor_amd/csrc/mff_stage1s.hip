@@ -1,0 +1,629 @@
+// mff_stage1s.hip — stage 1, one lane per stock-day: the streaming families.
+//
+// Lane = stock s of day d (a 256-thread block is 256 consecutive stocks of one day, so
+// every factor row store val[row][d][s] is one 512-byte line per wave).  Each lane walks
+// its own 240 bars in order, four at a time (one float4 per plane, the next four
+// prefetched), carrying the previous present bar and the running sums in registers:
+// nothing crosses lanes, no reduction, and every finishing formula runs once per
+// stock-day instead of once per 16-lane group (mff_stage1g.hip).  The families here are
+// the ones that need no order statistics (the sorted families stay 16 lanes per
+// stock-day):
+//
+//  SEG   session endpoints from the mask bits, values loaded directly   CM:10-90
+//  MOMR  returns r = c/o - 1: std / up / down / skew / kurt, sums shifted by the first
+//        return (a member, so a constant set gives exact zeros, C3)      CM:518-687
+//  TRD   return-volume sums over the minute windows                    CM:1203-1406
+//  MOMV  volume moments shifted by the first volume                     CM:485-496,690-729
+//  SUMV  volume sums over the minute windows                            CM:764-831,1251-1306
+//  SUMC  Amihud over the previous present bar                           CM:734-761
+//  CORR  six Pearson sums; prv/pv/pvd/pvl shifted by the first present pair (loaded
+//        directly), prvr/pvr by their first pair (captured in the walk)  CM:834-932
+//  OLS   50-minute windows (t-50, t]: running prefix sums of (low - low0, high - high0)
+//        and their products, and the same prefix 50 bars behind (the bars leaving the
+//        window are walked again: identical additions, so the difference is the g16
+//        kernel's window sum); a window needs all 50 bars; constancy from the last bar
+//        whose low / high differs from the previous bar                 CM:93-376
+//  MOMH  high / low moments shifted by the first ratio                   CM:499-515
+//
+// Semantics are those of the 16-lane kernel; the bar
+// minute m is wave-uniform, so the minute-window tests are scalar branches.
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/mff.h"
+#include "mff_internal.h"
+#include "mff_stats.h"
+#include "mff_wave.h"
+
+namespace mff {
+namespace s1s {
+
+struct SArgs {
+  const float* fld[5];
+  const uint32_t* mask;
+  double* val;
+  uint8_t* state;
+  int S, D;
+  uint32_t fam;
+  int8_t row[NF];
+};
+
+// the serial families, in launch groups (each gets its own register allocation)
+constexpr uint32_t kSerA = F_SEG | F_MOMR | F_TRD;             // open, close, volume
+constexpr uint32_t kSerB = F_MOMV | F_SUMV | F_SUMC | F_CORR;  // close, volume
+constexpr uint32_t kSerH = F_OLS | F_MOMH;                     // high, low
+constexpr uint32_t kSerial = kSerA | kSerB | kSerH;
+
+// ---- presence bits of one stock-day: 8 words, bit m%32 of word m/32 (compile-time
+// word indices only, so the array stays in registers)
+struct Mask {
+  uint32_t w[8];
+  __device__ __forceinline__ static uint32_t rng(int w, int lo, int hi) {  // bits of word w in [lo, hi]
+    const int a = max(lo - 32 * w, 0), b = min(hi - 32 * w, 31);
+    if (b < a) return 0u;
+    return ((0xFFFFFFFFu >> (31 - b)) >> a) << a;
+  }
+  __device__ __forceinline__ int count_in(int lo, int hi) const {
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += __builtin_popcount(w[i] & rng(i, lo, hi));
+    return t;
+  }
+  __device__ __forceinline__ bool any_in(int lo, int hi) const {
+    uint32_t t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t |= w[i] & rng(i, lo, hi);
+    return t != 0u;
+  }
+  __device__ __forceinline__ int first_in(int lo, int hi) const {
+    int r = -1;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+      const uint32_t x = w[i] & rng(i, lo, hi);
+      if (x) r = 32 * i + __builtin_ctz(x);
+    }
+    return r;
+  }
+  __device__ __forceinline__ int last_in(int lo, int hi) const {
+    int r = -1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t x = w[i] & rng(i, lo, hi);
+      if (x) r = 32 * i + 31 - __builtin_clz(x);
+    }
+    return r;
+  }
+  __device__ __forceinline__ bool has(int m) const {  // m compile-time
+    return (w[m >> 5] >> (m & 31)) & 1u;
+  }
+};
+
+// planes a family set reads (bit p = plane p: open, high, low, close, volume)
+__host__ __device__ constexpr uint32_t kPlanes(uint32_t set) {
+  return ((set & (F_SEG | F_MOMR | F_TRD)) ? 1u : 0u) | ((set & (F_OLS | F_MOMH)) ? 6u : 0u) |
+         ((set & (F_SEG | F_MOMR | F_TRD | F_SUMC | F_CORR)) ? 8u : 0u) |
+         ((set & (F_TRD | F_MOMV | F_SUMV | F_SUMC | F_CORR)) ? 16u : 0u);
+}
+typedef __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// one 16-byte load (a native vector type keeps it one global_load_dwordx4)
+typedef float vf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4(const float4* p) {
+  const vf4 x = *reinterpret_cast<const vf4*>(p);
+  return make_float4(x.x, x.y, x.z, x.w);
+}
+
+template <uint32_t SET>
+__global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
+  constexpr uint32_t needO = F_SEG | F_MOMR | F_TRD;
+  constexpr uint32_t needC = F_SEG | F_MOMR | F_TRD | F_SUMC | F_CORR;
+  constexpr uint32_t needV = F_TRD | F_MOMV | F_SUMV | F_SUMC | F_CORR;
+  constexpr uint32_t needHL = F_OLS | F_MOMH;
+  const uint32_t fam = a.fam & SET;
+  const int ntile = (a.S + 255) / 256;
+  const int d = blockIdx.x / ntile;
+  const int s0 = (blockIdx.x % ntile) * 256;
+  const int s = s0 + (int)threadIdx.x;
+  // every lane walks (with LDS staging a lane also fetches other lanes' rows); lanes past
+  // the last stock walk a copy of it and store nothing
+  const bool act = s < a.S;
+  const size_t plane = (size_t)a.D * a.S;
+  const size_t sd = (size_t)d * a.S + (act ? s : a.S - 1);
+
+  auto put = [&](int f, double x, uint32_t st) {
+    const int r = a.row[f];
+    if (r >= 0) {
+      a.val[(size_t)r * plane + sd] = x;
+      a.state[(size_t)r * plane + sd] = (uint8_t)st;
+    }
+  };
+  auto val = [&](int f, double x) { put(f, x, MFF_STATE_VALUE); };
+  auto nul = [&](int f) { put(f, 0.0, MFF_STATE_NULL); };
+  auto absent = [&](int f) { put(f, 0.0, MFF_STATE_ABSENT); };
+
+  Mask M;
+  {
+    const uint4* mp = reinterpret_cast<const uint4*>(a.mask + sd * 8);
+    const uint4 m0 = mp[0], m1 = mp[1];
+    M.w[0] = m0.x; M.w[1] = m0.y; M.w[2] = m0.z; M.w[3] = m0.w;
+    M.w[4] = m1.x; M.w[5] = m1.y; M.w[6] = m1.z; M.w[7] = m1.w;
+  }
+  const int n = M.count_in(0, NBAR - 1);
+  // suspended stock-days (n == 0) walk bar 0 as a stand-in and store ABSENT at the end
+  const int fb = max(M.first_in(0, NBAR - 1), 0);
+  const int f2 = M.first_in(fb + 1, NBAR - 1);
+  const float* O = a.fld[0] + sd * NBAR;
+  const float* C = a.fld[3] + sd * NBAR;
+  const float* V = a.fld[4] + sd * NBAR;
+
+  // ---------------------------------------------------------------- shifts
+  double x0r = 0.0, x0v = 0.0;
+  double x1 = 0, y1 = 0, x2 = 0, y2 = 0, x3 = 0, y3 = 0, x4 = 0, y4 = 0;
+  if (fam & (F_MOMR | F_TRD)) x0r = (double)C[fb] / (double)O[fb] - 1.0;
+  if (fam & (F_MOMV | F_SUMV)) x0v = (double)V[fb];
+  const float* Hp = a.fld[1] + sd * NBAR;
+  const float* Lp = a.fld[2] + sd * NBAR;
+  double x0 = 0.0, y0 = 0.0, xh0 = 0.0;  // OLS shifts (low, high at the first bar), MOMH
+  if (fam & (F_OLS | F_MOMH)) {
+    x0 = (double)Lp[fb];
+    y0 = (double)Hp[fb];
+    xh0 = y0 / x0;
+  }
+  if (fam & F_CORR) {
+    const double cf1 = (double)C[fb], vf1 = (double)V[fb];
+    const double cf2 = f2 >= 0 ? (double)C[f2] : 0.0, vf2 = f2 >= 0 ? (double)V[f2] : 0.0;
+    x1 = (cf2 - cf1) / cf1; y1 = vf2;  // prv: (pct_change(close), volume)
+    x2 = cf1; y2 = vf1;                // pv
+    x3 = cf2; y3 = vf1;                // pvd: (close, volume.shift(1))
+    x4 = cf1; y4 = vf2;                // pvl: (close, volume.shift(-1))
+  }
+
+  // ---------------------------------------------------------------- accumulators
+  double sumv = 0.0;
+  // MOMR
+  double s1 = 0, s2 = 0, s3 = 0, s4 = 0, u1 = 0, u2 = 0, w1 = 0, w2 = 0;
+  double umn = __builtin_inf(), umx = -__builtin_inf(), wmn = __builtin_inf(), wmx = -__builtin_inf();
+  int nu = 0, ndn = 0;
+  // TRD
+  double vT20 = 0, vT50 = 0, rT20 = 0, rT50 = 0, vH20 = 0, vH50 = 0, a20 = 0, n20 = 0, q20 = 0, a50 = 0;
+  // MOMV
+  double t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+  // SUMV
+  double spre = 0, scls = 0, shead = 0, stail = 0;
+  // SUMC
+  double amh = 0;
+  // CORR: pv, prv, pvd, pvl, prvr, pvr
+  double P[6][5];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) P[i][j] = 0.0;
+  double x5 = 0, y5 = 0, x6 = 0;
+  int nzc = 0;
+  // carries: previous present bar, previous present non-zero-volume bar
+  float cp = 1.f, vp = 0.f, czp = 1.f, vzp = 1.f;
+  bool hp = false, hz = false;
+
+  // OLS: prefix through this bar (R*) and through the bar 50 back (Q*)
+  double Rx = 0, Ry = 0, Rxx = 0, Ryy = 0, Rxy = 0, Qx = 0, Qy = 0, Qxx = 0, Qyy = 0, Qxy = 0;
+  int cR = 0, cQ = 0, lcx = -1, lcy = -1;
+  float plo = 0.f, phi = 0.f;
+  bool hph = false;
+  double sq = 0, scs = 0, scr = 0, bd1 = 0, bd2 = 0, b0 = 0, bl = 0;
+  int W = 0, Wq = 0;
+  // MOMH
+  double hs1 = 0, hs2 = 0;
+
+  auto olsbar = [&](int m, bool pk, float hf, float lf, bool lpk, float lhf, float llf) {
+    if (pk) {
+      if (fam & F_OLS) {
+        const double dx = (double)lf - x0, dy = (double)hf - y0;
+        Rx += dx; Ry += dy; Rxx += dx * dx; Ryy += dy * dy; Rxy += dx * dy; ++cR;
+        if (hph && lf != plo) lcx = m;
+        if (hph && hf != phi) lcy = m;
+        plo = lf; phi = hf; hph = true;
+      }
+      if (fam & F_MOMH) {
+        const double dd = (double)hf / (double)lf - xh0;
+        hs1 += dd; hs2 += dd * dd;
+      }
+    }
+    if (!(fam & F_OLS)) return;
+    if (lpk) {  // bar m - 50 leaves the window
+      const double dx = (double)llf - x0, dy = (double)lhf - y0;
+      Qx += dx; Qy += dy; Qxx += dx * dx; Qyy += dy * dy; Qxy += dx * dy; ++cQ;
+    }
+    if (m >= 49 && cR - cQ == 50) {  // window m-49..m, all 50 bars present (CM:129)
+      const double Sx = Rx - Qx, Sy = Ry - Qy, Sxx = Rxx - Qxx, Syy = Ryy - Qyy, Sxy = Rxy - Qxy;
+      const bool cx = lcx <= m - 49, cy = lcy <= m - 49;  // constant low / high
+      const double vx = cx ? 0.0 : (Sxx - Sx * Sx * 0.02) * 0.02;
+      const double vy = cy ? 0.0 : (Syy - Sy * Sy * 0.02) * 0.02;
+      const double cv = (cx || cy) ? 0.0 : (Sxy - Sx * Sy * 0.02) * 0.02;
+      // beta = cov / var_x, or mean_y / mean_x when var_x == 0 (CM:131-134)
+      const bool vz = vx != 0.0;
+      const double beta = (vz ? cv : y0 + Sy * 0.02) / (vz ? vx : x0 + Sx * 0.02);
+      const double prod = vx * vy;
+      if (prod != 0.0) {
+        const double ip = 1.0 / prod;
+        sq += sqrt(cv) * ip;          // cov**0.5 / (vx*vy)   CM:137
+        scs += cv * cv * ip;          // cov**2 / (vx*vy)     CM:212
+        scr += cv * sqrt(prod) * ip;  // cov / (vx*vy)**0.5   CM:261
+        ++Wq;
+      }
+      if (W == 0) b0 = beta;  // betas shifted by the first one (a member)
+      const double db = beta - b0;
+      bd1 += db; bd2 += db * db;
+      bl = beta;
+      ++W;
+    }
+  };
+
+  auto acc5 = [](double (&p)[5], double dx, double dy) {
+    p[0] += dx; p[1] += dy; p[2] += dx * dx; p[3] += dy * dy; p[4] += dx * dy;
+  };
+
+  auto bar = [&](int m, bool pk, float of, float cf, float vf) {
+    if (!pk) return;
+    const double c = (double)cf, v = (double)vf;
+    if (fam & (F_MOMV | F_SUMV | F_TRD)) sumv += v;
+    if (fam & (F_MOMR | F_TRD)) {
+      const double r = c / (double)of - 1.0;  // close / open - 1
+      if (fam & F_MOMR) {
+        const double dd = r - x0r, d2 = dd * dd;
+        s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
+        if (tot_gt(r, 0.0)) { ++nu; u1 += dd; u2 += d2; umn = fmin(umn, r); umx = fmax(umx, r); }
+        if (tot_lt(r, 0.0)) { ++ndn; w1 += dd; w2 += d2; wmn = fmin(wmn, r); wmx = fmax(wmx, r); }
+      }
+      if (fam & F_TRD) {
+        if (m >= 220) { vT20 += v; rT20 += v * r; }
+        if (m >= 190) { vT50 += v; rT50 += v * r; }
+        if (m <= 50) {
+          const double iw = 1.0 / v;  // inf when v = 0: r/0 semantics
+          const double ta = r * iw;
+          vH50 += v; a50 += ta;
+          if (m <= 20) {
+            vH20 += v; a20 += ta;
+            n20 += (r < 0.0 ? -r : 0.0) * iw;
+            q20 += (r > 0.0 ? r : 0.0) * iw;
+          }
+        }
+      }
+    }
+    if (fam & F_MOMV) {
+      const double dd = v - x0v, d2 = dd * dd;
+      t1 += dd; t2 += d2; t3 += d2 * dd; t4 += d2 * d2;
+    }
+    if (fam & F_SUMV) {
+      if (m <= 236) spre += v;
+      if (m >= 237) scls += v;
+      if (m <= 30) shead += v;
+      if (m >= 210) stail += v;
+    }
+    if (fam & F_SUMC) {
+      if (hp && vf > 0.0f) amh += fabs(c - (double)cp) / ((double)cp * v);
+    }
+    if (fam & F_CORR) {
+      acc5(P[0], c - x2, v - y2);  // pv
+      if (hp) {
+        const double pc = (c - (double)cp) / (double)cp;
+        acc5(P[1], pc - x1, v - y1);           // prv
+        acc5(P[2], c - x3, (double)vp - y3);   // pvd
+        acc5(P[3], (double)cp - x4, v - y4);   // pvl: (close of the previous bar, this volume)
+      }
+      if (vf != 0.0f) {  // rows with volume != 0 (CM:855-866, 924-930)
+        if (hz) {
+          const double pcz = (c - (double)czp) / (double)czp;
+          const double pvz = (v - (double)vzp) / (double)vzp;
+          if (nzc == 1) { x5 = pcz; y5 = pvz; x6 = c; }  // first pair: the shifts
+          const double dy = pvz - y5;
+          acc5(P[4], pcz - x5, dy);  // prvr
+          acc5(P[5], c - x6, dy);    // pvr
+        }
+        czp = cf; vzp = vf; hz = true; ++nzc;
+      }
+    }
+    cp = cf; vp = vf; hp = true;
+  };
+
+  // ---------------------------------------------------------------- the walk
+  // Quads (4 bars: one float4 per plane) in pairs, the next pair in flight while this
+  // one is used.  OLS also walks the bars leaving its window: bars 4q-50 .. 4q-47 are
+  // quad q-13 (.z .w) and quad q-12 (.x .y), kept in a rolling set of lag quads.
+  const bool lo_ = (fam & needO) != 0u, lc_ = (fam & needC) != 0u, lv_ = (fam & needV) != 0u;
+  const bool lh_ = (fam & needHL) != 0u, lag_ = (fam & F_OLS) != 0u;
+  const float4* O4 = reinterpret_cast<const float4*>(O);
+  const float4* C4 = reinterpret_cast<const float4*>(C);
+  const float4* V4 = reinterpret_cast<const float4*>(V);
+  const float4* H4 = reinterpret_cast<const float4*>(Hp);
+  const float4* L4 = reinterpret_cast<const float4*>(Lp);
+  const float4 one4 = make_float4(1.f, 1.f, 1.f, 1.f), zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  struct Q4 {
+    float4 o, h, l, c, v;
+  };
+  auto ldq = [&](int q) {
+    Q4 r;
+    r.o = r.h = r.l = r.c = one4;
+    r.v = zero4;
+    if (lo_) r.o = ld4(O4 + q);
+    if (lh_) {
+      r.h = ld4(H4 + q);
+      r.l = ld4(L4 + q);
+    }
+    if (lc_) r.c = ld4(C4 + q);
+    if (lv_) r.v = ld4(V4 + q);
+    return r;
+  };
+  auto quad = [&](int m0, uint32_t pm, uint32_t lm, const Q4& x, const float4& lh0, const float4& ll0,
+                  const float4& lh1, const float4& ll1) {
+    // lagged bars: m0-50, m0-49 = (lh0, ll0).z .w; m0-48, m0-47 = (lh1, ll1).x .y
+    if (fam & kSerH) {
+      olsbar(m0 + 0, pm & 1u, x.h.x, x.l.x, lm & 1u, lh0.z, ll0.z);
+      olsbar(m0 + 1, (pm >> 1) & 1u, x.h.y, x.l.y, (lm >> 1) & 1u, lh0.w, ll0.w);
+      olsbar(m0 + 2, (pm >> 2) & 1u, x.h.z, x.l.z, (lm >> 2) & 1u, lh1.x, ll1.x);
+      olsbar(m0 + 3, (pm >> 3) & 1u, x.h.w, x.l.w, (lm >> 3) & 1u, lh1.y, ll1.y);
+    }
+    if (fam & (kSerA | kSerB)) {
+      bar(m0 + 0, pm & 1u, x.o.x, x.c.x, x.v.x);
+      bar(m0 + 1, (pm >> 1) & 1u, x.o.y, x.c.y, x.v.y);
+      bar(m0 + 2, (pm >> 2) & 1u, x.o.z, x.c.z, x.v.z);
+      bar(m0 + 3, (pm >> 3) & 1u, x.o.w, x.c.w, x.v.w);
+    }
+  };
+  uint32_t mw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mw[i] = M.w[i];
+  if constexpr (!(SET & F_OLS)) {
+    // LDS staging by LDS-DMA: each wave stages its 64 rows 16 bars (4 quads, 64 B per
+    // row and plane) at a time; one wave-instruction fetches 16 rows x 64 B.  The next
+    // chunk is in flight while this one is used.  The image is [row][quad] with the quad
+    // slot XOR-swizzled by (row >> 2) & 3 on the SOURCE address (the DMA destination is
+    // lane-linear), so each lane's ds_read_b128 of its own row is bank-conflict free.
+    constexpr uint32_t PLM = kPlanes(SET);
+    constexpr int NP = __builtin_popcount(PLM);
+    __shared__ __attribute__((aligned(16))) float4 sbuf[4][NP][256];
+    const int lane = (int)(threadIdx.x & 63u), wave = (int)(threadIdx.x >> 6);
+    float4(*sb)[256] = sbuf[wave];
+    const float* pbase[NP];
+    {
+      int pi = 0;
+#pragma unroll
+      for (int p = 0; p < 5; ++p)
+        if ((PLM >> p) & 1u) pbase[pi++] = a.fld[p];
+    }
+    const int rowbase = s0 + 64 * wave;
+    auto dma = [&](int c) {
+#pragma unroll
+      for (int pi = 0; pi < NP; ++pi)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * i + (lane >> 2);
+          const int k = (lane & 3) ^ ((r >> 2) & 3);
+          const size_t row = (size_t)d * a.S + min(rowbase + r, a.S - 1);
+          const float* src = pbase[pi] + row * NBAR + 16 * c + 4 * k;
+          __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)&sb[pi][64 * i], 16, 0, 0);
+        }
+    };
+    const int sw = (lane >> 2) & 3;
+    dma(0);
+    for (int w = 0; w < 8; ++w) {
+      const uint32_t bits = mw[0];
+      const int nc = (w == 7) ? 1 : 2;  // bars 224..239: one chunk
+      for (int h = 0; h < nc; ++h) {
+        const int c = 2 * w + h;
+        float4 X[NP][4];
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) X[pi][k] = sb[pi][4 * lane + (k ^ sw)];
+        // the reads have returned before the DMA refills the buffer
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (c + 1 < NBAR / 16) dma(c + 1);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          Q4 x;
+          x.o = x.h = x.l = x.c = one4;
+          x.v = zero4;
+          int pi = 0;
+#pragma unroll
+          for (int p = 0; p < 5; ++p)
+            if ((PLM >> p) & 1u) {
+              const float4 t = X[pi++][k];
+              if (p == 0) x.o = t;
+              if (p == 1) x.h = t;
+              if (p == 2) x.l = t;
+              if (p == 3) x.c = t;
+              if (p == 4) x.v = t;
+            }
+          quad(16 * c + 4 * k, bits >> (16 * h + 4 * k), 0u, x, one4, one4, one4, one4);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 7; ++i) mw[i] = mw[i + 1];
+    }
+  } else {
+    uint32_t pw1 = 0u, pw2 = 0u;  // mask words w-1, w-2
+    Q4 n0 = ldq(0), n1 = ldq(1);
+    float4 lah = one4, lal = one4, nbh = one4, nbl = one4, nch = one4, ncl = one4;
+    for (int w = 0; w < 8; ++w) {
+      const uint32_t bits = mw[0];
+      const uint32_t lbits = (pw1 << 18) | (pw2 >> 14);  // bit i: bar 32w + i - 50
+      const int np = (w == 7) ? 2 : 4;                   // bars 224..239: two pairs
+      for (int jj = 0; jj < np; ++jj) {
+        const int qq = 8 * w + 2 * jj;
+        const Q4 A = n0, B = n1;
+        if (qq + 2 < NBAR / 4) {
+          n0 = ldq(qq + 2);
+          n1 = ldq(qq + 3);
+        }
+        const float4 lbh = nbh, lbl = nbl, lch = nch, lcl = ncl;  // quads qq-12, qq-11
+        if (lag_ && qq >= 10) {
+          nbh = ld4(H4 + qq - 10); nbl = ld4(L4 + qq - 10);
+          nch = ld4(H4 + qq - 9); ncl = ld4(L4 + qq - 9);
+        }
+        const uint32_t pm = bits >> (8 * jj), lm = lbits >> (8 * jj);
+        quad(4 * qq, pm, lm, A, lah, lal, lbh, lbl);
+        quad(4 * qq + 4, pm >> 4, lm >> 4, B, lbh, lbl, lch, lcl);
+        lah = lch;
+        lal = lcl;
+      }
+  #pragma unroll
+      for (int i = 0; i < 7; ++i) mw[i] = mw[i + 1];
+      pw2 = pw1;
+      pw1 = bits;
+    }
+  }
+
+  // ---------------------------------------------------------------- finishing
+  if (!act) return;
+  if (n == 0) {  // suspended: every factor of the set is absent
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+      if (kFamOf(f) & fam) absent(f);
+    return;
+  }
+  if (fam & F_SEG) {
+    auto seg = [&](int f, int ma, int mb) {
+      const bool pa = M.has(ma), pb = M.has(mb);
+      if (!pa && !pb) { absent(f); return; }
+      val(f, (double)C[pb ? mb : ma] / (double)O[pa ? ma : mb]);
+    };
+    seg(0, 120, 239);  // mmt_pm
+    seg(1, 210, 239);  // mmt_last30
+    seg(3, 0, 119);    // mmt_am
+    seg(4, 30, 209);   // mmt_between
+    // mmt_paratio CM:42-60, C1: g(PM) - g(AM); one session gives g - g
+    const int af = M.first_in(0, 119), al = M.last_in(0, 119);
+    const int pf = M.first_in(120, 239), pl = M.last_in(120, 239);
+    double gA = 0.0, gP = 0.0;
+    if (af >= 0) gA = (double)C[al] / (double)O[af] - 1.0;
+    if (pf >= 0) gP = (double)C[pl] / (double)O[pf] - 1.0;
+    val(2, (af >= 0 && pf >= 0) ? gP - gA : (af >= 0 ? gA - gA : gP - gP));
+  }
+  if (fam & F_MOMR) {
+    const RawMom m{s1, s2, s3, s4, n};
+    double sdr;
+    const bool has_sdr = std1_raw(m, m.s1 == 0.0 && m.s2 == 0.0, sdr);
+    if (has_sdr) val(16, sdr); else nul(16);  // vol_return1min
+    double sup = 0.0, sdn = 0.0;  // fill_null(0)
+    std1_raw(RawMom{u1, u2, 0, 0, nu}, umn == umx, sup);
+    std1_raw(RawMom{w1, w2, 0, 0, ndn}, wmn == wmx, sdn);
+    val(17, sup);  // vol_upVol
+    val(19, sdn);  // vol_downVol
+    if (has_sdr) { val(18, sup / sdr); val(20, sdn / sdr); }
+    else { nul(18); nul(20); }
+    double sk, ku;
+    skew_kurt(m, sk, ku);
+    val(21, sk);
+    val(22, ku);
+    val(23, sk / ku);
+  }
+  if (fam & F_TRD) {
+    if (M.any_in(220, 239)) val(50, rT20 / (vT20 + 1.0)); else absent(50);
+    if (M.any_in(190, 239)) val(51, rT50 / (vT50 == 0.0 ? 1.0 : vT50)); else absent(51);
+    const int nh20 = M.count_in(0, 20), nh50 = M.count_in(0, 50);
+    if (nh20 > 0) {
+      val(54, vH20 * a20 / (double)nh20);
+      val(56, vH20 * n20 / (double)nh20);
+      val(57, vH20 * q20 / (double)nh20);
+    } else {
+      absent(54); absent(56); absent(57);
+    }
+    if (nh50 > 0) val(55, vH50 * a50 / (double)nh50); else absent(55);
+  }
+  if (fam & F_MOMV) {
+    const RawMom m{t1, t2, t3, t4, n};
+    double sdv;
+    if (std1_raw(m, m.s1 == 0.0 && m.s2 == 0.0, sdv)) val(14, sdv); else nul(14);
+    // skew/kurt of v / sum(v) == of v (scale-free); sum(v) = 0 -> shares NaN
+    double sk, ku;
+    skew_kurt(m, sk, ku);
+    if (sumv == 0.0) sk = ku = qnan();
+    val(24, sk);
+    val(25, ku);
+    val(26, sk / ku);
+  }
+  if (fam & F_SUMV) {
+    if (M.any_in(0, 236)) val(28, spre); else absent(28);
+    if (M.any_in(237, 239)) val(29, scls); else absent(29);
+    const double vfirst = x0v;
+    val(30, vfirst / sumv);
+    val(31, scls / sumv);
+    val(32, vfirst);
+    val(52, sumv > 0.0 ? shead / sumv : 0.125);
+    val(53, sumv > 0.0 ? stail / sumv : 0.125);
+  }
+  if (fam & F_SUMC) val(27, amh);  // liq_amihud_1min
+  if (fam & F_OLS) {
+    if (W > 0) {
+      const double bmean = b0 + bd1 / (double)W;
+      const bool has_std = W >= 2;
+      double bstd = 0.0;
+      if (has_std) bstd = sqrt((bd2 - bd1 * bd1 / (double)W) / (double)(W - 1));
+      if (has_std && tot_ne(bstd, 0.0) && Wq > 0)
+        val(5, (sq / (double)Wq) * (bl - bmean) / bstd);  // mmt_ols_qrs CM:156-171
+      else
+        val(5, 0.0);
+      val(6, Wq > 0 ? scs / (double)Wq : 0.0);  // mmt_ols_corr_square_mean
+      val(7, Wq > 0 ? scr / (double)Wq : 0.0);  // mmt_ols_corr_mean
+      val(8, bmean);                            // mmt_ols_beta_mean
+      val(9, (has_std && tot_gt(bstd, 0.0)) ? (bl - bmean) / bstd : bmean);  // beta_zscore_last
+    } else {
+#pragma unroll
+      for (int f = 5; f < 10; ++f) absent(f);
+    }
+  }
+  if (fam & F_MOMH) {
+    const RawMom m{hs1, hs2, 0, 0, n};
+    double sdv;
+    if (std1_raw(m, m.s1 == 0.0 && m.s2 == 0.0, sdv)) val(15, sdv); else nul(15);  // vol_range1min
+  }
+  if (fam & F_CORR) {
+    auto fin = [&](int f, int np, const double (&p)[5]) { val(f, pearson_raw(np, p[0], p[1], p[2], p[3], p[4])); };
+    fin(35, n, P[0]);      // corr_pv
+    fin(33, n - 1, P[1]);  // corr_prv
+    fin(36, n - 1, P[2]);  // corr_pvd
+    fin(37, n - 1, P[3]);  // corr_pvl
+    if (nzc > 0) {
+      fin(34, nzc - 1, P[4]);  // corr_prvr
+      fin(38, nzc - 1, P[5]);  // corr_pvr
+    } else {
+      absent(34); absent(38);
+    }
+  }
+}
+
+}  // namespace s1s
+
+// launch the serial kernel for the families of `fam` it covers (mff_stage1g.hip)
+int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
+                  uint32_t fam, double* val, uint8_t* state, hipStream_t st) {
+  using namespace s1s;
+  SArgs a;
+  memset(&a, 0, sizeof(a));
+  for (int f = 0; f < 5; ++f) a.fld[f] = fld[f];
+  a.mask = valid; a.val = val; a.state = state; a.S = S; a.D = D;
+  a.fam = fam & kSerial;
+  for (int i = 0; i < NF; ++i) a.row[i] = (kFactorFamily[i] & kSerial) ? row[i] : (int8_t)-1;
+  if (!a.fam) return 0;
+  const long long nblk = (long long)((S + 255) / 256) * D;
+  // a launch stages every plane of its set: planes the requested factors do not read may
+  // be NULL, so they alias one the launch does read (fetched, never used)
+  auto patched = [&](uint32_t set) {
+    SArgs b = a;
+    const uint32_t pl = kPlanes(set);
+    const float* any = nullptr;
+    for (int p = 0; p < 5; ++p)
+      if (((pl >> p) & 1u) && b.fld[p]) any = b.fld[p];
+    for (int p = 0; p < 5; ++p)
+      if (((pl >> p) & 1u) && !b.fld[p]) b.fld[p] = any;
+    return b;
+  };
+  if (a.fam & kSerA) hipLaunchKernelGGL(k_stage1s<kSerA>, dim3((unsigned)nblk), dim3(256), 0, st, patched(kSerA));
+  if (a.fam & kSerB) hipLaunchKernelGGL(k_stage1s<kSerB>, dim3((unsigned)nblk), dim3(256), 0, st, patched(kSerB));
+  if (a.fam & kSerH) hipLaunchKernelGGL(k_stage1s<kSerH>, dim3((unsigned)nblk), dim3(256), 0, st, patched(kSerH));
+  MFF_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace mff
