@@ -107,19 +107,9 @@ __host__ __device__ constexpr uint32_t kPlanes(uint32_t set) {
 typedef __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
-// one 16-byte load (a native vector type keeps it one global_load_dwordx4)
-typedef float vf4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ld4(const float4* p) {
-  const vf4 x = *reinterpret_cast<const vf4*>(p);
-  return make_float4(x.x, x.y, x.z, x.w);
-}
 
 template <uint32_t SET>
 __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
-  constexpr uint32_t needO = F_SEG | F_MOMR | F_TRD;
-  constexpr uint32_t needC = F_SEG | F_MOMR | F_TRD | F_SUMC | F_CORR;
-  constexpr uint32_t needV = F_TRD | F_MOMV | F_SUMV | F_SUMC | F_CORR;
-  constexpr uint32_t needHL = F_OLS | F_MOMH;
   const uint32_t fam = a.fam & SET;
   const int ntile = (a.S + 255) / 256;
   const int d = blockIdx.x / ntile;
@@ -327,32 +317,10 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
   };
 
   // ---------------------------------------------------------------- the walk
-  // Quads (4 bars: one float4 per plane) in pairs, the next pair in flight while this
-  // one is used.  OLS also walks the bars leaving its window: bars 4q-50 .. 4q-47 are
-  // quad q-13 (.z .w) and quad q-12 (.x .y), kept in a rolling set of lag quads.
-  const bool lo_ = (fam & needO) != 0u, lc_ = (fam & needC) != 0u, lv_ = (fam & needV) != 0u;
-  const bool lh_ = (fam & needHL) != 0u, lag_ = (fam & F_OLS) != 0u;
-  const float4* O4 = reinterpret_cast<const float4*>(O);
-  const float4* C4 = reinterpret_cast<const float4*>(C);
-  const float4* V4 = reinterpret_cast<const float4*>(V);
-  const float4* H4 = reinterpret_cast<const float4*>(Hp);
-  const float4* L4 = reinterpret_cast<const float4*>(Lp);
+  // Quads (4 bars: one float4 per plane); OLS also walks the bars leaving its window.
   const float4 one4 = make_float4(1.f, 1.f, 1.f, 1.f), zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
   struct Q4 {
     float4 o, h, l, c, v;
-  };
-  auto ldq = [&](int q) {
-    Q4 r;
-    r.o = r.h = r.l = r.c = one4;
-    r.v = zero4;
-    if (lo_) r.o = ld4(O4 + q);
-    if (lh_) {
-      r.h = ld4(H4 + q);
-      r.l = ld4(L4 + q);
-    }
-    if (lc_) r.c = ld4(C4 + q);
-    if (lv_) r.v = ld4(V4 + q);
-    return r;
   };
   auto quad = [&](int m0, uint32_t pm, uint32_t lm, const Q4& x, const float4& lh0, const float4& ll0,
                   const float4& lh1, const float4& ll1) {
@@ -373,15 +341,19 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
   uint32_t mw[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) mw[i] = M.w[i];
-  if constexpr (!(SET & F_OLS)) {
+  {
     // LDS staging by LDS-DMA: each wave stages its 64 rows 16 bars (4 quads, 64 B per
     // row and plane) at a time; one wave-instruction fetches 16 rows x 64 B.  The next
     // chunk is in flight while this one is used.  The image is [row][quad] with the quad
     // slot XOR-swizzled by (row >> 2) & 3 on the SOURCE address (the DMA destination is
     // lane-linear), so each lane's ds_read_b128 of its own row is bank-conflict free.
+    // OLS also stages chunk c-3 (its bars 2..15 are the bars 50 back of bars 0..13 of
+    // chunk c; bars 14, 15 of chunk c-4 are carried in registers).
     constexpr uint32_t PLM = kPlanes(SET);
     constexpr int NP = __builtin_popcount(PLM);
-    __shared__ __attribute__((aligned(16))) float4 sbuf[4][NP][256];
+    constexpr bool LAG = (SET & F_OLS) != 0u;
+    constexpr int NB = LAG ? 2 * NP : NP;  // images: the planes, then their lag copies
+    __shared__ __attribute__((aligned(16))) float4 sbuf[4][NB][256];
     const int lane = (int)(threadIdx.x & 63u), wave = (int)(threadIdx.x >> 6);
     float4(*sb)[256] = sbuf[wave];
     const float* pbase[NP];
@@ -392,7 +364,7 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
         if ((PLM >> p) & 1u) pbase[pi++] = a.fld[p];
     }
     const int rowbase = s0 + 64 * wave;
-    auto dma = [&](int c) {
+    auto dma = [&](int c, int img0) {
 #pragma unroll
       for (int pi = 0; pi < NP; ++pi)
 #pragma unroll
@@ -401,73 +373,63 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
           const int k = (lane & 3) ^ ((r >> 2) & 3);
           const size_t row = (size_t)d * a.S + min(rowbase + r, a.S - 1);
           const float* src = pbase[pi] + row * NBAR + 16 * c + 4 * k;
-          __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)&sb[pi][64 * i], 16, 0, 0);
+          __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)&sb[img0 + pi][64 * i], 16, 0, 0);
         }
     };
     const int sw = (lane >> 2) & 3;
-    dma(0);
-    for (int w = 0; w < 8; ++w) {
-      const uint32_t bits = mw[0];
-      const int nc = (w == 7) ? 1 : 2;  // bars 224..239: one chunk
-      for (int h = 0; h < nc; ++h) {
-        const int c = 2 * w + h;
-        float4 X[NP][4];
+    auto toq = [&](const float4 (&X)[NB][4], int img0, int k) {
+      Q4 x;
+      x.o = x.h = x.l = x.c = one4;
+      x.v = zero4;
+      int pi = 0;
 #pragma unroll
-        for (int pi = 0; pi < NP; ++pi)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) X[pi][k] = sb[pi][4 * lane + (k ^ sw)];
-        // the reads have returned before the DMA refills the buffer
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (c + 1 < NBAR / 16) dma(c + 1);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          Q4 x;
-          x.o = x.h = x.l = x.c = one4;
-          x.v = zero4;
-          int pi = 0;
-#pragma unroll
-          for (int p = 0; p < 5; ++p)
-            if ((PLM >> p) & 1u) {
-              const float4 t = X[pi++][k];
-              if (p == 0) x.o = t;
-              if (p == 1) x.h = t;
-              if (p == 2) x.l = t;
-              if (p == 3) x.c = t;
-              if (p == 4) x.v = t;
-            }
-          quad(16 * c + 4 * k, bits >> (16 * h + 4 * k), 0u, x, one4, one4, one4, one4);
+      for (int p = 0; p < 5; ++p)
+        if ((PLM >> p) & 1u) {
+          const float4 t = X[img0 + pi++][k];
+          if (p == 0) x.o = t;
+          if (p == 1) x.h = t;
+          if (p == 2) x.l = t;
+          if (p == 3) x.c = t;
+          if (p == 4) x.v = t;
         }
-      }
-#pragma unroll
-      for (int i = 0; i < 7; ++i) mw[i] = mw[i + 1];
-    }
-  } else {
+      return x;
+    };
+    Q4 carry;  // lag bars 14, 15 of chunk c-4 (in .z .w)
+    carry.o = carry.h = carry.l = carry.c = one4;
+    carry.v = zero4;
     uint32_t pw1 = 0u, pw2 = 0u;  // mask words w-1, w-2
-    Q4 n0 = ldq(0), n1 = ldq(1);
-    float4 lah = one4, lal = one4, nbh = one4, nbl = one4, nch = one4, ncl = one4;
+    dma(0, 0);
     for (int w = 0; w < 8; ++w) {
       const uint32_t bits = mw[0];
       const uint32_t lbits = (pw1 << 18) | (pw2 >> 14);  // bit i: bar 32w + i - 50
-      const int np = (w == 7) ? 2 : 4;                   // bars 224..239: two pairs
-      for (int jj = 0; jj < np; ++jj) {
-        const int qq = 8 * w + 2 * jj;
-        const Q4 A = n0, B = n1;
-        if (qq + 2 < NBAR / 4) {
-          n0 = ldq(qq + 2);
-          n1 = ldq(qq + 3);
+      const int nc = (w == 7) ? 1 : 2;                   // bars 224..239: one chunk
+      for (int h = 0; h < nc; ++h) {
+        const int c = 2 * w + h;
+        float4 X[NB][4];
+#pragma unroll
+        for (int ii = 0; ii < NB; ++ii)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) X[ii][k] = sb[ii][4 * lane + (k ^ sw)];
+        // the reads have returned before the DMA refills the buffers
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (c + 1 < NBAR / 16) {
+          dma(c + 1, 0);
+          if (LAG && c + 1 >= 3) dma(c - 2, NP);
         }
-        const float4 lbh = nbh, lbl = nbl, lch = nch, lcl = ncl;  // quads qq-12, qq-11
-        if (lag_ && qq >= 10) {
-          nbh = ld4(H4 + qq - 10); nbl = ld4(L4 + qq - 10);
-          nch = ld4(H4 + qq - 9); ncl = ld4(L4 + qq - 9);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const Q4 x = toq(X, 0, k);
+          if constexpr (LAG) {
+            const Q4 l1 = toq(X, NP, k);
+            const Q4 l0 = k > 0 ? toq(X, NP, k - 1) : carry;
+            quad(16 * c + 4 * k, bits >> (16 * h + 4 * k), lbits >> (16 * h + 4 * k), x, l0.h, l0.l, l1.h, l1.l);
+          } else {
+            quad(16 * c + 4 * k, bits >> (16 * h + 4 * k), 0u, x, one4, one4, one4, one4);
+          }
         }
-        const uint32_t pm = bits >> (8 * jj), lm = lbits >> (8 * jj);
-        quad(4 * qq, pm, lm, A, lah, lal, lbh, lbl);
-        quad(4 * qq + 4, pm >> 4, lm >> 4, B, lbh, lbl, lch, lcl);
-        lah = lch;
-        lal = lcl;
+        if constexpr (LAG) carry = toq(X, NP, 3);
       }
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < 7; ++i) mw[i] = mw[i + 1];
       pw2 = pw1;
       pw1 = bits;
