@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include "../../include/mff.h"
+#include "mff_fmath.h"
 #include "mff_internal.h"
 #include "mff_stats.h"
 #include "mff_wave.h"
@@ -150,7 +151,7 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
   // ---------------------------------------------------------------- shifts
   double x0r = 0.0, x0v = 0.0;
   double x1 = 0, y1 = 0, x2 = 0, y2 = 0, x3 = 0, y3 = 0, x4 = 0, y4 = 0;
-  if (fam & (F_MOMR | F_TRD)) x0r = (double)C[fb] / (double)O[fb] - 1.0;
+  if (fam & (F_MOMR | F_TRD)) x0r = fdiv((double)C[fb], (double)O[fb]) - 1.0;  // as in the walk
   if (fam & (F_MOMV | F_SUMV)) x0v = (double)V[fb];
   const float* Hp = a.fld[1] + sd * NBAR;
   const float* Lp = a.fld[2] + sd * NBAR;
@@ -158,12 +159,12 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
   if (fam & (F_OLS | F_MOMH)) {
     x0 = (double)Lp[fb];
     y0 = (double)Hp[fb];
-    xh0 = y0 / x0;
+    xh0 = fdiv(y0, x0);
   }
   if (fam & F_CORR) {
     const double cf1 = (double)C[fb], vf1 = (double)V[fb];
     const double cf2 = f2 >= 0 ? (double)C[f2] : 0.0, vf2 = f2 >= 0 ? (double)V[f2] : 0.0;
-    x1 = (cf2 - cf1) / cf1; y1 = vf2;  // prv: (pct_change(close), volume)
+    x1 = fdivr(cf2 - cf1, cf1, frcp(cf1)); y1 = vf2;  // prv: (pct_change(close), volume), as in the walk
     x2 = cf1; y2 = vf1;                // pv
     x3 = cf2; y3 = vf1;                // pvd: (close, volume.shift(1))
     x4 = cf1; y4 = vf2;                // pvl: (close, volume.shift(-1))
@@ -193,6 +194,7 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
   int nzc = 0;
   // carries: previous present bar, previous present non-zero-volume bar
   float cp = 1.f, vp = 0.f, czp = 1.f, vzp = 1.f;
+  double rcp_ = 1.0, rcz = 1.0, rvz = 1.0;  // their reciprocals (frcp)
   bool hp = false, hz = false;
 
   // OLS: prefix through this bar (R*) and through the bar 50 back (Q*)
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
         plo = lf; phi = hf; hph = true;
       }
       if (fam & F_MOMH) {
-        const double dd = (double)hf / (double)lf - xh0;
+        const double dd = fdiv((double)hf, (double)lf) - xh0;
         hs1 += dd; hs2 += dd * dd;
       }
     }
@@ -232,10 +234,10 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
       const double cv = (cx || cy) ? 0.0 : (Sxy - Sx * Sy * 0.02) * 0.02;
       // beta = cov / var_x, or mean_y / mean_x when var_x == 0 (CM:131-134)
       const bool vz = vx != 0.0;
-      const double beta = (vz ? cv : y0 + Sy * 0.02) / (vz ? vx : x0 + Sx * 0.02);
+      const double beta = fdiv(vz ? cv : y0 + Sy * 0.02, vz ? vx : x0 + Sx * 0.02);
       const double prod = vx * vy;
       if (prod != 0.0) {
-        const double ip = 1.0 / prod;
+        const double ip = frcp(prod);
         sq += sqrt(cv) * ip;          // cov**0.5 / (vx*vy)   CM:137
         scs += cv * cv * ip;          // cov**2 / (vx*vy)     CM:212
         scr += cv * sqrt(prod) * ip;  // cov / (vx*vy)**0.5   CM:261
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
     const double c = (double)cf, v = (double)vf;
     if (fam & (F_MOMV | F_SUMV | F_TRD)) sumv += v;
     if (fam & (F_MOMR | F_TRD)) {
-      const double r = c / (double)of - 1.0;  // close / open - 1
+      const double r = fdiv(c, (double)of) - 1.0;  // close / open - 1
       if (fam & F_MOMR) {
         const double dd = r - x0r, d2 = dd * dd;
         s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
@@ -269,7 +271,7 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
         if (m >= 220) { vT20 += v; rT20 += v * r; }
         if (m >= 190) { vT50 += v; rT50 += v * r; }
         if (m <= 50) {
-          const double iw = 1.0 / v;  // inf when v = 0: r/0 semantics
+          const double iw = vf == 0.0f ? __builtin_inf() : frcp(v);  // inf when v = 0: r/0 semantics
           const double ta = r * iw;
           vH50 += v; a50 += ta;
           if (m <= 20) {
@@ -290,30 +292,37 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
       if (m <= 30) shead += v;
       if (m >= 210) stail += v;
     }
+    // one reciprocal per close and per volume serves every quotient of this bar and
+    // of the bars that follow it (pct_change, Amihud)
+    double rc = 1.0, rv = 1.0;
+    if (fam & (F_SUMC | F_CORR)) {
+      rc = frcp(c);
+      rv = frcp(vf != 0.0f ? v : 1.0);
+    }
     if (fam & F_SUMC) {
-      if (hp && vf > 0.0f) amh += fabs(c - (double)cp) / ((double)cp * v);
+      if (hp && vf > 0.0f) amh += fabs(c - (double)cp) * (rcp_ * rv);  // |dc| / (c_prev * v)
     }
     if (fam & F_CORR) {
       acc5(P[0], c - x2, v - y2);  // pv
       if (hp) {
-        const double pc = (c - (double)cp) / (double)cp;
+        const double pc = fdivr(c - (double)cp, (double)cp, rcp_);
         acc5(P[1], pc - x1, v - y1);           // prv
         acc5(P[2], c - x3, (double)vp - y3);   // pvd
         acc5(P[3], (double)cp - x4, v - y4);   // pvl: (close of the previous bar, this volume)
       }
       if (vf != 0.0f) {  // rows with volume != 0 (CM:855-866, 924-930)
         if (hz) {
-          const double pcz = (c - (double)czp) / (double)czp;
-          const double pvz = (v - (double)vzp) / (double)vzp;
+          const double pcz = fdivr(c - (double)czp, (double)czp, rcz);
+          const double pvz = fdivr(v - (double)vzp, (double)vzp, rvz);
           if (nzc == 1) { x5 = pcz; y5 = pvz; x6 = c; }  // first pair: the shifts
           const double dy = pvz - y5;
           acc5(P[4], pcz - x5, dy);  // prvr
           acc5(P[5], c - x6, dy);    // pvr
         }
-        czp = cf; vzp = vf; hz = true; ++nzc;
+        czp = cf; vzp = vf; rcz = rc; rvz = rv; hz = true; ++nzc;
       }
     }
-    cp = cf; vp = vf; hp = true;
+    cp = cf; vp = vf; rcp_ = rc; hp = true;
   };
 
   // ---------------------------------------------------------------- the walk
