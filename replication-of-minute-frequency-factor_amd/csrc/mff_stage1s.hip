@@ -109,9 +109,11 @@ typedef __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
 
-template <uint32_t SET>
+// FULL: every family of SET is requested (the usual case), so the family tests fold
+// away at compile time instead of branching per bar
+template <uint32_t SET, bool FULL>
 __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
-  const uint32_t fam = a.fam & SET;
+  const uint32_t fam = FULL ? SET : (a.fam & SET);
   const int ntile = (a.S + 255) / 256;
   const int d = blockIdx.x / ntile;
   const int s0 = (blockIdx.x % ntile) * 256;
@@ -256,32 +258,47 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
   };
 
   auto bar = [&](int m, bool pk, float of, float cf, float vf) {
-    if (!pk) return;
-    const double c = (double)cf, v = (double)vf;
-    if (fam & (F_MOMV | F_SUMV | F_TRD)) sumv += v;
+    // Returns (MOMR, TRD) without branches: an absent bar gets r = x0r and v = 0, so its
+    // deviation, products and window sums are exact zeros, and every per-bar condition
+    // is a select; the minute windows are wave-uniform selects (only m <= 50, which
+    // needs a reciprocal, stays a uniform branch).  Straight-line code lets the
+    // scheduler overlap the dependent f64 chains of the four bars of a quad.
     if (fam & (F_MOMR | F_TRD)) {
-      const double r = fdiv(c, (double)of) - 1.0;  // close / open - 1
+      const double q = fdiv((double)cf, (double)of);  // close / open
+      const double r = pk ? q - 1.0 : x0r;
+      const double v = pk ? (double)vf : 0.0;
       if (fam & F_MOMR) {
         const double dd = r - x0r, d2 = dd * dd;
         s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
-        if (tot_gt(r, 0.0)) { ++nu; u1 += dd; u2 += d2; umn = fmin(umn, r); umx = fmax(umx, r); }
-        if (tot_lt(r, 0.0)) { ++ndn; w1 += dd; w2 += d2; wmn = fmin(wmn, r); wmx = fmax(wmx, r); }
+        const bool up = pk && r > 0.0, dn = pk && r < 0.0;  // r is finite (S11 needs no NaN case)
+        nu += up ? 1 : 0;
+        ndn += dn ? 1 : 0;
+        u1 += up ? dd : 0.0; u2 += up ? d2 : 0.0;
+        w1 += dn ? dd : 0.0; w2 += dn ? d2 : 0.0;
+        umn = (up && r < umn) ? r : umn; umx = (up && r > umx) ? r : umx;
+        wmn = (dn && r < wmn) ? r : wmn; wmx = (dn && r > wmx) ? r : wmx;
       }
       if (fam & F_TRD) {
-        if (m >= 220) { vT20 += v; rT20 += v * r; }
-        if (m >= 190) { vT50 += v; rT50 += v * r; }
+        const double vr = v * r;
+        const bool t20 = m >= 220, t50 = m >= 190;
+        vT20 += t20 ? v : 0.0; rT20 += t20 ? vr : 0.0;
+        vT50 += t50 ? v : 0.0; rT50 += t50 ? vr : 0.0;
         if (m <= 50) {
-          const double iw = vf == 0.0f ? __builtin_inf() : frcp(v);  // inf when v = 0: r/0 semantics
-          const double ta = r * iw;
+          const double iw = vf == 0.0f ? __builtin_inf() : frcp((double)vf);  // inf when v = 0: r/0 semantics
+          const double ta = pk ? r * iw : 0.0;
           vH50 += v; a50 += ta;
           if (m <= 20) {
             vH20 += v; a20 += ta;
-            n20 += (r < 0.0 ? -r : 0.0) * iw;
-            q20 += (r > 0.0 ? r : 0.0) * iw;
+            n20 += pk ? (r < 0.0 ? -r : 0.0) * iw : 0.0;
+            q20 += pk ? (r > 0.0 ? r : 0.0) * iw : 0.0;
           }
         }
       }
     }
+    if (!(fam & (F_MOMV | F_SUMV | F_SUMC | F_CORR))) return;
+    if (!pk) return;
+    const double c = (double)cf, v = (double)vf;
+    if (fam & (F_MOMV | F_SUMV)) sumv += v;
     if (fam & F_MOMV) {
       const double dd = v - x0v, d2 = dd * dd;
       t1 += dd; t2 += d2; t3 += d2 * dd; t4 += d2 * d2;
@@ -590,9 +607,13 @@ int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D
       if (((pl >> p) & 1u) && !b.fld[p]) b.fld[p] = any;
     return b;
   };
-  if (a.fam & kSerA) hipLaunchKernelGGL(k_stage1s<kSerA>, dim3((unsigned)nblk), dim3(256), 0, st, patched(kSerA));
-  if (a.fam & kSerB) hipLaunchKernelGGL(k_stage1s<kSerB>, dim3((unsigned)nblk), dim3(256), 0, st, patched(kSerB));
-  if (a.fam & kSerH) hipLaunchKernelGGL(k_stage1s<kSerH>, dim3((unsigned)nblk), dim3(256), 0, st, patched(kSerH));
+  const dim3 grid((unsigned)nblk), blk(256);
+  if ((a.fam & kSerA) == kSerA) hipLaunchKernelGGL((k_stage1s<kSerA, true>), grid, blk, 0, st, patched(kSerA));
+  else if (a.fam & kSerA) hipLaunchKernelGGL((k_stage1s<kSerA, false>), grid, blk, 0, st, patched(kSerA));
+  if ((a.fam & kSerB) == kSerB) hipLaunchKernelGGL((k_stage1s<kSerB, true>), grid, blk, 0, st, patched(kSerB));
+  else if (a.fam & kSerB) hipLaunchKernelGGL((k_stage1s<kSerB, false>), grid, blk, 0, st, patched(kSerB));
+  if ((a.fam & kSerH) == kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, true>), grid, blk, 0, st, patched(kSerH));
+  else if (a.fam & kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, false>), grid, blk, 0, st, patched(kSerH));
   MFF_LAUNCH_CHECK();
   return 0;
 }
