@@ -258,71 +258,99 @@ __global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
       c4 = *reinterpret_cast<const float4*>(a.lvl_close + sd * NBAR + i0);
       cu = *reinterpret_cast<const uint32_t*>(a.lvl_cum + sd * NBAR + i0);
     };
-    // bin levels j0 + 4g .. j0 + 4g + 3 of one stock-day
-    auto bin = [&](double clast, int nl, int j0, uint32_t cprev, const float4& c4, uint32_t cu) {
-      // bars at each level: cum - cum of the previous level (lane g-1's last byte)
-      const uint32_t left = g16::dpp_u<g16::ROW_SHR + 1>(cu) >> 24;
-      const uint32_t pc = (g == 0) ? cprev : left;
-      uint32_t w[4];
-      w[0] = (cu & 0xFFu) - pc;
-      w[1] = ((cu >> 8) & 0xFFu) - (cu & 0xFFu);
-      w[2] = ((cu >> 16) & 0xFFu) - ((cu >> 8) & 0xFFu);
-      w[3] = (cu >> 24) - ((cu >> 16) & 0xFFu);
-      const float cl[4] = {c4.x, c4.y, c4.z, c4.w};
-      uint64_t key[4];
-      int j[4];
+    // A level block: levels j0 + 4g .. j0 + 4g + 3 of one stock-day (one float4 of closes,
+    // one u32 of cumulative bar counts per lane).  NB blocks are binned together so that
+    // every search step issues 4*NB independent LDS reads before it waits.
+    struct Blk {
+      float4 c4;
+      uint32_t cu, cprev;
+      double clast;
+      int nl, j0;
+    };
+    auto bin = [&](const Blk* blk, int NB) {
+      uint64_t key[8];
+      int j[8];
+      uint32_t w[8];
       uint32_t inm = 0u;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool v = j0 + 4 * g + u < nl;
-        key[u] = ord64(clast / (double)cl[u]);
-        const bool bl = v && key[u] <= sl.L0;
-        const bool in = v && !bl && key[u] <= sl.qmax;
-        below += bl ? w[u] : 0u;
-        inm |= (in ? 1u : 0u) << u;
-        const bool gtmin = key[u] > sl.qmin;
-        const int bk = (in && gtmin) ? (int)((key[u] - sl.qmin) >> sl.sh) : 0;
-        j[u] = (in && gtmin) ? (int)sl.T[bk] - 1 : -1;
+      for (int bi = 0; bi < 2; ++bi) {
+        if (bi >= NB) break;
+        const Blk& B = blk[bi];
+        // bars at each level: cum - cum of the previous level (lane g-1's last byte)
+        const uint32_t left = g16::dpp_u<g16::ROW_SHR + 1>(B.cu) >> 24;
+        const uint32_t pc = (g == 0) ? B.cprev : left;
+        w[4 * bi + 0] = (B.cu & 0xFFu) - pc;
+        w[4 * bi + 1] = ((B.cu >> 8) & 0xFFu) - (B.cu & 0xFFu);
+        w[4 * bi + 2] = ((B.cu >> 16) & 0xFFu) - ((B.cu >> 8) & 0xFFu);
+        w[4 * bi + 3] = (B.cu >> 24) - ((B.cu >> 16) & 0xFFu);
+        const float cl[4] = {B.c4.x, B.c4.y, B.c4.z, B.c4.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = 4 * bi + u;
+          const bool v = B.j0 + 4 * g + u < B.nl;
+          key[i] = ord64(B.clast / (double)cl[u]);
+          const bool bl = v && key[i] <= sl.L0;
+          const bool in = v && !bl && key[i] <= sl.qmax;
+          below += bl ? w[i] : 0u;
+          inm |= (in ? 1u : 0u) << i;
+          const bool gtmin = key[i] > sl.qmin;
+          const int bk = (in && gtmin) ? (int)((key[i] - sl.qmin) >> sl.sh) : 0;
+          j[i] = (in && gtmin) ? (int)sl.T[bk] - 1 : -1;
+        }
       }
+      const int nc = 4 * NB;
       for (int bb = (1 << sl.steps) >> 1; bb > 0; bb >>= 1) {
-        uint64_t x[4];
+        uint64_t x[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = L1[min(j[u] + bb, nvc)];
+        for (int i = 0; i < 8; ++i)
+          if (i < nc) x[i] = L1[min(j[i] + bb, nvc)];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) j[u] = x[u] < key[u] ? j[u] + bb : j[u];
+        for (int i = 0; i < 8; ++i)
+          if (i < nc) j[i] = x[i] < key[i] ? j[i] + bb : j[i];
       }
-      uint64_t x[4];
+      uint64_t x[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) x[u] = L1[j[u] + 1];
+      for (int i = 0; i < 8; ++i)
+        if (i < nc) x[i] = L1[j[i] + 1];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if ((inm >> u) & 1u)
-          atomicAdd((unsigned long long*)&C[j[u] + 1],
-                    x[u] == key[u] ? ((uint64_t)w[u] << 32) : (uint64_t)w[u]);
+      for (int i = 0; i < 8; ++i)
+        if (i < nc && ((inm >> i) & 1u))
+          atomicAdd((unsigned long long*)&C[j[i] + 1], x[i] == key[i] ? ((uint64_t)w[i] << 32) : (uint64_t)w[i]);
     };
-    const int slast = S - 1;
-    uint64_t meta_n = a.lvl_meta[(size_t)d * S + min(grp, slast)];
-    float4 c4_n;
-    uint32_t cu_n;
-    load(min(grp, slast), 0, c4_n, cu_n);
-    for (int s = grp; s < S; s += 64) {  // group-uniform trip count
-      const uint64_t meta = meta_n;
-      const float4 c4 = c4_n;
-      const uint32_t cu = cu_n;
-      const int sn = min(s + 64, slast);  // prefetch (the last one is a harmless re-read)
-      meta_n = a.lvl_meta[(size_t)d * S + sn];
-      load(sn, 0, c4_n, cu_n);
-      const int nl = (int)(meta & 0xFFFFu);
-      if (nl == 0) continue;  // absent stock-day (group-uniform)
-      const double clast = (double)bitsf((uint32_t)(meta >> 32));
-      bin(clast, nl, 0, 0u, c4, cu);
-      for (int j0 = 64; j0 < nl; j0 += 64) {  // more than 64 levels (group-uniform)
-        float4 c4b;
-        uint32_t cub;
-        load(s, j0, c4b, cub);
-        const uint32_t cprev = a.lvl_cum[((size_t)d * S + s) * NBAR + j0 - 1];
-        bin(clast, nl, j0, cprev, c4b, cub);
+    auto first_blk = [&](int s, uint64_t meta, Blk& B) {
+      B.nl = (int)(meta & 0xFFFFu);
+      B.clast = (double)bitsf((uint32_t)(meta >> 32));
+      B.j0 = 0;
+      B.cprev = 0u;
+      load(s, 0, B.c4, B.cu);
+    };
+    // the rest of a stock-day's levels past the first 64 (group-uniform loop)
+    auto tail = [&](int s, const Blk& B0) {
+      for (int j0 = 64; j0 < B0.nl; j0 += 64) {
+        Blk B = B0;
+        B.j0 = j0;
+        load(s, j0, B.c4, B.cu);
+        B.cprev = a.lvl_cum[((size_t)d * S + s) * NBAR + j0 - 1];
+        bin(&B, 1);
       }
+    };
+    // the group's stocks s = grp + 64 i, two per step; the next pair is loaded while this
+    // one is binned (the last prefetch is a harmless re-read)
+    const int slast = S - 1;
+    Blk nA, nB;
+    first_blk(min(grp, slast), a.lvl_meta[(size_t)d * S + min(grp, slast)], nA);
+    first_blk(min(grp + 64, slast), a.lvl_meta[(size_t)d * S + min(grp + 64, slast)], nB);
+    for (int s = grp; s < S; s += 128) {  // group-uniform trip count
+      Blk P[2] = {nA, nB};
+      const int s2 = s + 64;
+      const int sn = min(s + 128, slast), sn2 = min(s + 192, slast);
+      first_blk(sn, a.lvl_meta[(size_t)d * S + sn], nA);
+      first_blk(sn2, a.lvl_meta[(size_t)d * S + sn2], nB);
+      if (s2 > slast) P[1].nl = 0;  // no second stock in this step
+      if (P[0].nl == 0 && P[1].nl == 0) continue;  // absent stock-days (group-uniform)
+      bin(P, 2);
+      if (P[0].nl > 64) tail(s, P[0]);
+      if (P[1].nl > 64) tail(s2, P[1]);
     }
     below = (uint32_t)__reduce_add_sync(~0ull, (int)below);
     if (lane_id() == 0) atomicAdd(&below_s, below);
