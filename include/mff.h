@@ -63,9 +63,10 @@ const char* mff_factor_name(int id);
  * factor_ids (host, nf entries): catalogue ids in output-row order.
  * pdf_query: float64 [5][D][S] workspace, required when any doc_pdf* id is requested
  * (the doc_pdf values are then produced by mff_pdf_* below), else may be NULL.
- * pdf_levels: mff_pdf_levels_bytes(S, D) bytes, required with doc_pdf (else NULL): the
- * per-stock-day level list (distinct closes, descending, with cumulative bar counts)
- * that mff_pdf_count / mff_pdf_rank_local bin against the sorted queries.
+ * pdf_levels: mff_pdf_levels_bytes(S, D) bytes, required with doc_pdf (else NULL): per
+ * day, the flat list of every stock-day's price levels as (key c_last/c_level, total-
+ * order u64; bars at the level, u8) that mff_pdf_count / mff_pdf_rank_local bin against
+ * the sorted queries (filled and counted by the call itself).
  * workspace: mff_stage1_workspace_bytes(S, D) bytes of device scratch (the list of
  * stock-days the exact general path finishes; zeroed by the call itself).
  * Environment MFF_STAGE1_IMPL=w64 selects the wave-per-stock-day kernel for everything.
@@ -86,7 +87,7 @@ int mff_stage1(const float* open, const float* high, const float* low,
  *             [5][D][S_loc] padded to S_all with NaN)
  *             -> q_sorted uint64 [nd][M], M = R*5*S_all <= 32767 (total-order keys)
  *   count:    this rank's keys c_last/c_b (from stage 1's pdf_levels: one key per
- *             distinct close, weighted by its bar count) against q_sorted
+ *             distinct close of a stock-day, weighted by its bar count) against q_sorted
  *             -> counts uint32 [nd][M][2] (n_less, n_eq) over local keys
  *   [R > 1: the caller sums `counts` over ranks (all-reduce), see INTEGRATION.md]
  *   finalize: own queries [5][D][S_loc] -> val/state rows pdf_rows[5] (host, -1 = skip)

@@ -9,10 +9,12 @@
 //   1. sort    — per day, the 5*S (x R ranks) queries as total-order u64 (mff_sort.h);
 //   2. count   — per (day, slice of <= PDF_ZQ sorted queries) workgroup, every local key
 //                c_last/c_b finds its position among the slice's queries (LDS bucket
-//                table + fixed-depth LDS binary search, 16 keys of a lane in lockstep) and
-//                bumps a packed (n_eq << 32 | n_less) LDS counter; a scan turns the
+//                table + fixed-depth LDS binary search) and bumps a packed
+//                (n_eq << 32 | n_less) LDS counter by its weight; a scan turns the
 //                counters into (n_less, n_eq) per sorted query position, over THIS
-//                rank's keys;
+//                rank's keys.  The keys are stage 1's flat per-day level list: one key
+//                per distinct close of a stock-day (rows with equal closes have equal
+//                keys), weighted by its bar count, so ~L << 240 keys per stock-day;
 //   [multi-GPU: counts are summed over ranks with one all-reduce]
 //   3. finalize — each own query looks its position up in its slice (LDS) and writes the
 //                rank.  With one rank, 2 and 3 run as one kernel (mff_pdf_rank_local):
@@ -25,7 +27,7 @@
 
 namespace mff {
 
-size_t pdf_levels_split(int S, int D, size_t* off_cum, size_t* off_meta);  // mff_stage1g.hip
+size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w);  // mff_stage1g.hip
 
 constexpr int PDF_MAXM = 32767;  // queries per day (all ranks)
 constexpr int PDF_ZQ = 9200;     // sorted queries per count workgroup (LDS: 16 B each)
@@ -203,9 +205,12 @@ __device__ __forceinline__ void pdf_slice_resolve(const PdfSlice& sl, const uint
 }
 
 struct PdfArgs {
-  const float* lvl_close;  // level side channel written by stage 1 (mff_pdf_levels_bytes)
-  const uint8_t* lvl_cum;
-  const uint64_t* lvl_meta;
+  // level side channel written by stage 1 (mff_pdf_levels_bytes): per-day entry counts,
+  // flat key / weight lists of capacity `cap` per day
+  const uint32_t* lvl_count;
+  const uint64_t* lvl_key;
+  const uint8_t* lvl_w;
+  size_t cap;
   const uint64_t* q_sorted;
   uint32_t* counts;       // [nd][M][2] (count phase) or NULL (fused finalize)
   const double* q_local;  // fused finalize: own queries [5][D][S]
@@ -241,116 +246,52 @@ __global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
 
   uint32_t below = 0u;
   if (sl.nv > 0) {
-    const int g = lane_id() & 15;
-    const int grp = threadIdx.x >> 4;  // 64 groups of 16 lanes, one stock each
-    // One stock-day per 16-lane group; its levels (distinct closes, ascending key
-    // c_last/c) 64 at a time, lane g holding levels 4g..4g+3 (one float4 + one u32 of
-    // cumulative counts), each binned with its bar count as weight.  The next
-    // stock-day's first 64 levels are loaded while this one is binned (slots past the
-    // level count are read but ignored: the side channel holds 240 per stock-day).
-    // Search: binary lifting from T[b]-1 (L1[T[b]-1] < key <= L1[T[b+1]]), so a step
-    // is one LDS read, one compare and one select.
+    // The day's level list is flat (stage 1 appends every stock-day's levels: key =
+    // c_last / c as ord64, weight = bars at the level), so a thread simply takes every
+    // blockDim-th entry, UNR at a time (their loads in flight together, their searches
+    // interleaved).  A key at or below Q[P0-1] only adds its weight to `below`; a key
+    // above the slice belongs to a later slice.  Search: binary lifting from T[b]-1
+    // (L1[T[b]-1] < key <= L1[T[b+1]]), one LDS read, compare and select per step.
+    constexpr int UNR = 4;
     const uint64_t* L1 = L + 1;
     const int nvc = sl.nv;  // L1[nv] = ~0 stops every probe past the end
-    auto load = [&](int s, int j0, float4& c4, uint32_t& cu) {
-      const size_t sd = (size_t)d * S + s;
-      const int i0 = min(j0 + 4 * g, NBAR - 4);  // lanes past slot 240 re-read (ignored)
-      c4 = *reinterpret_cast<const float4*>(a.lvl_close + sd * NBAR + i0);
-      cu = *reinterpret_cast<const uint32_t*>(a.lvl_cum + sd * NBAR + i0);
-    };
-    // A level block: levels j0 + 4g .. j0 + 4g + 3 of one stock-day (one float4 of closes,
-    // one u32 of cumulative bar counts per lane).  NB blocks are binned together so that
-    // every search step issues 4*NB independent LDS reads before it waits.
-    struct Blk {
-      float4 c4;
-      uint32_t cu, cprev;
-      double clast;
-      int nl, j0;
-    };
-    auto bin = [&](const Blk* blk, int NB) {
-      uint64_t key[8];
-      int j[8];
-      uint32_t w[8];
-      uint32_t inm = 0u;
+    const int n = (int)a.lvl_count[d];
+    const uint64_t* K = a.lvl_key + (size_t)d * a.cap;
+    const uint8_t* Wt = a.lvl_w + (size_t)d * a.cap;
+    const int step = (int)blockDim.x * UNR;
+    for (int i0 = (int)threadIdx.x; i0 < n; i0 += step) {
+      uint64_t key[UNR];
+      uint32_t w[UNR];
+      int j[UNR];
+      bool in[UNR];
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi) {
-        if (bi >= NB) break;
-        const Blk& B = blk[bi];
-        // bars at each level: cum - cum of the previous level (lane g-1's last byte)
-        const uint32_t left = g16::dpp_u<g16::ROW_SHR + 1>(B.cu) >> 24;
-        const uint32_t pc = (g == 0) ? B.cprev : left;
-        w[4 * bi + 0] = (B.cu & 0xFFu) - pc;
-        w[4 * bi + 1] = ((B.cu >> 8) & 0xFFu) - (B.cu & 0xFFu);
-        w[4 * bi + 2] = ((B.cu >> 16) & 0xFFu) - ((B.cu >> 8) & 0xFFu);
-        w[4 * bi + 3] = (B.cu >> 24) - ((B.cu >> 16) & 0xFFu);
-        const float cl[4] = {B.c4.x, B.c4.y, B.c4.z, B.c4.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int i = 4 * bi + u;
-          const bool v = B.j0 + 4 * g + u < B.nl;
-          key[i] = ord64(B.clast / (double)cl[u]);
-          const bool bl = v && key[i] <= sl.L0;
-          const bool in = v && !bl && key[i] <= sl.qmax;
-          below += bl ? w[i] : 0u;
-          inm |= (in ? 1u : 0u) << i;
-          const bool gtmin = key[i] > sl.qmin;
-          const int bk = (in && gtmin) ? (int)((key[i] - sl.qmin) >> sl.sh) : 0;
-          j[i] = (in && gtmin) ? (int)sl.T[bk] - 1 : -1;
-        }
+      for (int u = 0; u < UNR; ++u) {
+        const int i = i0 + u * (int)blockDim.x;
+        const bool v = i < n;
+        key[u] = v ? K[i] : 0ull;
+        w[u] = v ? (uint32_t)Wt[i] : 0u;
       }
-      const int nc = 4 * NB;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const bool bl = key[u] <= sl.L0;  // (padding entries have weight 0)
+        in[u] = !bl && key[u] <= sl.qmax;
+        below += bl ? w[u] : 0u;
+        const bool gtmin = key[u] > sl.qmin;
+        const int bk = (in[u] && gtmin) ? (int)((key[u] - sl.qmin) >> sl.sh) : 0;
+        j[u] = (in[u] && gtmin) ? (int)sl.T[bk] - 1 : -1;
+      }
       for (int bb = (1 << sl.steps) >> 1; bb > 0; bb >>= 1) {
-        uint64_t x[8];
+        uint64_t x[UNR];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (i < nc) x[i] = L1[min(j[i] + bb, nvc)];
+        for (int u = 0; u < UNR; ++u) x[u] = L1[min(j[u] + bb, nvc)];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (i < nc) j[i] = x[i] < key[i] ? j[i] + bb : j[i];
+        for (int u = 0; u < UNR; ++u) j[u] = x[u] < key[u] ? j[u] + bb : j[u];
       }
-      uint64_t x[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (i < nc) x[i] = L1[j[i] + 1];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        if (i < nc && ((inm >> i) & 1u))
-          atomicAdd((unsigned long long*)&C[j[i] + 1], x[i] == key[i] ? ((uint64_t)w[i] << 32) : (uint64_t)w[i]);
-    };
-    auto first_blk = [&](int s, uint64_t meta, Blk& B) {
-      B.nl = (int)(meta & 0xFFFFu);
-      B.clast = (double)bitsf((uint32_t)(meta >> 32));
-      B.j0 = 0;
-      B.cprev = 0u;
-      load(s, 0, B.c4, B.cu);
-    };
-    // the rest of a stock-day's levels past the first 64 (group-uniform loop)
-    auto tail = [&](int s, const Blk& B0) {
-      for (int j0 = 64; j0 < B0.nl; j0 += 64) {
-        Blk B = B0;
-        B.j0 = j0;
-        load(s, j0, B.c4, B.cu);
-        B.cprev = a.lvl_cum[((size_t)d * S + s) * NBAR + j0 - 1];
-        bin(&B, 1);
+      for (int u = 0; u < UNR; ++u) {
+        const uint64_t x = L1[j[u] + 1];
+        if (in[u]) atomicAdd((unsigned long long*)&C[j[u] + 1], x == key[u] ? ((uint64_t)w[u] << 32) : (uint64_t)w[u]);
       }
-    };
-    // the group's stocks s = grp + 64 i, two per step; the next pair is loaded while this
-    // one is binned (the last prefetch is a harmless re-read)
-    const int slast = S - 1;
-    Blk nA, nB;
-    first_blk(min(grp, slast), a.lvl_meta[(size_t)d * S + min(grp, slast)], nA);
-    first_blk(min(grp + 64, slast), a.lvl_meta[(size_t)d * S + min(grp + 64, slast)], nB);
-    for (int s = grp; s < S; s += 128) {  // group-uniform trip count
-      Blk P[2] = {nA, nB};
-      const int s2 = s + 64;
-      const int sn = min(s + 128, slast), sn2 = min(s + 192, slast);
-      first_blk(sn, a.lvl_meta[(size_t)d * S + sn], nA);
-      first_blk(sn2, a.lvl_meta[(size_t)d * S + sn2], nB);
-      if (s2 > slast) P[1].nl = 0;  // no second stock in this step
-      if (P[0].nl == 0 && P[1].nl == 0) continue;  // absent stock-days (group-uniform)
-      bin(P, 2);
-      if (P[0].nl > 64) tail(s, P[0]);
-      if (P[1].nl > 64) tail(s2, P[1]);
     }
     below = (uint32_t)__reduce_add_sync(~0ull, (int)below);
     if (lane_id() == 0) atomicAdd(&below_s, below);
@@ -460,12 +401,13 @@ static int pdf_launch(PdfArgs& a, const uint64_t* q_sorted, int M, hipStream_t s
 }
 
 static void pdf_levels_args(PdfArgs& a, const void* pdf_levels, int S, int D) {
-  size_t oc, om;
-  pdf_levels_split(S, D, &oc, &om);
+  size_t ok, ow;
+  pdf_levels_split(S, D, &ok, &ow);
   const char* base = reinterpret_cast<const char*>(pdf_levels);
-  a.lvl_close = reinterpret_cast<const float*>(base);
-  a.lvl_cum = reinterpret_cast<const uint8_t*>(base + oc);
-  a.lvl_meta = reinterpret_cast<const uint64_t*>(base + om);
+  a.lvl_count = reinterpret_cast<const uint32_t*>(base);
+  a.lvl_key = reinterpret_cast<const uint64_t*>(base + ok);
+  a.lvl_w = reinterpret_cast<const uint8_t*>(base + ow);
+  a.cap = (size_t)S * NBAR;
 }
 
 int mff_pdf_count(const void* pdf_levels, int S_loc, int D, int d0, int nd,

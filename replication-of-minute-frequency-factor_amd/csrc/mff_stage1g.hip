@@ -50,9 +50,12 @@ struct GArgs {
   double* val;
   uint8_t* state;
   double* pdfq;
-  float* lvl_close;     // doc_pdf level side channel (mff_pdf_levels_bytes), or null
-  uint8_t* lvl_cum;
-  uint64_t* lvl_meta;
+  // doc_pdf level side channel (mff_pdf_levels_bytes), or null: per day, a flat list of
+  // (key c_last/c_level as ord64, bars at the level) over every stock-day's levels, in
+  // no particular order; lvl_count[d] = entries (appended by atomic reservation)
+  uint32_t* lvl_count;
+  uint64_t* lvl_key;
+  uint8_t* lvl_w;
   int* fb_list;
   int* fb_count;
   uint32_t fam_exact;  // families whose non-fast stock-days go to the exact list
@@ -193,8 +196,6 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
     R.r[0] = R.r[1] = R.r[2] = R.r[3] = 0.0;
     R.st = 0u;
     double qv[5] = {qnan(), qnan(), qnan(), qnan(), qnan()};
-    uint32_t lvl_n = 0u;
-    float lvl_clast = 0.f;
 
     if (n > 0) {
       // ---------------------------------------------------------------- loads
@@ -818,8 +819,6 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           }
         }
         const int L = gcount(endm);
-        lvl_n = (uint32_t)L;
-        lvl_clast = (float)clast;
         if (fast) {
           // exact u32 prefix sums: sum(v) <= 240 * 2^24 < 2^32
           const uint32_t carry = gscan_excl_u(tv);
@@ -903,19 +902,32 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             if (tie) fast = false;  // exact tie: the reference's float order decides
           }
         }
-        int li = (int)gscan_excl_u((uint32_t)__builtin_popcount(endm));
-        if (a.lvl_close && ln) {
-          // level list for doc_pdf's frame-wide rank: level i (descending close) at its
-          // run end e: close, and e + 1 = bars in levels 0..i (mff_pdf.hip)
-          float* lc = a.lvl_close + sd * NBAR;
-          uint8_t* lu = a.lvl_cum + sd * NBAR;
+        if (a.lvl_key) {
+          // level list for doc_pdf's frame-wide rank (mff_pdf.hip): per level (a run
+          // end e), the key c_last / close (IEEE, as the reference's row keys) and its
+          // bar count e - start + 1; one reservation per stock-day in the day's list
+          uint32_t base = 0u;
+          if (g == 0 && L > 0) base = atomicAdd(a.lvl_count + d, (uint32_t)L);
+          base = bpermu(gb, base);
+          int li = (int)base + (int)gscan_excl_u((uint32_t)__builtin_popcount(endm));
+          uint32_t ls = 0u;
 #pragma unroll
           for (int k = 0; k < K; ++k)
+            if ((startm >> k) & 1u) ls = (uint32_t)(e0 + k);
+          uint32_t cs;
+          bool hs;
+          carry_left(ls, startm != 0u, cs, hs);  // last run start left of this lane
+          uint64_t* kd = a.lvl_key + (size_t)d * ((size_t)a.S * NBAR);
+          uint8_t* wd = a.lvl_w + (size_t)d * ((size_t)a.S * NBAR);
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            if ((startm >> k) & 1u) cs = (uint32_t)(e0 + k);
             if ((endm >> k) & 1u) {
-              lc[li] = bitsf(cbase - cw[k]);
-              lu[li] = (uint8_t)(e0 + k + 1);
+              kd[li] = ord64(clast / (double)bitsf(cbase - cw[k]));
+              wd[li] = (uint8_t)((uint32_t)(e0 + k) - cs + 1u);
               ++li;
             }
+          }
         }
         if (!fast && (fam & (a.fam_exact))) {
           if (g == 0) {
@@ -946,7 +958,6 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           }
         }
       }
-      if (a.lvl_meta && g == 0) a.lvl_meta[sd] = (uint64_t)lvl_n | ((uint64_t)fbits(lvl_clast) << 32);
       if (a.pdfq && g < 5) {
         const double qq = (g == 0) ? qv[0] : (g == 1) ? qv[1] : (g == 2) ? qv[2] : (g == 3) ? qv[3] : qv[4];
         a.pdfq[(size_t)g * plane + sd] = qq;
@@ -965,12 +976,13 @@ extern "C" size_t mff_stage1_workspace_bytes(int S, int D) {
 }
 
 namespace mff {
-// doc_pdf level side channel: closes f32 [D][S][240] | cum u8 [D][S][240] | meta u64 [D][S]
-size_t pdf_levels_split(int S, int D, size_t* off_cum, size_t* off_meta) {
-  const size_t sd = (size_t)S * (size_t)D;
-  *off_cum = sd * NBAR * 4;
-  *off_meta = ((*off_cum + sd * NBAR) + 255) & ~(size_t)255;
-  return *off_meta + sd * 8;
+// doc_pdf level side channel: counts u32 [D] | keys u64 [D][S*240] | bars u8 [D][S*240]
+// (a day holds at most one level per bar of every stock)
+size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w) {
+  const size_t cap = (size_t)S * (size_t)D * NBAR;
+  *off_key = ((size_t)D * 4 + 255) & ~(size_t)255;
+  *off_w = *off_key + cap * 8;
+  return *off_w + cap;
 }
 }  // namespace mff
 
@@ -1012,15 +1024,16 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
     MFF_REQUIRE(!(a.fam & use[f]) || fld[f] != nullptr, "mff_stage1: field plane %d required", f);
   MFF_REQUIRE(!(a.fam & F_PDF) || (pdf_query != nullptr && pdf_levels != nullptr),
               "mff_stage1: doc_pdf requested but pdf_query / pdf_levels is NULL");
-  if (a.fam & F_PDF) {
-    size_t oc, om;
-    pdf_levels_split(S, D, &oc, &om);
-    char* base = reinterpret_cast<char*>(pdf_levels);
-    a.lvl_close = reinterpret_cast<float*>(base);
-    a.lvl_cum = reinterpret_cast<uint8_t*>(base + oc);
-    a.lvl_meta = reinterpret_cast<uint64_t*>(base + om);
-  }
   hipStream_t st = as_stream(stream);
+  if (a.fam & F_PDF) {
+    size_t ok, ow;
+    pdf_levels_split(S, D, &ok, &ow);
+    char* base = reinterpret_cast<char*>(pdf_levels);
+    a.lvl_count = reinterpret_cast<uint32_t*>(base);
+    a.lvl_key = reinterpret_cast<uint64_t*>(base + ok);
+    a.lvl_w = reinterpret_cast<uint8_t*>(base + ow);
+    MFF_HIP(hipMemsetAsync(a.lvl_count, 0, (size_t)D * 4, st));
+  }
   int* cnt = reinterpret_cast<int*>(workspace);
   a.fb_count = cnt;
   a.fb_list = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + 256);
