@@ -10,11 +10,16 @@ and its cross-rank exchange) over the whole panel, inputs already resident in HB
 The panel (S stocks x D days) is sharded by stock over the ranks: total work is fixed,
 so "scaling" is "strong".  value = S*D*K / max-over-ranks(wall time of the K steps).
 
-roofline: the fused stage-1 kernel (k_stage1), algorithmic bytes per launch =
-5,354 B/stock-day (4,832 B OHLCV+mask in, 58 x 9 B out) x local stock-days,
-over its average duration from HIP events on its launch stream; peak 8.0 TB/s
-(MI355X_MICROARCH.md).  traffic: HBM bytes per launch from the committed rocprofv3 PMC
-passes (profiles/pmc_stage1.json, FETCH_SIZE doubled per the gfx950 correction), or null.
+roofline: the stage-1 pass (one mff_stage1 call = five launches: k_stage1s for the
+streaming / OLS families x3, k_stage1g for the sorted families x2, plus the small exact
+list kernel), algorithmic bytes per pass = 5,354 B/stock-day (4,832 B OHLCV+mask in,
+58 x 9 B out) x local stock-days, over the pass's average duration from HIP
+events on its launch stream; peak 8.0 TB/s (MI355X_MICROARCH.md).  traffic: HBM bytes per
+pass from the committed rocprofv3 PMC passes (profiles/pmc_stage1.json: FETCH_SIZE x 2 per
+the gfx950 correction + WRITE_SIZE, summed over the launches), or null;
+traffic_calibrated: the same with the LDS-DMA kernels' factor measured by
+profiles/ubench/rowload.hip.  valu_util: SQ_INSTS_VALU x 4 cycles / (1,024 SIMDs x 2.4 GHz
+x pass time) from the same PMC passes (the pass is VALU / latency bound, not HBM bound).
 
 cpu_baseline: the CPU oracle (oracle/mff_oracle.py, a numpy restatement of the reference
 cal_* functions) timed on this host, rank 0 at N=1, on a bounded sample of the same
@@ -70,7 +75,7 @@ def load_pmc(S_loc: int, D: int):
         pmc = json.load(f)
     if pmc.get("stocks") != S_loc or pmc.get("days") != D:
         return None
-    return pmc.get("hbm_bytes_per_launch")
+    return pmc
 
 
 def main():
@@ -136,7 +141,11 @@ def main():
     ids = list(range(catalog.N_FACTORS))
     bytes_launch = catalog.algorithmic_bytes_per_stock_day(ids) * S_loc * D
     achieved = bytes_launch / (k_ms * 1e-3) / 1e9
-    traffic = load_pmc(S_loc, D)
+    pmc = load_pmc(S_loc, D)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    traffic_cal = pmc.get("hbm_bytes_calibrated") if pmc else None
+    valu = pmc.get("sq", {}).get("SQ_INSTS_VALU") if pmc else None
+    valu_util = round(valu * 4 / (1024 * 2.4e9 * k_ms * 1e-3), 3) if valu else None
 
     extras = {}
     if not args.no_extras:
@@ -185,7 +194,10 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": "k_stage1",
+                "traffic_calibrated": traffic_cal,
+                "valu_util": valu_util,
+                "kernel": "stage-1 pass: k_stage1s<SEG|MOMR|TRD>, <MOMV|SUMV|SUMC|CORR>, <OLS|MOMH>, "
+                          "k_stage1g<ORD|ORDV>, <LVL|PDF> (+ k_stage1 exact list)",
                 "bytes_per_launch": bytes_launch,
                 "avg_kernel_ms": round(k_ms, 3),
             },

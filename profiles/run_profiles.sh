@@ -2,7 +2,7 @@
 # Profiling recipe (run on the GPU box via gpurun from the repo root):
 #   1. kernel trace + stats of the default bench (c4: 5000 x 2500, all 58 factors)
 #   2. PMC passes on the same workload, one counter group per run (gfx950 slot limits),
-#      restricted to the fused stage-1 kernel.
+#      restricted to the stage-1 launches (k_stage1s x3, k_stage1g x2, k_stage1 exact list).
 # Outputs land in gpurun_out/prof_<tag>/; the summaries worth keeping are copied into
 # profiles/<round>/ and profiles/pmc_stage1.json by profiles/summarize.py.
 set -euo pipefail
@@ -20,9 +20,10 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/trace" -o trace -
 
 for pmc in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY" \
+           "SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH" \
            "GRBM_GUI_ACTIVE GRBM_COUNT"; do
-  name=$(echo "$pmc" | awk '{print $1}')
-  timeout -s KILL 240 rocprofv3 --pmc $pmc --kernel-include-regex k_stage1 -T -d "$OUT/pmc_$name" -o pmc \
+  name=$(echo "$pmc" | awk '{print $1}')_$(echo "$pmc" | wc -w)
+  timeout -s KILL 240 rocprofv3 --pmc $pmc --kernel-include-regex k_stage1 -d "$OUT/pmc_$name" -o pmc \
     --output-format csv -- python3 "${BENCH[@]}" --steps 1 --warmup 0 > "$OUT/pmc_$name.log" 2>&1
 done
 echo "profiles done: $OUT"
