@@ -100,6 +100,10 @@ def test_stage1_level_fallback_and_off_tick(dev):
     c[:, 10:15] = (c[:, 10:15] * np.linspace(0.8, 1.25, c.shape[2], dtype=np.float32)).astype(np.float32)
     # closes spanning more than 2^24 float steps (ratio > 2): the u64-key level sort
     c[:, 15:18] = (c[:, 15:18] * np.linspace(0.6, 2.4, c.shape[2], dtype=np.float32)).astype(np.float32)
+    # on the 0.01 grid but spanning >= 512 ticks (u32 sort) and 256..511 ticks (tick bins)
+    ramp = np.linspace(-1.0, 1.0, c.shape[2])
+    c[:, 18:21] = (np.round(10000 + 700 * ramp) * 0.01).astype(np.float32)
+    c[:, 21:24] = (np.round(3000 + 200 * ramp + rng.integers(0, 3, c[:, 21:24].shape)) * 0.01).astype(np.float32)
     v = panel["volume"]
     v[:, 20:25] = v[:, 20:25] + np.float32(0.5)
     ov, os_ = O.oracle_stage1(panel)
