@@ -35,6 +35,11 @@ struct S1Args {
   double* pdfq;            // [5][D][S] or null
   const int* list;         // list mode: stock-day indices d*S+s to process (else null)
   const int* list_count;   // list mode: number of entries (device)
+  // list mode: doc_pdf level list of the 16-lane kernel (mff_stage1g.hip); entries
+  // flagged with the top bit (wide stock-days) append their levels here
+  uint32_t* lvl_count;
+  uint64_t* lvl_key;
+  uint8_t* lvl_w;
   int S, D, nf;
   uint32_t fam;
   int8_t row[NF];          // output row of each factor id, -1 = not requested
@@ -174,7 +179,7 @@ __device__ __forceinline__ double msum(const double (&x)[4], const bool (&f)[4])
 // general path: the tile kernel below, and the list-mode fallback of the 16-lane kernel
 // (mff_stage1g.hip) for stock-days whose closes are not on the 0.01 tick grid or whose
 // doc_pdf threshold is an exact tie.
-__device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, float* vw) {
+__device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, float* vw, bool emit_levels = false) {
   const int lane = lane_id();
   const bool lv = lane < 60;
   const uint32_t fam = a.fam;
@@ -531,6 +536,32 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
       double pcum[4];
       bool hpc[4];
       prev_valid(cum, lend, pcum, hpc);
+      if (emit_levels) {
+        // doc_pdf level list (as mff_stage1g.hip): per level, key c_last / close (IEEE)
+        // and its bar count; one reservation per stock-day in the day's flat list
+        const Bits LE = ballot4(lend);
+        const int L = count(LE);
+        const uint64_t lt = (1ull << lane) - 1ull;
+        uint32_t idx = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) idx += (uint32_t)__popcll(LE.b[k] & lt);
+        uint32_t base = 0u;
+        if (lane == 0) base = atomicAdd(a.lvl_count + d, (uint32_t)L);
+        idx += (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        double pos[4] = {(double)l4, (double)(l4 + 1), (double)(l4 + 2), (double)(l4 + 3)};
+        double ppos[4];
+        bool hpp[4];
+        prev_valid(pos, lend, ppos, hpp);
+        const double cl = (double)elem(c, ml);
+        const size_t cap = (size_t)a.S * NBAR;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (lend[k]) {
+            a.lvl_key[(size_t)d * cap + idx] = ord64(cl / (double)bitsf(~hi[k]));
+            a.lvl_w[(size_t)d * cap + idx] = (uint8_t)(l4 + k - (hpp[k] ? (int)ppos[k] : -1));
+            ++idx;
+          }
+      }
       // integral-volume contract check (exact level arithmetic)
       bool vint = true;
 #pragma unroll
@@ -732,9 +763,10 @@ __global__ __launch_bounds__(256) void k_stage1(S1Args a) {
     const int cnt = *a.list_count;
     const int nw = gridDim.x * WPB;
     for (int w = blockIdx.x * WPB + wave; w < cnt; w += nw) {
-      const int sd = __builtin_amdgcn_readfirstlane(a.list[w]);
+      const int raw = __builtin_amdgcn_readfirstlane(a.list[w]);
+      const int sd = raw & 0x7fffffff;  // top bit: a wide day whose levels are emitted here
       const Out out{a.val, a.state, a.row, -1, (size_t)sd, (size_t)a.D * a.S};
-      stock_day_w64(a, sd / a.S, sd % a.S, out, vw);
+      stock_day_w64(a, sd / a.S, sd % a.S, out, vw, raw < 0 && a.lvl_key != nullptr);
     }
     return;
   }
@@ -776,12 +808,14 @@ namespace mff {
 // 16-lane kernel; `fam_mask` restricts the families recomputed, `list_grid` blocks)
 int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, const int32_t* ids, int nf,
                double* val, uint8_t* state, double* pdfq, const int* list, const int* list_count,
-               uint32_t fam_mask, int list_grid, hipStream_t st) {
+               uint32_t fam_mask, int list_grid, hipStream_t st, uint32_t* lvl_count, uint64_t* lvl_key,
+               uint8_t* lvl_w) {
   S1Args a;
   memset(&a, 0, sizeof(a));
   for (int f = 0; f < 5; ++f) a.fld[f] = fld[f];
   a.mask = valid; a.val = val; a.state = state; a.pdfq = pdfq;
   a.list = list; a.list_count = list_count;
+  a.lvl_count = lvl_count; a.lvl_key = lvl_key; a.lvl_w = lvl_w;
   a.S = S; a.D = D; a.nf = nf;
   for (int i = 0; i < NF; ++i) a.row[i] = -1;
   for (int r = 0; r < nf; ++r) {

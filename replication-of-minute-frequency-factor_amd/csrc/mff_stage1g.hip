@@ -36,7 +36,8 @@ namespace mff {
 
 int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, const int32_t* ids, int nf,
                double* val, uint8_t* state, double* pdfq, const int* list, const int* list_count,
-               uint32_t fam_mask, int list_grid, hipStream_t st);
+               uint32_t fam_mask, int list_grid, hipStream_t st, uint32_t* lvl_count = nullptr,
+               uint64_t* lvl_key = nullptr, uint8_t* lvl_w = nullptr);
 int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
                   uint32_t fam, double* val, uint8_t* state, hipStream_t st);
 
@@ -766,8 +767,19 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
         bool fast = !gany(!ok);
         double q[5] = {qnan(), qnan(), qnan(), qnan(), qnan()};
         const int e0 = 16 * g;
-        uint32_t cw[K], vv[K], cbase;
-        if (cmx - cmn < (1u << 24)) {  // uniform inside the group
+        uint32_t cw[K], vv[K], cbase = cmx;
+        // a day whose closes span >= 2^24 float steps (a close ratio of 2 or more) does
+        // not fit the u32 keys: the exact wave64 kernel takes it whole (values, queries
+        // and its doc_pdf levels; list entry flagged by the top bit)
+        const bool wide = cmx - cmn >= (1u << 24);  // uniform inside the group
+        if (wide) {
+          if (g == 0) {
+            const int idx = atomicAdd(a.fb_count, 1);
+            a.fb_list[idx] = (int)((uint32_t)sd | 0x80000000u);
+          }
+#pragma unroll
+          for (int k = 0; k < K; ++k) { cw[k] = 0u; vv[k] = 0u; }
+        } else {
           uint32_t* sv = reinterpret_cast<uint32_t*>(scr);  // 256 volumes of this group
           uint32_t key[K];
 #pragma unroll
@@ -785,22 +797,6 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             vv[k] = (e0 + k < n) ? sv[key[k] & 0xffu] : 0u;
           }
           lds_fence();
-          cbase = cmx;
-        } else {
-          uint64_t key[K];
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            const bool pk = (pb >> k) & 1u;
-            const bool vok = (v[k] == rintf(v[k])) && (v[k] >= 0.0f) && (v[k] <= 16777216.0f);
-            key[k] = pk ? (((uint64_t)~fbits(c[k]) << 32) | (uint64_t)(vok ? (uint32_t)v[k] : 0u)) : ~0ull;
-          }
-          gsort256(key);
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            cw[k] = (uint32_t)(key[k] >> 32);
-            vv[k] = (uint32_t)key[k];
-          }
-          cbase = 0xffffffffu;
         }
         // close word of the neighbours across the lane boundary
         const uint32_t prevw = dpp_u<ROW_SHR + 1>(cw[K - 1]);
@@ -819,7 +815,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           }
         }
         const int L = gcount(endm);
-        if (fast) {
+        if (fast && !wide) {
           // exact u32 prefix sums: sum(v) <= 240 * 2^24 < 2^32
           const uint32_t carry = gscan_excl_u(tv);
           // running prefix at the last level start of the lane -> start prefix carried in
@@ -902,7 +898,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             if (tie) fast = false;  // exact tie: the reference's float order decides
           }
         }
-        if (a.lvl_key) {
+        if (a.lvl_key && !wide) {
           // level list for doc_pdf's frame-wide rank (mff_pdf.hip): per level (a run
           // end e), the key c_last / close (IEEE, as the reference's row keys) and its
           // bar count e - start + 1; one reservation per stock-day in the day's list
@@ -929,7 +925,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             }
           }
         }
-        if (!fast && (fam & (a.fam_exact))) {
+        if (!fast && !wide && (fam & (a.fam_exact))) {
           if (g == 0) {
             const int idx = atomicAdd(a.fb_count, 1);
             a.fb_list[idx] = (int)sd;
@@ -1050,7 +1046,9 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
     b.fam_exact = 0u;
     hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b);
     MFF_LAUNCH_CHECK();
-    return 0;
+    // levels of the wide days (listed by the launch above)
+    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_PDF, 1024, st,
+                      a.lvl_count, a.lvl_key, a.lvl_w);
   }
   {
     const int rc = launch_serial(fld, valid, S, D, a.row, a.fam, val, state, st);
@@ -1072,7 +1070,7 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
   if (a.fam & (F_LVL | F_PDF)) {
     // exact general path for the listed stock-days (LVL + PDF only)
     return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt,
-                      F_LVL | F_PDF, 1024, st);
+                      F_LVL | F_PDF, 1024, st, a.lvl_count, a.lvl_key, a.lvl_w);
   }
   return 0;
 }
