@@ -39,7 +39,7 @@ int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, c
                uint32_t fam_mask, int list_grid, hipStream_t st, uint32_t* lvl_count = nullptr,
                uint64_t* lvl_key = nullptr, uint8_t* lvl_w = nullptr);
 int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
-                  uint32_t fam, double* val, uint8_t* state, hipStream_t st);
+                  uint32_t fam, double* val, uint8_t* state, const float* ord_th, hipStream_t st);
 
 namespace g16 {
 
@@ -60,6 +60,8 @@ struct GArgs {
   int* fb_list;
   int* fb_count;
   uint32_t fam_exact;  // families whose non-fast stock-days go to the exact list
+  float* ord_th;       // ORD thresholds [3][D][S] (top-50 min, top-20 min, bottom-50 max)
+                       // for the serial returns kernel's products, or null
   int S, D;
   uint32_t fam;
   int8_t row[NF];
@@ -161,7 +163,7 @@ __device__ __forceinline__ void gsort256(T (&a)[K]) {
 // are allocated for that group alone; the planes a group reads are re-read by the next
 // launch, which costs little here: the stage is VALU bound.
 [[maybe_unused]] constexpr uint32_t G_HL = F_OLS | F_MOMH;  // high, low
-constexpr uint32_t G_ORD = F_ORD | F_ORDV;   // open, close, volume
+constexpr uint32_t G_ORD = F_ORD | F_ORDV;   // volume (thresholds; the products are serial)
 constexpr uint32_t G_LVL = F_LVL | F_PDF;    // close, volume
 constexpr uint32_t kGroups[2] = {G_ORD, G_LVL};
 
@@ -214,9 +216,9 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           for (int k = 0; k < K; ++k) x[k] = dflt;
         }
       };
-      const uint32_t needO = F_SEG | F_ORD | F_MOMR | F_TRD;
+      const uint32_t needO = F_SEG | F_MOMR | F_TRD;
       const uint32_t needHL = F_OLS | F_MOMH;
-      const uint32_t needC = F_SEG | F_ORD | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD;
+      const uint32_t needC = F_SEG | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD;
       const uint32_t needV = F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD;
       auto sanitize = [&](float (&x)[K], float dflt) {
 #pragma unroll
@@ -417,6 +419,10 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
         th50 = kth(n >= 50 ? n - 50 : 0);  // top_k(50).min()   CM:391-396
         th20 = kth(n >= 20 ? n - 20 : 0);  // top_k(20).min()
         tb50 = kth(n >= 50 ? 49 : n - 1);  // bottom_k(50).max() CM:417-422
+        if ((fam & F_ORD) && a.ord_th && g < 3 && act) {
+          const size_t pl = (size_t)a.D * a.S;
+          a.ord_th[(size_t)g * pl + sd] = g == 0 ? th50 : g == 1 ? th20 : tb50;
+        }
         if (fam & F_ORDV) {
           double t10 = 0.0, t5 = 0.0;
 #pragma unroll
@@ -435,7 +441,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
       }
 
       // ================================================================ RET: MOMR + TRD + ORD products
-      if (fam & (F_MOMR | F_TRD | F_ORD)) {
+      if (fam & (F_MOMR | F_TRD)) {
         fresh(c);
         fresh(o);
         fresh(v);
@@ -445,7 +451,6 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
         double u1 = 0, u2 = 0, umn = __builtin_inf(), umx = -__builtin_inf();
         double w1 = 0, w2 = 0, wmn = __builtin_inf(), wmx = -__builtin_inf();
         uint32_t upm = 0, dnm = 0;
-        double p50 = 1.0, p20 = 1.0, pb50 = 1.0;
         double vT20 = 0, vT50 = 0, rT20 = 0, rT50 = 0, vH20 = 0, vH50 = 0, a20 = 0, n20 = 0, q20 = 0, a50 = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -458,9 +463,6 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
             if (tot_gt(r, 0.0)) { upm |= 1u << k; u1 += dd; u2 += d2; umn = fmin(umn, r); umx = fmax(umx, r); }
             if (tot_lt(r, 0.0)) { dnm |= 1u << k; w1 += dd; w2 += d2; wmn = fmin(wmn, r); wmx = fmax(wmx, r); }
-            if (v[k] >= th50) p50 *= q;
-            if (v[k] >= th20) p20 *= q;
-            if (v[k] <= tb50) pb50 *= q;
             const double vk = (double)v[k];
             if (m >= 220) { vT20 += vk; rT20 += vk * r; }
             if (m >= 190) { vT50 += vk; rT50 += vk * r; }
@@ -496,13 +498,6 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           R.val(21, sk);
           R.val(22, ku);
           R.val(23, sk / ku);
-        }
-        if (fam & F_ORD) {
-          const double pbb = gprod(pb50) - 1.0;
-          R.val(10, gprod(p50) - 1.0);
-          R.val(11, pbb);
-          R.val(12, gprod(p20) - 1.0);
-          R.val(13, pbb);  // bottom_k(50) [sic CM:471]
         }
         if (fam & F_TRD) {
           if (gany((pb & rmask(220, 239)) != 0u)) R.val(50, gsum(rT20) / (gsum(vT20) + 1.0));
@@ -967,8 +962,9 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
 
 using namespace mff;
 
+// workspace: list count (256 B) | exact list int [S*D] | ORD thresholds float [3][S*D]
 extern "C" size_t mff_stage1_workspace_bytes(int S, int D) {
-  return 256 + (size_t)S * (size_t)D * sizeof(int);
+  return 256 + (size_t)S * (size_t)D * (sizeof(int) + 3 * sizeof(float));
 }
 
 namespace mff {
@@ -1050,11 +1046,13 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
     return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_PDF, 1024, st,
                       a.lvl_count, a.lvl_key, a.lvl_w);
   }
-  {
-    const int rc = launch_serial(fld, valid, S, D, a.row, a.fam, val, state, st);
-    if (rc != 0) return rc;
-  }
+  a.ord_th = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256 + (size_t)S * D * sizeof(int));
+  // order: the ORD sort (thresholds) before the serial returns kernel (products)
   for (int gi = 0; gi < 2; ++gi) {
+    if (gi == 1) {
+      const int rc = launch_serial(fld, valid, S, D, a.row, a.fam, val, state, a.ord_th, st);
+      if (rc != 0) return rc;
+    }
     const uint32_t set = g16::kGroups[gi];
     if (!(a.fam & set)) continue;
     g16::GArgs b = a;  // this launch stores its own group's rows (and the queries) only

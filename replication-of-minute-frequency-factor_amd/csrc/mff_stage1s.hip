@@ -13,6 +13,8 @@
 //  MOMR  returns r = c/o - 1: std / up / down / skew / kurt, sums shifted by the first
 //        return (a member, so a constant set gives exact zeros, C3)      CM:518-687
 //  TRD   return-volume sums over the minute windows                    CM:1203-1406
+//  ORD   products of close/open over the bars beyond the volume order statistics,
+//        whose thresholds the 16-lane sort kernel leaves in the workspace CM:379-480
 //  MOMV  volume moments shifted by the first volume                     CM:485-496,690-729
 //  SUMV  volume sums over the minute windows                            CM:764-831,1251-1306
 //  SUMC  Amihud over the previous present bar                           CM:734-761
@@ -47,10 +49,11 @@ struct SArgs {
   int S, D;
   uint32_t fam;
   int8_t row[NF];
+  const float* ord_th;  // ORD thresholds [3][D][S] from the 16-lane sort kernel
 };
 
 // the serial families, in launch groups (each gets its own register allocation)
-constexpr uint32_t kSerA = F_SEG | F_MOMR | F_TRD;             // open, close, volume
+constexpr uint32_t kSerA = F_SEG | F_MOMR | F_TRD | F_ORD;     // open, close, volume
 constexpr uint32_t kSerB = F_MOMV | F_SUMV | F_SUMC | F_CORR;  // close, volume
 constexpr uint32_t kSerH = F_OLS | F_MOMH;                     // high, low
 constexpr uint32_t kSerial = kSerA | kSerB | kSerH;
@@ -101,9 +104,9 @@ struct Mask {
 
 // planes a family set reads (bit p = plane p: open, high, low, close, volume)
 __host__ __device__ constexpr uint32_t kPlanes(uint32_t set) {
-  return ((set & (F_SEG | F_MOMR | F_TRD)) ? 1u : 0u) | ((set & (F_OLS | F_MOMH)) ? 6u : 0u) |
-         ((set & (F_SEG | F_MOMR | F_TRD | F_SUMC | F_CORR)) ? 8u : 0u) |
-         ((set & (F_TRD | F_MOMV | F_SUMV | F_SUMC | F_CORR)) ? 16u : 0u);
+  return ((set & (F_SEG | F_MOMR | F_TRD | F_ORD)) ? 1u : 0u) | ((set & (F_OLS | F_MOMH)) ? 6u : 0u) |
+         ((set & (F_SEG | F_MOMR | F_TRD | F_ORD | F_SUMC | F_CORR)) ? 8u : 0u) |
+         ((set & (F_TRD | F_ORD | F_MOMV | F_SUMV | F_SUMC | F_CORR)) ? 16u : 0u);
 }
 typedef __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -112,7 +115,7 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 // FULL: every family of SET is requested (the usual case), so the family tests fold
 // away at compile time instead of branching per bar
 template <uint32_t SET, bool FULL>
-__global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
+__global__ __launch_bounds__(256, 2) void k_stage1s(SArgs a) {
   const uint32_t fam = FULL ? SET : (a.fam & SET);
   const int ntile = (a.S + 255) / 256;
   const int d = blockIdx.x / ntile;
@@ -178,6 +181,15 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
   double s1 = 0, s2 = 0, s3 = 0, s4 = 0, u1 = 0, u2 = 0, w1 = 0, w2 = 0;
   double umn = __builtin_inf(), umx = -__builtin_inf(), wmn = __builtin_inf(), wmx = -__builtin_inf();
   int nu = 0, ndn = 0;
+  // ORD: products of close/open over the bars at or beyond the volume thresholds
+  double p50 = 1.0, p20 = 1.0, pb50 = 1.0;
+  float th50 = 0.f, th20 = 0.f, tb50 = 0.f;
+  if (fam & F_ORD) {
+    const size_t pl = (size_t)a.D * a.S;
+    th50 = a.ord_th[sd];
+    th20 = a.ord_th[pl + sd];
+    tb50 = a.ord_th[2 * pl + sd];
+  }
   // TRD
   double vT20 = 0, vT50 = 0, rT20 = 0, rT50 = 0, vH20 = 0, vH50 = 0, a20 = 0, n20 = 0, q20 = 0, a50 = 0;
   // MOMV
@@ -263,7 +275,7 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
     // is a select; the minute windows are wave-uniform selects (only m <= 50, which
     // needs a reciprocal, stays a uniform branch).  Straight-line code lets the
     // scheduler overlap the dependent f64 chains of the four bars of a quad.
-    if (fam & (F_MOMR | F_TRD)) {
+    if (fam & (F_MOMR | F_TRD | F_ORD)) {
       const double q = fdiv((double)cf, (double)of);  // close / open
       const double r = pk ? q - 1.0 : x0r;
       const double v = pk ? (double)vf : 0.0;
@@ -277,6 +289,11 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
         w1 += dn ? dd : 0.0; w2 += dn ? d2 : 0.0;
         umn = (up && r < umn) ? r : umn; umx = (up && r > umx) ? r : umx;
         wmn = (dn && r < wmn) ? r : wmn; wmx = (dn && r > wmx) ? r : wmx;
+      }
+      if (fam & F_ORD) {  // CM:379-480: top_k(k).min() <= v, v <= bottom_k(50).max()
+        p50 *= (pk && vf >= th50) ? q : 1.0;
+        p20 *= (pk && vf >= th20) ? q : 1.0;
+        pb50 *= (pk && vf <= tb50) ? q : 1.0;
       }
       if (fam & F_TRD) {
         const double vr = v * r;
@@ -506,6 +523,12 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
     val(22, ku);
     val(23, sk / ku);
   }
+  if (fam & F_ORD) {
+    val(10, p50 - 1.0);   // mmt_top50VolumeRet
+    val(11, pb50 - 1.0);  // mmt_bottom50VolumeRet
+    val(12, p20 - 1.0);   // mmt_top20VolumeRet
+    val(13, pb50 - 1.0);  // mmt_bottom20VolumeRet: bottom_k(50) [sic CM:471]
+  }
   if (fam & F_TRD) {
     if (M.any_in(220, 239)) val(50, rT20 / (vT20 + 1.0)); else absent(50);
     if (M.any_in(190, 239)) val(51, rT50 / (vT50 == 0.0 ? 1.0 : vT50)); else absent(51);
@@ -585,12 +608,13 @@ __global__ __launch_bounds__(256) void k_stage1s(SArgs a) {
 
 // launch the serial kernel for the families of `fam` it covers (mff_stage1g.hip)
 int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
-                  uint32_t fam, double* val, uint8_t* state, hipStream_t st) {
+                  uint32_t fam, double* val, uint8_t* state, const float* ord_th, hipStream_t st) {
   using namespace s1s;
   SArgs a;
   memset(&a, 0, sizeof(a));
   for (int f = 0; f < 5; ++f) a.fld[f] = fld[f];
   a.mask = valid; a.val = val; a.state = state; a.S = S; a.D = D;
+  a.ord_th = ord_th;
   a.fam = fam & kSerial;
   for (int i = 0; i < NF; ++i) a.row[i] = (kFactorFamily[i] & kSerial) ? row[i] : (int8_t)-1;
   if (!a.fam) return 0;
