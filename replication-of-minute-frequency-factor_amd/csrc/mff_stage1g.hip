@@ -810,45 +810,93 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           }
         }
         const int L = gcount(endm);
-        if (fast && !wide) {
-          // exact u32 prefix sums: sum(v) <= 240 * 2^24 < 2^32
+        if (!wide) {
+          // Compact the levels (run ends, descending close) into LDS by level index:
+          //   lv[l] = V_l, the level's exact u32 volume (sum(v) <= 240 * 2^24 < 2^32),
+          //   lc[l] = cw << 8 | bars (cw < 2^24 on this path, bars <= 240),
+          // so that everything per level below runs over ceil(L/16) slots per lane
+          // (levels of a lane contiguous) instead of the 16 sorted bars.
+          uint32_t* lv = reinterpret_cast<uint32_t*>(scr);
+          uint32_t* lc = lv + 256;
           const uint32_t carry = gscan_excl_u(tv);
-          // running prefix at the last level start of the lane -> start prefix carried in
-          uint32_t lastS = 0u, run = carry;
+          uint32_t lastS = 0u, run = carry, ls = 0u;
 #pragma unroll
           for (int k = 0; k < K; ++k) {
-            if ((startm >> k) & 1u) lastS = run;
+            if ((startm >> k) & 1u) { lastS = run; ls = (uint32_t)(e0 + k); }
             if (e0 + k < n) run += vv[k];
           }
-          uint32_t sc;
-          bool hs;
-          carry_left(lastS, startm != 0u, sc, hs);
-          const uint32_t Sv = (uint32_t)sumv;
-          if (fam & F_LVL) {
-            // level shares V_l / sum(v) (C7: equal volumes -> identical shares)
-            const double inv = 1.0 / sumv;
-            uint32_t cum = carry, st0 = sc, V0 = 0u;
-            bool got = false;
+          uint32_t st0, cs;
+          bool h0, h1;
+          carry_left(lastS, startm != 0u, st0, h0);  // prefix at the open run's start
+          carry_left(ls, startm != 0u, cs, h1);      // and its first element
+          uint32_t cum = carry;
+          int li = (int)gscan_excl_u((uint32_t)__builtin_popcount(endm));
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-              if ((startm >> k) & 1u) st0 = cum;
-              if (e0 + k < n) cum += vv[k];
-              if (((endm >> k) & 1u) && !got) { V0 = cum - st0; got = true; }
+          for (int k = 0; k < K; ++k) {
+            if ((startm >> k) & 1u) { st0 = cum; cs = (uint32_t)(e0 + k); }
+            if (e0 + k < n) cum += vv[k];
+            if ((endm >> k) & 1u) {
+              lv[li] = cum - st0;
+              lc[li] = (cw[k] << 8) | ((uint32_t)(e0 + k) - cs + 1u);
+              ++li;
             }
-            const int fe = gfirst(endm);
-            const double x0 = (double)bpermu(gb + (fe >> 4), V0) * inv;
-            double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
-            cum = carry;
-            st0 = sc;
+          }
+          lds_fence();
+          const int nj = (L + 15) >> 4;  // levels per lane (uniform inside the group)
+          const int l0 = nj * g;
+          const uint32_t Sv = (uint32_t)sumv;
+          const double inv = 1.0 / sumv;
+          // level 0 (the highest close) is the member shift of the share moments
+          const double x0 = (double)lv[0] * inv;
+          // doc_pdf: the first level whose cumulative share exceeds k/20 is the first with
+          // 20*cum > k*Sv, i.e. cum > floor(k*Sv/20) (integers); an exact tie
+          // 20*cum == k*Sv at a level (only when 20 | k*Sv) is left to the exact path
+          const uint32_t kk[5] = {12u, 14u, 16u, 18u, 19u};
+          uint32_t T[5];
+          bool dv[5];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-              if ((startm >> k) & 1u) st0 = cum;
-              if (e0 + k < n) cum += vv[k];
-              if ((endm >> k) & 1u) {
-                const double dd = (double)(cum - st0) * inv - x0, d2 = dd * dd;
+          for (int t = 0; t < 5; ++t) {
+            const uint64_t x = (uint64_t)kk[t] * Sv;
+            T[t] = (uint32_t)(x / 20u);
+            dv[t] = (x % 20u) == 0u;
+          }
+          // lane totals -> carry of the level prefix
+          uint32_t tl = 0u;
+          for (int j = 0; j < nj; ++j)
+            if (l0 + j < L) tl += lv[l0 + j];
+          uint32_t c2 = gscan_excl_u(tl);
+          int cnt[5] = {0, 0, 0, 0, 0};
+          bool tie = false;
+          double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+          uint64_t* kd = a.lvl_key ? a.lvl_key + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
+          uint8_t* wd = a.lvl_w ? a.lvl_w + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
+          uint32_t base = 0u;
+          if (kd && g == 0) base = atomicAdd(a.lvl_count + d, (uint32_t)L);
+          base = bpermu(gb, base);
+          for (int j = 0; j < nj; ++j) {
+            const int l = l0 + j;
+            if (l < L) {
+              const uint32_t V = lv[l], cwb = lc[l];
+              c2 += V;
+              if (fam & F_LVL) {
+                const double dd = (double)V * inv - x0, d2 = dd * dd;
                 s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
               }
+              if (fam & F_PDF) {
+#pragma unroll
+                for (int t = 0; t < 5; ++t) {
+                  cnt[t] += c2 <= T[t] ? 1 : 0;
+                  tie = tie || (dv[t] && c2 == T[t]);
+                }
+              }
+              if (kd) {  // doc_pdf level list: key c_last / close (IEEE), bars
+                kd[base + l] = ord64(clast / (double)bitsf(cbase - (cwb >> 8)));
+                wd[base + l] = (uint8_t)(cwb & 0xFFu);
+              }
             }
+          }
+          if (fast && (fam & F_LVL)) {
+            // level shares V_l / sum(v) (C7: equal volumes -> identical shares)
             RawMom m{gsum(s1), gsum(s2), gsum(s3), gsum(s4), L};
             double sk, ku;
             skew_kurt(m, sk, ku);
@@ -857,68 +905,17 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             R.val(40, sk);  // doc_skew
             R.val(41, sk);  // doc_std: .skew() [sic CM:999]
           }
-          if (fam & F_PDF) {
-            // first level (descending close) whose cumulative share exceeds k/20:
-            // 20*cum > k*sum(v), exact in f64 (both sides < 2^37)
-            const double kk[5] = {12.0, 14.0, 16.0, 18.0, 19.0};
-            int ep[5], et[5];
-#pragma unroll
-            for (int t = 0; t < 5; ++t) { ep[t] = 1 << 20; et[t] = 1 << 20; }
-            uint32_t cum = carry;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-              if (e0 + k < n) cum += vv[k];
-              if ((endm >> k) & 1u) {
-                const double lhs = 20.0 * (double)cum;
-#pragma unroll
-                for (int t = 0; t < 5; ++t) {
-                  const double rhs = kk[t] * (double)Sv;
-                  if (lhs > rhs && ep[t] == (1 << 20)) ep[t] = e0 + k;
-                  if (lhs == rhs && et[t] == (1 << 20)) et[t] = e0 + k;
-                }
-              }
-            }
-            bool tie = false;
+          if (fast && (fam & F_PDF)) {
+            if (gany(tie) && Sv != 0u) fast = false;  // the reference's float order decides
 #pragma unroll
             for (int t = 0; t < 5; ++t) {
-              int e = gmin_i(ep[t]);
-              const int te = gmin_i(et[t]);
-              if (Sv == 0u) e = 0;  // shares NaN: NaN > p (S11) -> the first level
-              else if (te < e) tie = true;
-              if (e < (1 << 20)) {
-                const uint32_t w = bpermu(gb + (e >> 4), pick(cw, e & 15));
-                q[t] = clast / (double)bitsf(cbase - w);
-              }
-            }
-            if (tie) fast = false;  // exact tie: the reference's float order decides
-          }
-        }
-        if (a.lvl_key && !wide) {
-          // level list for doc_pdf's frame-wide rank (mff_pdf.hip): per level (a run
-          // end e), the key c_last / close (IEEE, as the reference's row keys) and its
-          // bar count e - start + 1; one reservation per stock-day in the day's list
-          uint32_t base = 0u;
-          if (g == 0 && L > 0) base = atomicAdd(a.lvl_count + d, (uint32_t)L);
-          base = bpermu(gb, base);
-          int li = (int)base + (int)gscan_excl_u((uint32_t)__builtin_popcount(endm));
-          uint32_t ls = 0u;
-#pragma unroll
-          for (int k = 0; k < K; ++k)
-            if ((startm >> k) & 1u) ls = (uint32_t)(e0 + k);
-          uint32_t cs;
-          bool hs;
-          carry_left(ls, startm != 0u, cs, hs);  // last run start left of this lane
-          uint64_t* kd = a.lvl_key + (size_t)d * ((size_t)a.S * NBAR);
-          uint8_t* wd = a.lvl_w + (size_t)d * ((size_t)a.S * NBAR);
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            if ((startm >> k) & 1u) cs = (uint32_t)(e0 + k);
-            if ((endm >> k) & 1u) {
-              kd[li] = ord64(clast / (double)bitsf(cbase - cw[k]));
-              wd[li] = (uint8_t)((uint32_t)(e0 + k) - cs + 1u);
-              ++li;
+              // levels with cum <= T come first (cum is monotone); Sv = 0: shares NaN,
+              // NaN > p (S11) -> the first level
+              const int e = Sv == 0u ? 0 : gsum_i(cnt[t]);
+              if (e < L) q[t] = clast / (double)bitsf(cbase - (lc[e] >> 8));
             }
           }
+          lds_fence();
         }
         if (!fast && !wide && (fam & (a.fam_exact))) {
           if (g == 0) {
