@@ -252,7 +252,7 @@ __global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
     // interleaved).  A key at or below Q[P0-1] only adds its weight to `below`; a key
     // above the slice belongs to a later slice.  Search: binary lifting from T[b]-1
     // (L1[T[b]-1] < key <= L1[T[b+1]]), one LDS read, compare and select per step.
-    constexpr int UNR = 4;
+    constexpr int UNR = 8;
     const uint64_t* L1 = L + 1;
     const int nvc = sl.nv;  // L1[nv] = ~0 stops every probe past the end
     const int n = (int)a.lvl_count[d];
