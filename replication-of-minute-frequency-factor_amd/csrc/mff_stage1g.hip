@@ -793,51 +793,39 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           }
           lds_fence();
         }
-        // close word of the neighbours across the lane boundary
-        const uint32_t prevw = dpp_u<ROW_SHR + 1>(cw[K - 1]);
+        // Levels = runs of equal close words among the n sorted bars.  validm: this lane's
+        // elements e < n; a run ends where the next element's word differs (or at
+        // e = n - 1); the element after an end starts a run.
+        const int nin = min(max(n - e0, 0), K);
+        const uint32_t validm = (uint32_t)((1u << nin) - 1u);
         const uint32_t nextw = dpp_u<ROW_SHL + 1>(cw[0]);
-        uint32_t endm = 0u, startm = 0u, tv = 0u;
+        uint32_t diffm = 0u, tv = 0u;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          const int e = e0 + k;
-          const uint32_t w = cw[k];
-          const uint32_t wp = k > 0 ? cw[k - 1] : prevw;
           const uint32_t wn = k < K - 1 ? cw[k + 1] : nextw;
-          if (e < n) {
-            tv += vv[k];
-            if (e == 0 || wp != w) startm |= 1u << k;
-            if (e == n - 1 || wn != w) endm |= 1u << k;
-          }
+          diffm |= (cw[k] != wn ? 1u : 0u) << k;
+          tv += vv[k];  // 0 past n
         }
+        const uint32_t lastm = (n - 1 >= e0 && n - 1 < e0 + K) ? 1u << (n - 1 - e0) : 0u;
+        const uint32_t endm = (diffm | lastm) & validm;
         const int L = gcount(endm);
         if (!wide) {
           // Compact the levels (run ends, descending close) into LDS by level index:
-          //   lv[l] = V_l, the level's exact u32 volume (sum(v) <= 240 * 2^24 < 2^32),
-          //   lc[l] = cw << 8 | bars (cw < 2^24 on this path, bars <= 240),
-          // so that everything per level below runs over ceil(L/16) slots per lane
-          // (levels of a lane contiguous) instead of the 16 sorted bars.
+          //   lv[l] = cumulative volume through level l (exact u32: sum(v) <= 240 * 2^24),
+          //   lc[l] = cw << 8 | e, its last sorted element (cw < 2^24 on this path),
+          // so level l has volume lv[l] - lv[l-1] and e_l - e_(l-1) bars, and everything
+          // per level below runs over ceil(L/16) slots per lane (a lane's levels
+          // contiguous) instead of the 16 sorted bars.
           uint32_t* lv = reinterpret_cast<uint32_t*>(scr);
           uint32_t* lc = lv + 256;
-          const uint32_t carry = gscan_excl_u(tv);
-          uint32_t lastS = 0u, run = carry, ls = 0u;
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            if ((startm >> k) & 1u) { lastS = run; ls = (uint32_t)(e0 + k); }
-            if (e0 + k < n) run += vv[k];
-          }
-          uint32_t st0, cs;
-          bool h0, h1;
-          carry_left(lastS, startm != 0u, st0, h0);  // prefix at the open run's start
-          carry_left(ls, startm != 0u, cs, h1);      // and its first element
-          uint32_t cum = carry;
+          uint32_t cum = gscan_excl_u(tv);
           int li = (int)gscan_excl_u((uint32_t)__builtin_popcount(endm));
 #pragma unroll
           for (int k = 0; k < K; ++k) {
-            if ((startm >> k) & 1u) { st0 = cum; cs = (uint32_t)(e0 + k); }
-            if (e0 + k < n) cum += vv[k];
+            cum += vv[k];
             if ((endm >> k) & 1u) {
-              lv[li] = cum - st0;
-              lc[li] = (cw[k] << 8) | ((uint32_t)(e0 + k) - cs + 1u);
+              lv[li] = cum;
+              lc[li] = (cw[k] << 8) | (uint32_t)(e0 + k);
               ++li;
             }
           }
@@ -850,21 +838,25 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           const double x0 = (double)lv[0] * inv;
           // doc_pdf: the first level whose cumulative share exceeds k/20 is the first with
           // 20*cum > k*Sv, i.e. cum > floor(k*Sv/20) (integers); an exact tie
-          // 20*cum == k*Sv at a level (only when 20 | k*Sv) is left to the exact path
+          // 20*cum == k*Sv at a level (only when 20 | k*Sv) is left to the exact path.
+          // floor(k*Sv/20) = k*(Sv/20) + (k*(Sv%20))/20 in u32.
           const uint32_t kk[5] = {12u, 14u, 16u, 18u, 19u};
+          const uint32_t sq20 = Sv / 20u, sr20 = Sv - 20u * sq20;
           uint32_t T[5];
           bool dv[5];
 #pragma unroll
           for (int t = 0; t < 5; ++t) {
-            const uint64_t x = (uint64_t)kk[t] * Sv;
-            T[t] = (uint32_t)(x / 20u);
-            dv[t] = (x % 20u) == 0u;
+            const uint32_t b = kk[t] * sr20;  // < 380
+            const uint32_t bq = b / 20u;
+            T[t] = kk[t] * sq20 + bq;
+            dv[t] = b == 20u * bq;
           }
-          // lane totals -> carry of the level prefix
-          uint32_t tl = 0u;
-          for (int j = 0; j < nj; ++j)
-            if (l0 + j < L) tl += lv[l0 + j];
-          uint32_t c2 = gscan_excl_u(tl);
+          // the lane's first level continues from the previous lane's last one
+          uint32_t pcum = 0u, pe = 0xFFFFFFFFu;  // (cum, last element) before level l0
+          if (l0 > 0 && l0 <= L) {
+            pcum = lv[l0 - 1];
+            pe = lc[l0 - 1] & 0xFFu;
+          }
           int cnt[5] = {0, 0, 0, 0, 0};
           bool tie = false;
           double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
@@ -876,8 +868,11 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           for (int j = 0; j < nj; ++j) {
             const int l = l0 + j;
             if (l < L) {
-              const uint32_t V = lv[l], cwb = lc[l];
-              c2 += V;
+              const uint32_t c2 = lv[l], cwb = lc[l];
+              const uint32_t V = c2 - pcum, ee = cwb & 0xFFu;
+              const uint32_t bars = ee - pe;  // pe = -1 before level 0
+              pcum = c2;
+              pe = ee;
               if (fam & F_LVL) {
                 const double dd = (double)V * inv - x0, d2 = dd * dd;
                 s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
@@ -891,7 +886,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
               }
               if (kd) {  // doc_pdf level list: key c_last / close (IEEE), bars
                 kd[base + l] = ord64(clast / (double)bitsf(cbase - (cwb >> 8)));
-                wd[base + l] = (uint8_t)(cwb & 0xFFu);
+                wd[base + l] = (uint8_t)bars;
               }
             }
           }
