@@ -282,13 +282,16 @@ __global__ __launch_bounds__(256, 2) void k_stage1s(SArgs a) {
       if (fam & F_MOMR) {
         const double dd = r - x0r, d2 = dd * dd;
         s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
-        const bool up = pk && r > 0.0, dn = pk && r < 0.0;  // r is finite (S11 needs no NaN case)
+        const bool up = pk & (r > 0.0), dn = pk & (r < 0.0);  // r is finite (no NaN case)
         nu += up ? 1 : 0;
         ndn += dn ? 1 : 0;
         u1 += up ? dd : 0.0; u2 += up ? d2 : 0.0;
         w1 += dn ? dd : 0.0; w2 += dn ? d2 : 0.0;
-        umn = (up && r < umn) ? r : umn; umx = (up && r > umx) ? r : umx;
-        wmn = (dn && r < wmn) ? r : wmn; wmx = (dn && r > wmx) ? r : wmx;
+        // min / max as plain compares + selects of candidates (+-inf when not in the set)
+        const double ru = up ? r : __builtin_inf(), rd = dn ? r : __builtin_inf();
+        const double ru2 = up ? r : -__builtin_inf(), rd2 = dn ? r : -__builtin_inf();
+        umn = ru < umn ? ru : umn; umx = ru2 > umx ? ru2 : umx;
+        wmn = rd < wmn ? rd : wmn; wmx = rd2 > wmx ? rd2 : wmx;
       }
       if (fam & F_ORD) {  // CM:379-480: top_k(k).min() <= v, v <= bottom_k(50).max()
         p50 *= (pk && vf >= th50) ? q : 1.0;
