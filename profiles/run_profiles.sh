@@ -15,7 +15,7 @@ export TMPDIR=/tmp
 cd /tmp
 BENCH=("$R/bench.py" --no-cpu-baseline --no-extras)
 
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/trace" -o trace --output-format csv \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv \
   -- python3 "${BENCH[@]}" --steps "$STEPS" --warmup 1 > "$OUT/trace_bench.log" 2>&1
 
 for pmc in "FETCH_SIZE" "WRITE_SIZE" \
@@ -26,4 +26,5 @@ for pmc in "FETCH_SIZE" "WRITE_SIZE" \
   timeout -s KILL 240 rocprofv3 --pmc $pmc --kernel-include-regex k_stage1 -d "$OUT/pmc_$name" -o pmc \
     --output-format csv -- python3 "${BENCH[@]}" --steps 1 --warmup 0 > "$OUT/pmc_$name.log" 2>&1
 done
+find "$OUT" -name "*kernel_trace.csv" -delete
 echo "profiles done: $OUT"
