@@ -256,13 +256,9 @@ __device__ __forceinline__ uint32_t swz_xor4(uint32_t x) {
 // partner value for lane xor M (M in {1,2,3,4,7,8,15}) of element register x
 template <int M>
 __device__ __forceinline__ uint32_t gpartner(uint32_t x) {
-  if constexpr (M == 1) return dpp_full<QP_XOR1>(x);
-  else if constexpr (M == 2) return dpp_full<QP_XOR2>(x);
-  else if constexpr (M == 3) return dpp_full<QP_XOR3>(x);
-  else if constexpr (M == 4) return swz_xor4(x);
-  else if constexpr (M == 7) return dpp_full<ROW_HALF_MIRROR>(x);
-  else if constexpr (M == 8) return dpp_full<ROW_ROR8>(x);
-  else return dpp_full<ROW_MIRROR>(x);
+  // ds_swizzle (bit mode, xor M inside 32 lanes): the exchange runs on the LDS pipe and
+  // leaves the VALU (the sorted kernels' limit) to the compare-exchanges
+  return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (M << 10));
 }
 // one cross-lane step: lane partner g ^ M, register k paired with partner register
 // FLIP ? 15-k : k; the lane whose bit LB is clear keeps the minimum
