@@ -114,8 +114,9 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 
 // FULL: every family of SET is requested (the usual case), so the family tests fold
 // away at compile time instead of branching per bar
+// set B stages 8-bar chunks (two in flight) and fits 168 VGPRs: three waves per SIMD
 template <uint32_t SET, bool FULL>
-__global__ __launch_bounds__(256, 2) void k_stage1s(SArgs a) {
+__global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) {
   const uint32_t fam = FULL ? SET : (a.fam & SET);
   const int ntile = (a.S + 255) / 256;
   const int d = blockIdx.x / ntile;
@@ -252,9 +253,12 @@ __global__ __launch_bounds__(256, 2) void k_stage1s(SArgs a) {
       const double prod = vx * vy;
       if (prod != 0.0) {
         const double ip = frcp(prod);
-        sq += sqrt(cv) * ip;          // cov**0.5 / (vx*vy)   CM:137
-        scs += cv * cv * ip;          // cov**2 / (vx*vy)     CM:212
-        scr += cv * sqrt(prod) * ip;  // cov / (vx*vy)**0.5   CM:261
+        double sp, rp, sc, rc;
+        fsqrt2(prod, sp, rp);  // prod < 0: NaN, as sqrt(prod)
+        fsqrt2(cv, sc, rc);    // cv < 0: NaN, as cov**0.5
+        sq += (cv == 0.0 ? 0.0 : sc) * ip;  // cov**0.5 / (vx*vy)   CM:137
+        scs += cv * cv * ip;                // cov**2 / (vx*vy)     CM:212
+        scr += cv * rp;                     // cov / (vx*vy)**0.5   CM:261
         ++Wq;
       }
       if (W == 0) b0 = beta;  // betas shifted by the first one (a member)
@@ -399,9 +403,18 @@ __global__ __launch_bounds__(256, 2) void k_stage1s(SArgs a) {
     constexpr int NP = __builtin_popcount(PLM);
     constexpr bool LAG = (SET & F_OLS) != 0u;
     constexpr int NB = LAG ? 2 * NP : NP;  // images: the planes, then their lag copies
-    __shared__ __attribute__((aligned(16))) float4 sbuf[4][NB][256];
+    // chunk = CQ quads (4*CQ bars) per stock-day; the lag sets use 8-bar chunks so the
+    // staged registers (NB*CQ float4) leave room for a third wave per SIMD
+    constexpr int CQ = (SET == kSerB) ? 2 : 4, BC = 4 * CQ;
+    constexpr int NBUF = (SET == kSerB) ? 2 : 1;  // chunks in flight ahead of the one in use
+    constexpr int LAGC = 48 / BC;                 // lag bar t-50 = chunk c-LAGC, element j-2
+    __shared__ __attribute__((aligned(16))) float4 sbufA[4][NB][64 * CQ];
+    __shared__ __attribute__((aligned(16))) float4 sbufB[NBUF == 2 ? 4 : 1][NB][64 * CQ];
     const int lane = (int)(threadIdx.x & 63u), wave = (int)(threadIdx.x >> 6);
-    float4(*sb)[256] = sbuf[wave];
+    float4(*sbA)[64 * CQ] = sbufA[wave];
+    float4(*sbB)[64 * CQ] = NBUF == 2 ? sbufB[NBUF == 2 ? wave : 0] : sbufA[wave];
+    // source-quad swizzle: a 16-lane ds_read_b128 phase touches distinct banks
+    auto swz = [](int r) { return CQ == 4 ? (r >> 2) & 3 : (r >> 3) & 1; };
     const float* pbase[NP];
     {
       int pi = 0;
@@ -410,20 +423,20 @@ __global__ __launch_bounds__(256, 2) void k_stage1s(SArgs a) {
         if ((PLM >> p) & 1u) pbase[pi++] = a.fld[p];
     }
     const int rowbase = s0 + 64 * wave;
-    auto dma = [&](int c, int img0) {
+    auto dma = [&](float4(*sb)[64 * CQ], int c, int img0) {
 #pragma unroll
       for (int pi = 0; pi < NP; ++pi)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 16 * i + (lane >> 2);
-          const int k = (lane & 3) ^ ((r >> 2) & 3);
+        for (int i = 0; i < CQ; ++i) {
+          const int r = (64 / CQ) * i + lane / CQ;
+          const int k = (lane % CQ) ^ swz(r);
           const size_t row = (size_t)d * a.S + min(rowbase + r, a.S - 1);
-          const float* src = pbase[pi] + row * NBAR + 16 * c + 4 * k;
+          const float* src = pbase[pi] + row * NBAR + BC * c + 4 * k;
           __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)&sb[img0 + pi][64 * i], 16, 0, 0);
         }
     };
-    const int sw = (lane >> 2) & 3;
-    auto toq = [&](const float4 (&X)[NB][4], int img0, int k) {
+    const int sw = swz(lane);
+    auto toq = [&](const float4 (&X)[NB][CQ], int img0, int k) {
       Q4 x;
       x.o = x.h = x.l = x.c = one4;
       x.v = zero4;
@@ -440,40 +453,65 @@ __global__ __launch_bounds__(256, 2) void k_stage1s(SArgs a) {
         }
       return x;
     };
-    Q4 carry;  // lag bars 14, 15 of chunk c-4 (in .z .w)
+    Q4 carry;  // lag bars BC-2, BC-1 of chunk c-1-LAGC (in .z .w)
     carry.o = carry.h = carry.l = carry.c = one4;
     carry.v = zero4;
     uint32_t pw1 = 0u, pw2 = 0u;  // mask words w-1, w-2
-    dma(0, 0);
-    for (int w = 0; w < 8; ++w) {
-      const uint32_t bits = mw[0];
-      const uint32_t lbits = (pw1 << 18) | (pw2 >> 14);  // bit i: bar 32w + i - 50
-      const int nc = (w == 7) ? 1 : 2;                   // bars 224..239: one chunk
-      for (int h = 0; h < nc; ++h) {
-        const int c = 2 * w + h;
-        float4 X[NB][4];
+    auto step = [&](float4(*sb)[64 * CQ], int c, int h, uint32_t bits, uint32_t lbits) {
+      float4 X[NB][CQ];
+      if constexpr (NBUF == 2 && NB == 2 && CQ == 2) {
+        // two chunks in flight: the compiler would wait for every LDS-DMA (vmcnt(0))
+        // before a ds_read, so the reads are issued here after waiting only for chunk
+        // c (chunk c+1's NB*CQ DMA instructions, issued last, may stay outstanding;
+        // vector memory operations complete in issue order)
+        const uint32_t a0 = (uint32_t)(uintptr_t)(lptr_t)&sb[0][CQ * lane + sw];
+        const uint32_t a1 = (uint32_t)(uintptr_t)(lptr_t)&sb[0][CQ * lane + (1 ^ sw)];
+#define MFF_RD4(N)                                                                       \
+  asm volatile("s_waitcnt vmcnt(" #N ")\n\t"                                          \
+               "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\t"                      \
+               "ds_read_b128 %2, %4 offset:%6\n\tds_read_b128 %3, %5 offset:%6\n\t"    \
+               "s_waitcnt lgkmcnt(0)"                                                    \
+               : "=&v"(X[0][0]), "=&v"(X[0][1]), "=&v"(X[1][0]), "=&v"(X[1][1])          \
+               : "v"(a0), "v"(a1), "i"(64 * CQ * 16)                                     \
+               : "memory")
+        if (c + 1 < NBAR / BC) MFF_RD4(4);
+        else MFF_RD4(0);
+#undef MFF_RD4
+      } else {
 #pragma unroll
         for (int ii = 0; ii < NB; ++ii)
 #pragma unroll
-          for (int k = 0; k < 4; ++k) X[ii][k] = sb[ii][4 * lane + (k ^ sw)];
+          for (int k = 0; k < CQ; ++k) X[ii][k] = sb[ii][CQ * lane + (k ^ sw)];
         // the reads have returned before the DMA refills the buffers
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (c + 1 < NBAR / 16) {
-          dma(c + 1, 0);
-          if (LAG && c + 1 >= 3) dma(c - 2, NP);
-        }
+      }
+      if (c + NBUF < NBAR / BC) {
+        dma(sb, c + NBUF, 0);
+        if (LAG && c + 1 >= LAGC) dma(sb, c + 1 - LAGC, NP);
+      }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const Q4 x = toq(X, 0, k);
-          if constexpr (LAG) {
-            const Q4 l1 = toq(X, NP, k);
-            const Q4 l0 = k > 0 ? toq(X, NP, k - 1) : carry;
-            quad(16 * c + 4 * k, bits >> (16 * h + 4 * k), lbits >> (16 * h + 4 * k), x, l0.h, l0.l, l1.h, l1.l);
-          } else {
-            quad(16 * c + 4 * k, bits >> (16 * h + 4 * k), 0u, x, one4, one4, one4, one4);
-          }
+      for (int k = 0; k < CQ; ++k) {
+        const Q4 x = toq(X, 0, k);
+        if constexpr (LAG) {
+          const Q4 l1 = toq(X, NP, k);
+          const Q4 l0 = k > 0 ? toq(X, NP, k - 1) : carry;
+          quad(BC * c + 4 * k, bits >> (BC * h + 4 * k), lbits >> (BC * h + 4 * k), x, l0.h, l0.l, l1.h, l1.l);
+        } else {
+          quad(BC * c + 4 * k, bits >> (BC * h + 4 * k), 0u, x, one4, one4, one4, one4);
         }
-        if constexpr (LAG) carry = toq(X, NP, 3);
+      }
+      if constexpr (LAG) carry = toq(X, NP, CQ - 1);
+    };
+    dma(sbA, 0, 0);
+    if constexpr (NBUF == 2) dma(sbB, 1, 0);
+    for (int w = 0; w < 8; ++w) {
+      const uint32_t bits = mw[0];
+      const uint32_t lbits = (pw1 << 18) | (pw2 >> 14);  // bit i: bar 32w + i - 50
+      const int nc = (w == 7 ? 16 : 32) / BC;            // bars 224..239: half a word
+      for (int h = 0; h < nc; h += NBUF) {
+        const int c = (32 / BC) * w + h;
+        step(sbA, c, h, bits, lbits);
+        if constexpr (NBUF == 2) step(sbB, c + 1, h + 1, bits, lbits);
       }
 #pragma unroll
       for (int i = 0; i < 7; ++i) mw[i] = mw[i + 1];
