@@ -28,8 +28,9 @@ constexpr int K = 16;  // bars per lane
 
 template <int CTRL>
 __device__ __forceinline__ int dpp_i(int x) {
-  // lanes whose source is outside the row keep `old` = 0 (identity for sums / scans)
-  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, false);
+  // lanes whose source is outside the row read 0 (bound_ctrl: identity for sums /
+  // scans) without a register holding an `old` value to copy first
+  return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, true);
 }
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u(uint32_t x) { return (uint32_t)dpp_i<CTRL>((int)x); }
@@ -264,12 +265,13 @@ __device__ __forceinline__ uint32_t gpartner(uint32_t x) {
 // FLIP ? 15-k : k; the lane whose bit LB is clear keeps the minimum
 template <int M, int LB, bool FLIP>
 __device__ __forceinline__ void gcross(uint32_t (&a)[K]) {
-  const bool lower = (gi() & LB) == 0;
+  // one v_med3_u32 per register: med3(x, p, 0) = min, med3(x, p, ~0) = max
+  const uint32_t bound = (gi() & LB) == 0 ? 0u : 0xFFFFFFFFu;
   uint32_t p[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) p[k] = gpartner<M>(a[FLIP ? K - 1 - k : k]);
 #pragma unroll
-  for (int k = 0; k < K; ++k) a[k] = lower ? min(a[k], p[k]) : max(a[k], p[k]);
+  for (int k = 0; k < K; ++k) asm("v_med3_u32 %0, %1, %2, %3" : "=v"(a[k]) : "v"(a[k]), "v"(p[k]), "v"(bound));
 }
 template <int J, bool FLIP>
 __device__ __forceinline__ void glocal(uint32_t (&a)[K]) {
