@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
     Res R;
     R.r[0] = R.r[1] = R.r[2] = R.r[3] = 0.0;
     R.st = 0u;
-    double qv[5] = {qnan(), qnan(), qnan(), qnan(), qnan()};
+    double qv = qnan();  // lane t < 5: doc_pdf query t (the level close ratio)
 
     if (n > 0) {
       // ---------------------------------------------------------------- loads
@@ -744,23 +744,21 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
         // Closes are > 0, so the float order is the bit order; absent bars sort last.
         // A stock-day with a non-integral volume still sorts (volume 0) for the level
         // list, and its LVL/PDF values go to the exact path.
-        bool ok = true;
+        uint32_t vokm = 0u;  // bars with an integral volume in [0, 2^24]
         uint32_t cmx = 0u, cmn = 0xffffffffu;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const bool pk = (pb >> k) & 1u;
-          const bool vok = (v[k] == rintf(v[k])) && (v[k] >= 0.0f) && (v[k] <= 16777216.0f);
-          if (pk) {
-            ok = ok && vok;
-            cmx = max(cmx, fbits(c[k]));
-            cmn = min(cmn, fbits(c[k]));
-          }
+          const bool vok = (v[k] == rintf(v[k])) & (v[k] >= 0.0f) & (v[k] <= 16777216.0f);
+          vokm |= (vok ? 1u : 0u) << k;
+          cmx = max(cmx, pk ? fbits(c[k]) : 0u);
+          cmn = min(cmn, pk ? fbits(c[k]) : 0xffffffffu);
         }
+        const bool ok = (pb & ~vokm) == 0u;
         cmx = gmax_u(cmx);
         cmn = gmin_u(cmn);
         const double clast = (double)gval(c, lb);
         bool fast = !gany(!ok);
-        double q[5] = {qnan(), qnan(), qnan(), qnan(), qnan()};
         const int e0 = 16 * g;
         uint32_t cw[K], vv[K], cbase = cmx;
         // a day whose closes span >= 2^24 float steps (a close ratio of 2 or more) does
@@ -780,8 +778,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
 #pragma unroll
           for (int k = 0; k < K; ++k) {
             const bool pk = (pb >> k) & 1u;
-            const bool vok = (v[k] == rintf(v[k])) && (v[k] >= 0.0f) && (v[k] <= 16777216.0f);
-            sv[e0 + k] = (pk && vok) ? (uint32_t)v[k] : 0u;
+            sv[e0 + k] = ((pb & vokm) >> k) & 1u ? (uint32_t)v[k] : 0u;
             key[k] = pk ? ((cmx - fbits(c[k])) << 8) | (uint32_t)(e0 + k) : 0xffffffffu;
           }
           gsort256u(key);
@@ -840,25 +837,12 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           // 20*cum > k*Sv, i.e. cum > floor(k*Sv/20) (integers); an exact tie
           // 20*cum == k*Sv at a level (only when 20 | k*Sv) is left to the exact path.
           // floor(k*Sv/20) = k*(Sv/20) + (k*(Sv%20))/20 in u32.
-          const uint32_t kk[5] = {12u, 14u, 16u, 18u, 19u};
-          const uint32_t sq20 = Sv / 20u, sr20 = Sv - 20u * sq20;
-          uint32_t T[5];
-          bool dv[5];
-#pragma unroll
-          for (int t = 0; t < 5; ++t) {
-            const uint32_t b = kk[t] * sr20;  // < 380
-            const uint32_t bq = b / 20u;
-            T[t] = kk[t] * sq20 + bq;
-            dv[t] = b == 20u * bq;
-          }
           // the lane's first level continues from the previous lane's last one
           uint32_t pcum = 0u, pe = 0xFFFFFFFFu;  // (cum, last element) before level l0
           if (l0 > 0 && l0 <= L) {
             pcum = lv[l0 - 1];
             pe = lc[l0 - 1] & 0xFFu;
           }
-          int cnt[5] = {0, 0, 0, 0, 0};
-          bool tie = false;
           double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
           uint64_t* kd = a.lvl_key ? a.lvl_key + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
           uint8_t* wd = a.lvl_w ? a.lvl_w + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
@@ -877,13 +861,6 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
                 const double dd = (double)V * inv - x0, d2 = dd * dd;
                 s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
               }
-              if (fam & F_PDF) {
-#pragma unroll
-                for (int t = 0; t < 5; ++t) {
-                  cnt[t] += c2 <= T[t] ? 1 : 0;
-                  tie = tie || (dv[t] && c2 == T[t]);
-                }
-              }
               if (kd) {  // doc_pdf level list: key c_last / close (IEEE), bars
                 kd[base + l] = ord64(clast / (double)bitsf(cbase - (cwb >> 8)));
                 wd[base + l] = (uint8_t)bars;
@@ -901,14 +878,23 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             R.val(41, sk);  // doc_std: .skew() [sic CM:999]
           }
           if (fast && (fam & F_PDF)) {
-            if (gany(tie) && Sv != 0u) fast = false;  // the reference's float order decides
+            // lane t < 5 answers query t: levels with cum <= T come first (cum is
+            // monotone), so their count e is found by binary search over lv
+            const uint32_t kt = g == 0 ? 12u : g == 1 ? 14u : g == 2 ? 16u : g == 3 ? 18u : 19u;
+            const uint32_t sq20 = Sv / 20u, sr20 = Sv - 20u * sq20;
+            const uint32_t b = kt * sr20;  // < 380
+            const uint32_t bq = b / 20u;
+            const uint32_t T = kt * sq20 + bq;
+            int e = 0;
 #pragma unroll
-            for (int t = 0; t < 5; ++t) {
-              // levels with cum <= T come first (cum is monotone); Sv = 0: shares NaN,
-              // NaN > p (S11) -> the first level
-              const int e = Sv == 0u ? 0 : gsum_i(cnt[t]);
-              if (e < L) q[t] = clast / (double)bitsf(cbase - (lc[e] >> 8));
-            }
+            for (int st = 128; st >= 1; st >>= 1)
+              if (e + st <= L && lv[e + st - 1] <= T) e += st;
+            // an exact tie 20*cum == k*Sv is at the last level with cum <= T
+            const bool tie = g < 5 && b == 20u * bq && e > 0 && lv[e - 1] == T;
+            if (gany(tie) && Sv != 0u) fast = false;  // the reference's float order decides
+            // Sv = 0: shares NaN, NaN > p (S11) -> the first level
+            if (Sv == 0u) e = 0;
+            if (g < 5 && e < L) qv = clast / (double)bitsf(cbase - (lc[e] >> 8));
           }
           lds_fence();
         }
@@ -919,11 +905,9 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
           }
         }
         if (fam & F_PDF) {
+          if (!fast) qv = qnan();
 #pragma unroll
-          for (int t = 0; t < 5; ++t) {
-            qv[t] = q[t];
-            R.null(PDF0 + t);  // filled by mff_pdf_finalize (or the fallback)
-          }
+          for (int t = 0; t < 5; ++t) R.null(PDF0 + t);  // filled by mff_pdf_finalize (or the fallback)
         }
       }
     }
@@ -942,8 +926,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
         }
       }
       if (a.pdfq && g < 5) {
-        const double qq = (g == 0) ? qv[0] : (g == 1) ? qv[1] : (g == 2) ? qv[2] : (g == 3) ? qv[3] : qv[4];
-        a.pdfq[(size_t)g * plane + sd] = qq;
+        a.pdfq[(size_t)g * plane + sd] = qv;
       }
     }
   }
