@@ -9,8 +9,8 @@
 // estimates are good to 5e-8; one Newton (Goldschmidt) step brings the reciprocal to
 // 2.1e-15 and sqrt / rsqrt to 4.2e-15; a * (1/b) corrected by fma(fma(-b, q, a), r, q)
 // is then within about 1 ulp of a/b and returned exactly 1 for every a == b.  A
-// quotient never flips sign.  Nothing here feeds an exact comparison key: doc_pdf keys
-// keep IEEE division (mff_stage1g.hip).
+// quotient never flips sign.  fdiv_f32in is the one exception to "tolerance only" (see
+// there): it is the correctly rounded quotient for float operands.
 // Domain: finite nonzero b (callers guard zero volumes); fsqrt2 needs x > 0 for
 // finite results (x < 0 gives NaN in both outputs, as sqrt does).
 #pragma once
@@ -29,6 +29,18 @@ __device__ __forceinline__ double fdivr(double a, double b, double r) {
   return fma(fma(-b, q, a), r, q);
 }
 __device__ __forceinline__ double fdiv(double a, double b) { return fdivr(a, b, frcp(b)); }
+// a / b correctly rounded (bit-identical to IEEE f64 division) when a and b are f64
+// images of positive normal floats, as the doc_pdf keys c_last / c are.  Why: with
+// 24-bit significands A, B, the exact quotient is at least 2^-78 (relative) away from
+// any midpoint between doubles unless it is exact (A*2^-j - M*B is a nonzero integer
+// for the 54-bit midpoint M), while q0 = a * r is within an ulp, the remainder
+// fma(-b, q0, a) is exact, and fma(e, r, q0) differs from a/b by at most
+// ulp * |r*b - 1| <= 2^-53 * 2^-48 relative before its single rounding.  Checked on
+// 3.4e10 random pairs against the hardware IEEE quotient (profiles/ubench/fdiv_exact.hip).
+__device__ __forceinline__ double fdiv_f32in(float a, float b) {
+  const double A = (double)a, B = (double)b;
+  return fdivr(A, B, frcp(B));
+}
 // sqrt(x) and 1/sqrt(x) for x > 0: hardware rsq estimate plus one Goldschmidt step
 __device__ __forceinline__ void fsqrt2(double x, double& sq, double& rsq) {
   const double r = __builtin_amdgcn_rsq(x);

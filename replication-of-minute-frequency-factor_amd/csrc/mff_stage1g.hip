@@ -29,6 +29,7 @@
 
 #include "../../include/mff.h"
 #include "mff_group.h"
+#include "mff_fmath.h"
 #include "mff_stats.h"
 #include "mff_internal.h"
 
@@ -757,7 +758,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
         const bool ok = (pb & ~vokm) == 0u;
         cmx = gmax_u(cmx);
         cmn = gmin_u(cmn);
-        const double clast = (double)gval(c, lb);
+        const float clastf = gval(c, lb);
         bool fast = !gany(!ok);
         const int e0 = 16 * g;
         uint32_t cw[K], vv[K], cbase = cmx;
@@ -861,8 +862,8 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
                 const double dd = (double)V * inv - x0, d2 = dd * dd;
                 s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
               }
-              if (kd) {  // doc_pdf level list: key c_last / close (IEEE), bars
-                kd[base + l] = ord64(clast / (double)bitsf(cbase - (cwb >> 8)));
+              if (kd) {  // doc_pdf level list: key c_last / close (correctly rounded), bars
+                kd[base + l] = dbits(fdiv_f32in(clastf, bitsf(cbase - (cwb >> 8)))) | 0x8000000000000000ull;  // ord64 of a positive
                 wd[base + l] = (uint8_t)bars;
               }
             }
@@ -894,7 +895,7 @@ __global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
             if (gany(tie) && Sv != 0u) fast = false;  // the reference's float order decides
             // Sv = 0: shares NaN, NaN > p (S11) -> the first level
             if (Sv == 0u) e = 0;
-            if (g < 5 && e < L) qv = clast / (double)bitsf(cbase - (lc[e] >> 8));
+            if (g < 5 && e < L) qv = fdiv_f32in(clastf, bitsf(cbase - (lc[e] >> 8)));
           }
           lds_fence();
         }
