@@ -12,7 +12,9 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmff.so")
+# MFF_LIBRARY: another in-tree build of the same sources (A/B timing of two builds in
+# one GPU session, profiles/gpu_ab.sh); the default is the build next to this file
+LIB_PATH = os.environ.get("MFF_LIBRARY") or os.path.join(HERE, "libmff.so")
 
 c_int, c_size_t, c_void_p, c_char_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p
 P = c_void_p  # device pointers travel as void*
