@@ -30,7 +30,8 @@ namespace mff {
 size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w);  // mff_stage1g.hip
 
 constexpr int PDF_MAXM = 32767;  // queries per day (all ranks)
-constexpr int PDF_ZQ = 9200;     // sorted queries per count workgroup (LDS: 16 B each)
+constexpr int PDF_ZQ = 9160;     // sorted queries per count workgroup (LDS: 16 B each)
+constexpr int PDF_PAD = 64;      // ~0 sentinels after the slice's distinct values
 constexpr int PDF_NBK = 8192;    // bucket table over the workgroup's distinct query values
 
 struct QLoader {
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_pdf_sort(const double* q_all, 
 // (n_less in the low word, n_eq in the high word): one ds_add_u64 per binned key.
 // The slice then turns them into (n_less, n_eq) at its positions: below + exclusive scan.
 struct PdfSlice {
-  const uint64_t* L;  // LDS [nq + 2]: Q[P0-1], Q[P0..P1), ~0
+  const uint64_t* L;  // LDS [nq + 1 + PDF_PAD]: Q[P0-1], Q[P0..P1), ~0 x PDF_PAD
   const uint16_t* T;  // LDS [PDF_NBK + 1]
   uint64_t L0, qmin, qmax;
   int nv, sh, steps;
@@ -104,7 +105,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, 
 // Load the slice, keep its DISTINCT values above Q[P0-1] (duplicated queries -- many
 // stock-days share e.g. the key 1.0 -- would otherwise deepen every search), build the
 // bucket table and the search depth.  Block-wide; ends synced.
-//   L[0] = Q[P0-1], L[1..nv] = distinct slice values > L[0], L[nv+1] = ~0
+//   L[0] = Q[P0-1], L[1..nv] = distinct slice values > L[0], L[nv+1 .. nv+PDF_PAD] = ~0
 __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, int P0, int P1,
                                                     uint64_t* L, uint64_t* C, uint16_t* T,
                                                     uint32_t* wsum, int* occ_s) {
@@ -133,7 +134,7 @@ __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, in
   __syncthreads();
   for (int i = threadIdx.x; i < (int)nu; i += blockDim.x) L[1 + i] = C[i];
   for (int i = threadIdx.x; i < nq; i += blockDim.x) C[i] = 0ull;
-  if (threadIdx.x == 0) L[1 + nu] = ~0ull;
+  if (threadIdx.x < PDF_PAD) L[1 + nu + threadIdx.x] = ~0ull;
   __syncthreads();
   PdfSlice sl;
   sl.L = L;
@@ -238,8 +239,8 @@ __global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
   const int P0 = z * a.Mz, P1 = min(a.M, P0 + a.Mz);
   const int nq = P1 - P0;
 
-  uint64_t* L = reinterpret_cast<uint64_t*>(smem);  // [Mz + 2]
-  uint64_t* C = L + a.Mz + 2;                       // [Mz]
+  uint64_t* L = reinterpret_cast<uint64_t*>(smem);  // [Mz + 1 + PDF_PAD]
+  uint64_t* C = L + a.Mz + 1 + PDF_PAD;             // [Mz]
   uint16_t* T = reinterpret_cast<uint16_t*>(C + a.Mz);
   if (threadIdx.x == 0) below_s = 0u;
   const PdfSlice sl = pdf_slice_setup(Q, a.M, P0, P1, L, C, T, wsum, &occ_s);
@@ -251,18 +252,24 @@ __global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
     // blockDim-th entry, UNR at a time (their loads in flight together, their searches
     // interleaved).  A key at or below Q[P0-1] only adds its weight to `below`; a key
     // above the slice belongs to a later slice.  Search: binary lifting from T[b]-1
-    // (L1[T[b]-1] < key <= L1[T[b+1]]), one LDS read, compare and select per step.
+    // (L1[T[b]-1] < key <= L1[T[b+1]]), one LDS read, compare and select per step.  With
+    // at most 6 steps the probes stay inside the PDF_PAD sentinels (probe <= nv + 2^steps
+    // - 2), so the steps are unrolled with constant strides: j is a byte offset and each
+    // probe is one ds_read_b64 with an immediate offset.
     constexpr int UNR = 8;
     const uint64_t* L1 = L + 1;
-    const int nvc = sl.nv;  // L1[nv] = ~0 stops every probe past the end
+    const char* L1b = reinterpret_cast<const char*>(L1);
+    const int nvc = sl.nv;
     const int n = (int)a.lvl_count[d];
     const uint64_t* K = a.lvl_key + (size_t)d * a.cap;
     const uint8_t* Wt = a.lvl_w + (size_t)d * a.cap;
     const int step = (int)blockDim.x * UNR;
+    const int steps = sl.steps;
+    const bool shallow = steps <= 6;
     for (int i0 = (int)threadIdx.x; i0 < n; i0 += step) {
       uint64_t key[UNR];
       uint32_t w[UNR];
-      int j[UNR];
+      int j[UNR];  // byte offset of the probe base into L1 (shallow) or index (deep)
       bool in[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
@@ -280,12 +287,30 @@ __global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
         const int bk = (in[u] && gtmin) ? (int)((key[u] - sl.qmin) >> sl.sh) : 0;
         j[u] = (in[u] && gtmin) ? (int)sl.T[bk] - 1 : -1;
       }
-      for (int bb = (1 << sl.steps) >> 1; bb > 0; bb >>= 1) {
-        uint64_t x[UNR];
+      if (shallow) {
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) x[u] = L1[min(j[u] + bb, nvc)];
+        for (int u = 0; u < UNR; ++u) j[u] *= 8;
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) j[u] = x[u] < key[u] ? j[u] + bb : j[u];
+        for (int st = 5; st >= 0; --st) {
+          if (st < steps) {
+            const int bb = 8 << st;
+            uint64_t x[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) x[u] = *reinterpret_cast<const uint64_t*>(L1b + j[u] + bb);
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) j[u] += x[u] < key[u] ? bb : 0;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) j[u] >>= 3;
+      } else {
+        for (int bb = (1 << steps) >> 1; bb > 0; bb >>= 1) {
+          uint64_t x[UNR];
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) x[u] = L1[min(j[u] + bb, nvc)];
+#pragma unroll
+          for (int u = 0; u < UNR; ++u) j[u] = x[u] < key[u] ? j[u] + bb : j[u];
+        }
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
@@ -329,7 +354,7 @@ __global__ __launch_bounds__(1024) void k_pdf_finalize(PdfArgs a) {
   const uint64_t* Q = a.q_sorted + (size_t)dd * a.M;
   const int P0 = z * a.Mz, P1 = min(a.M, P0 + a.Mz);
   uint64_t* L = reinterpret_cast<uint64_t*>(smem);
-  uint64_t* C = L + a.Mz + 2;
+  uint64_t* C = L + a.Mz + 1 + PDF_PAD;
   uint16_t* T = reinterpret_cast<uint16_t*>(C + a.Mz);
   const PdfSlice sl = pdf_slice_setup(Q, a.M, P0, P1, L, C, T, wsum, &occ_s);
   // counts of each distinct value, from its first sorted position
@@ -376,7 +401,7 @@ int mff_pdf_sort(const double* q_all, int R, int S_loc, int D, int d0, int nd, u
 static void pdf_slices(int M, int& Z, int& Mz, size_t& lds) {
   Z = (M + PDF_ZQ - 1) / PDF_ZQ;
   Mz = (M + Z - 1) / Z;
-  lds = (size_t)(Mz + 2) * 8 + (size_t)Mz * 8 + (size_t)(PDF_NBK + 1) * 2;
+  lds = (size_t)(Mz + 1 + PDF_PAD) * 8 + (size_t)Mz * 8 + (size_t)(PDF_NBK + 1) * 2;
 }
 
 static int pdf_launch(PdfArgs& a, const uint64_t* q_sorted, int M, hipStream_t st, int mode) {
