@@ -43,14 +43,28 @@ struct QLoader {
     const double x = q[((size_t)rt * D + d) * S + s];
     return __builtin_isnan(x) ? ~0ull : ord64(x);
   }
+  // (row, column) view for segment_sort_binned: row r*5+t, column s
+  int nrow;
+  __device__ int rows() const { return nrow; }
+  __device__ int cols() const { return S; }
+  __device__ uint64_t at(int rt, int s) const {
+    const double x = q[((size_t)rt * D + d) * S + s];
+    return __builtin_isnan(x) ? ~0ull : ord64(x);
+  }
 };
 
 __global__ __launch_bounds__(SORT_THREADS) void k_pdf_sort(const double* q_all, int R, int S, int D,
                                                            int d0, uint64_t* q_sorted, uint64_t* tmp) {
-  __shared__ uint64_t sk[SORT_CAP];
+  __shared__ uint64_t sk[SORT_CAPB];  // >= SORT_CAP for the merge fallback
+  __shared__ uint32_t bins[SORT_NBIN + 1];
+  __shared__ __attribute__((aligned(8))) uint32_t ctl[64];
   const int dd = blockIdx.x;
   const int M = R * 5 * S;
-  QLoader ld{q_all, S, D, d0 + dd};
+  QLoader ld{q_all, S, D, d0 + dd, R * 5};
+  // bucketed (no merge passes) when the day's queries fit the registers and no bin
+  // overflows half a chunk; otherwise chunk sort + global merges
+  if (M <= SORT_REG * SORT_THREADS && segment_sort_binned(ld, M, q_sorted + (size_t)dd * M, sk, bins, ctl))
+    return;
   segment_sort(ld, M, q_sorted + (size_t)dd * M, tmp + (size_t)dd * M, sk);
 }
 

@@ -35,7 +35,7 @@ __device__ __forceinline__ void lds_bitonic(uint64_t* sk, int P) {
   for (int size = 2; size <= P; size <<= 1) {
     for (int j = size >> 1; j > 0; j >>= 1) {
       for (int i = threadIdx.x; i < (P >> 1); i += blockDim.x) {
-        const int lo = 2 * j * (i / j) + (i % j);
+        const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));  // 2j*(i/j) + i%j, j a power of 2
         const int hi = lo + j;
         const bool up = (lo & size) == 0;
         const uint64_t x = sk[lo], y = sk[hi];
@@ -47,6 +47,82 @@ __device__ __forceinline__ void lds_bitonic(uint64_t* sk, int P) {
       __syncthreads();
     }
   }
+}
+
+// 1024*E-key bitonic sort of LDS `sk` by a 1024-thread block with the keys in
+// registers: thread t holds elements E*t .. E*t+E-1, so compare-exchange distances
+// below E are in-thread, E .. 32E are lane exchanges inside the wave (ds_swizzle /
+// bpermute, no barrier), and only distances >= 64E go through LDS with barriers
+// (10 of the 91 stages for E = 8).
+template <int M>
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t x) {
+  int lo = (int)(uint32_t)x, hi = (int)(uint32_t)(x >> 32);
+  if constexpr (M < 32) {
+    lo = __builtin_amdgcn_ds_swizzle(lo, 0x1F | (M << 10));
+    hi = __builtin_amdgcn_ds_swizzle(hi, 0x1F | (M << 10));
+  } else {
+    lo = __shfl_xor(lo, M, 64);
+    hi = __shfl_xor(hi, M, 64);
+  }
+  return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+}
+template <int E, int SIZE, int J>
+__device__ __forceinline__ void bitonic_reg_stage(uint64_t (&x)[E], int tid, uint64_t* sk) {
+  if constexpr (J < E) {
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+      if (r & J) continue;
+      const bool up = ((tid * E + r) & SIZE) == 0;
+      const uint64_t a = x[r], b = x[r | J];
+      const bool sw = (a > b) == up;
+      x[r] = sw ? b : a;
+      x[r | J] = sw ? a : b;
+    }
+  } else {
+    constexpr int M = J / E;
+    const bool up = ((tid * E) & SIZE) == 0;
+    const bool keep_min = ((tid & M) == 0) == up;
+    if constexpr (M < 64) {
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        const uint64_t p = lane_xor64<M>(x[r]);
+        x[r] = ((x[r] < p) == keep_min) ? x[r] : p;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < E; ++r) sk[tid * E + r] = x[r];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < E; ++r) {
+        const uint64_t p = sk[(tid ^ M) * E + r];
+        x[r] = ((x[r] < p) == keep_min) ? x[r] : p;
+      }
+      __syncthreads();
+    }
+  }
+}
+template <int E, int SIZE, int J>
+__device__ __forceinline__ void bitonic_reg_merge(uint64_t (&x)[E], int tid, uint64_t* sk) {
+  bitonic_reg_stage<E, SIZE, J>(x, tid, sk);
+  if constexpr (J > 1) bitonic_reg_merge<E, SIZE, J / 2>(x, tid, sk);
+}
+template <int E, int SIZE>
+__device__ __forceinline__ void bitonic_reg_sizes(uint64_t (&x)[E], int tid, uint64_t* sk) {
+  bitonic_reg_merge<E, SIZE, SIZE / 2>(x, tid, sk);
+  if constexpr (SIZE < 1024 * E) bitonic_reg_sizes<E, SIZE * 2>(x, tid, sk);
+}
+// requires blockDim.x == 1024; sorts sk[0 .. 1024*E); ends synced
+template <int E>
+__device__ __forceinline__ void bitonic_regs(uint64_t* sk) {
+  const int tid = (int)threadIdx.x;
+  uint64_t x[E];
+#pragma unroll
+  for (int r = 0; r < E; ++r) x[r] = sk[tid * E + r];
+  __syncthreads();
+  bitonic_reg_sizes<E, 2>(x, tid, sk);
+#pragma unroll
+  for (int r = 0; r < E; ++r) sk[tid * E + r] = x[r];
+  __syncthreads();
 }
 
 // Loader: uint64_t operator()(int i) const -> key of element i of this segment.
@@ -100,6 +176,132 @@ __device__ void segment_sort(const Loader& ld, int M, uint64_t* out, uint64_t* t
   __syncthreads();
   if (src != out)
     for (int i = threadIdx.x; i < M; i += blockDim.x) out[i] = src[i];
+}
+
+// Bucketed segment sort (no merge passes) for M = ld.rows() * ld.cols() <= 32 * blockDim
+// keys (loader: uint64_t at(row, col)): a histogram over
+// NBIN bins of (key - kmin) >> sh groups the keys (read through the loader once per
+// pass: min/max, histogram, and once per range for the placement), the bins
+// are cut into consecutive ranges of at most SORT_CAP keys, and each range is placed
+// in LDS bin by bin (atomic cursors), bitonic-sorted and written to its final offset.
+// Keys ~0 (NaN queries) go last without binning.  Returns false (nothing written) when
+// one bin holds more than SORT_CAPB/2 keys: the caller then uses segment_sort.
+// LDS: sk [SORT_CAPB] keys, bins [SORT_NBIN + 1] u32, ctl [64] u32.  Ranges are sorted
+// by bitonic_regs<E> over the smallest 1024*E (E = 2..16) slots that hold them.
+constexpr int SORT_NBIN = 2048;
+constexpr int SORT_CAPB = 8192;  // keys per range (with the bins: 72 KiB of LDS, two workgroups per CU)
+constexpr int SORT_REG = 32;  // segment_sort_binned takes M <= SORT_REG * blockDim
+template <typename Loader>
+__device__ bool segment_sort_binned(const Loader& ld, int M, uint64_t* out, uint64_t* sk, uint32_t* bins,
+                                    uint32_t* ctl) {
+  const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
+  uint64_t mn = ~0ull, mx = 0ull;
+  // the loader is walked as (row, column) so no thread divides an index
+  for (int rw = 0; rw < ld.rows(); ++rw)
+    for (int c = tid; c < ld.cols(); c += nt) {
+      const uint64_t k = ld.at(rw, c);
+      if (k != ~0ull) {
+        mn = min(mn, k);
+        mx = max(mx, k);
+      }
+    }
+  // block min / max (ctl[0..1] lo/hi of min, ctl[2..3] of max, via 64-bit atomics)
+  unsigned long long* c64 = reinterpret_cast<unsigned long long*>(ctl);
+  if (tid == 0) {
+    c64[0] = ~0ull;
+    c64[1] = 0ull;
+  }
+  for (int i = tid; i <= SORT_NBIN; i += nt) bins[i] = 0u;
+  __syncthreads();
+  atomicMin(&c64[0], (unsigned long long)mn);
+  atomicMax(&c64[1], (unsigned long long)mx);
+  __syncthreads();
+  const uint64_t kmin = c64[0], kmax = c64[1];
+  const bool any = kmin != ~0ull;
+  int sh = 0;
+  while (any && ((kmax - kmin) >> sh) >= (uint64_t)SORT_NBIN) ++sh;
+  for (int rw = 0; rw < ld.rows(); ++rw)
+    for (int c = tid; c < ld.cols(); c += nt) {
+      const uint64_t k = ld.at(rw, c);
+      if (k != ~0ull) atomicAdd(&bins[(uint32_t)((k - kmin) >> sh)], 1u);
+    }
+  __syncthreads();
+  // exclusive scan of the bins (SORT_NBIN / nt contiguous bins per thread), max bin
+  const int per = SORT_NBIN / nt;
+  uint32_t loc = 0u, mb = 0u;
+  for (int i = 0; i < per; ++i) {
+    const uint32_t c = bins[tid * per + i];
+    loc += c;
+    mb = max(mb, c);
+  }
+  uint32_t incl = loc;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+    if ((tid & 63) >= o) incl += y;
+  }
+  for (int o = 32; o > 0; o >>= 1) mb = max(mb, (uint32_t)__shfl_xor((int)mb, o, 64));
+  uint32_t* wsum = ctl + 8;  // [16] wave totals, ctl[24] max bin, ctl[25] total
+  const int wave = tid >> 6, nw = nt >> 6;
+  if ((tid & 63) == 63) wsum[wave] = incl;
+  if (tid == 0) ctl[24] = 0u;
+  __syncthreads();
+  if ((tid & 63) == 0) atomicMax(&ctl[24], mb);
+  uint32_t off = incl - loc, tot = 0u;
+  for (int w = 0; w < nw; ++w) {
+    if (w < wave) off += wsum[w];
+    tot += wsum[w];
+  }
+  __syncthreads();
+  const uint32_t maxbin = ctl[24];
+  if (maxbin > (uint32_t)SORT_CAPB / 2 || nt != 1024) return false;
+  for (int i = 0; i < per; ++i) {
+    const uint32_t c = bins[tid * per + i];
+    bins[tid * per + i] = off;
+    off += c;
+  }
+  if (tid == 0) bins[SORT_NBIN] = tot;
+  // ranges: bin b belongs to range start[b] / T (T + maxbin <= SORT_CAPB)
+  const uint32_t T = (uint32_t)SORT_CAPB - maxbin;
+  int* rbeg = reinterpret_cast<int*>(ctl + 32);  // [32] first bin of each range, -1 = empty
+  if (tid < 32) rbeg[tid] = -1;
+  __syncthreads();
+  for (int b = tid; b < SORT_NBIN; b += nt) {
+    const uint32_t r = bins[b] / T;
+    if (b == 0 || bins[b - 1] / T != r) rbeg[r] = b;
+  }
+  __syncthreads();
+  const int nr = tot == 0u ? 0 : (int)((tot - 1u) / T) + 1;
+  int b0 = 0;
+  for (int r = 0; r < nr; ++r) {
+    if (rbeg[r] < 0) continue;
+    b0 = rbeg[r];
+    int b1 = SORT_NBIN;
+    for (int q = r + 1; q < nr; ++q)
+      if (rbeg[q] >= 0) { b1 = rbeg[q]; break; }
+    const uint32_t base = bins[b0], size = bins[b1] - base;
+    int P = 2048;
+    while (P < (int)size) P <<= 1;
+    __syncthreads();  // the previous range's readers are done with sk
+    for (int i = tid; i < P; i += nt) sk[i] = ~0ull;
+    __syncthreads();
+    for (int rw = 0; rw < ld.rows(); ++rw)
+      for (int c = tid; c < ld.cols(); c += nt) {
+        const uint64_t k = ld.at(rw, c);
+        if (k == ~0ull) continue;
+        const int b = (int)((k - kmin) >> sh);
+        if (b >= b0 && b < b1) sk[atomicAdd(&bins[b], 1u) - base] = k;
+      }
+    __syncthreads();
+    switch (P) {
+      case 2048: bitonic_regs<2>(sk); break;
+      case 4096: bitonic_regs<4>(sk); break;
+      default: bitonic_regs<8>(sk); break;
+    }
+    for (int i = tid; i < (int)size; i += nt) out[base + i] = sk[i];
+  }
+  for (int i = (int)tot + tid; i < M; i += nt) out[i] = ~0ull;
+  __syncthreads();
+  return true;
 }
 
 }  // namespace mff
