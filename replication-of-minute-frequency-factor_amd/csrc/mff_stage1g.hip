@@ -169,7 +169,8 @@ constexpr uint32_t G_LVL = F_LVL | F_PDF;    // close, volume
 constexpr uint32_t kGroups[2] = {G_ORD, G_LVL};
 
 template <uint32_t SET>
-__global__ __launch_bounds__(256) void k_stage1g(GArgs a) {
+// (256, 4): at most 128 VGPRs, four waves per SIMD (the LVL set would take 139 and three)
+__global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t scratch[16][NB];  // 2 KB per group
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;

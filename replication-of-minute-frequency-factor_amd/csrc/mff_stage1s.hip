@@ -291,11 +291,11 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
         ndn += dn ? 1 : 0;
         u1 += up ? dd : 0.0; u2 += up ? d2 : 0.0;
         w1 += dn ? dd : 0.0; w2 += dn ? d2 : 0.0;
-        // min / max as plain compares + selects of candidates (+-inf when not in the set)
+        // min / max of candidates (+-inf when not in the set): one v_min/v_max_f64 each
         const double ru = up ? r : __builtin_inf(), rd = dn ? r : __builtin_inf();
         const double ru2 = up ? r : -__builtin_inf(), rd2 = dn ? r : -__builtin_inf();
-        umn = ru < umn ? ru : umn; umx = ru2 > umx ? ru2 : umx;
-        wmn = rd < wmn ? rd : wmn; wmx = rd2 > wmx ? rd2 : wmx;
+        umn = __builtin_fmin(umn, ru); umx = __builtin_fmax(umx, ru2);
+        wmn = __builtin_fmin(wmn, rd); wmx = __builtin_fmax(wmx, rd2);
       }
       if (fam & F_ORD) {  // CM:379-480: top_k(k).min() <= v, v <= bottom_k(50).max()
         p50 *= (pk && vf >= th50) ? q : 1.0;
