@@ -35,6 +35,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "replication-of-minute-frequency-factor_amd")
 sys.path.insert(0, PKG)
@@ -78,6 +80,86 @@ def load_pmc(S_loc: int, D: int):
     return pmc
 
 
+INGEST_ROW_BYTES = 56 + 20 + 32 / 240  # per row: index/time/OHLCV in, 5 fp32 out, mask words
+
+
+def ingest_extras(panel, days: int, host_days: int):
+    """Long -> dense ingest (mff_ingest_rows) on `days` days of the
+    bench panel turned into device-resident long rows (the full 240-bar grid of every
+    stock-day): kernel time by HIP events on its stream, algorithmic GB/s; then the
+    PCIe-inclusive host path (pyarrow encode + pinned H2D + kernel) on `host_days` days."""
+    import pyarrow as pa
+    import torch
+    from mff import _lib, ingest, synth
+
+    lib = _lib.load()
+    dev = panel.device
+    S, D = panel.S, min(days, panel.D)
+    mm = torch.arange(240, device=dev)
+    pres = ((panel.mask[:D][..., mm // 32] >> (mm % 32)) & 1).bool()  # [D][S][240]
+    idx = pres.reshape(-1).nonzero().squeeze(1)  # present bars, (day, stock, minute) order
+    n = int(idx.numel())
+    m = idx % 240
+    stock = ((idx // 240) % S).to(torch.int32)
+    day = (idx // (240 * S)).to(torch.int32)
+    clock = torch.where(m < 120, 570 + m, 660 + m)
+    tm = (clock // 60) * 10000000 + (clock % 60) * 100000
+    cols = [panel.bars[f, :D].reshape(-1)[idx].double() for f in range(5)]
+    bars = torch.empty((5, D, S, 240), dtype=torch.float32, device=dev)
+    mask = torch.zeros((D, S, 8), dtype=torch.int32, device=dev)
+    err = torch.zeros(5, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def run():
+        _lib.check(lib.mff_ingest_rows(stock.data_ptr(), day.data_ptr(), tm.data_ptr(),
+                                       *[c.data_ptr() for c in cols], 0, n, S, D,
+                                       bars.data_ptr(), mask.data_ptr(), err.data_ptr(),
+                                       stream.cuda_stream), "mff_ingest_rows")
+    run()
+    torch.cuda.synchronize()
+    ok = (int(err.abs().sum()) == 0 and torch.equal(mask, panel.mask[:D])
+          and torch.equal(bars[:, pres], panel.bars[:, :D][:, pres]))
+    reps, ms = 5, 0.0
+    for _ in range(reps):
+        mask.zero_()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        run()
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms += a.elapsed_time(b) / reps
+    out = {"ingest_kernel_ms": round(ms, 3), "ingest_rows": n,
+           "ingest_kernel_GBps": round(n * INGEST_ROW_BYTES / (ms * 1e-3) / 1e9, 1),
+           "ingest_kernel_frac_hbm": round(n * INGEST_ROW_BYTES / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
+           "ingest_roundtrip_ok": bool(ok)}
+    del idx, m, stock, day, clock, tm, cols, bars, mask, err, pres
+    # host path: long pyarrow tables (one per day) -> PanelIngest
+    hd = min(host_days, panel.D)
+    pres = synth.unpack_mask(panel.mask[:hd].cpu().numpy().view("uint32"))
+    planes = panel.bars[:, :hd].cpu().numpy()
+    tabs = []
+    for d in range(hd):
+        s_idx, m_idx = pres[d].nonzero()
+        tabs.append(pa.table({
+            "code": pa.array([f"{s:06d}.SZ" for s in range(S)]).take(pa.array(s_idx)),
+            "date": pa.array([d] * s_idx.size, pa.int32()).cast(pa.date32()),
+            "time": pa.array(((np.where(m_idx < 120, 570 + m_idx, 660 + m_idx) // 60) * 10000000
+                              + (np.where(m_idx < 120, 570 + m_idx, 660 + m_idx) % 60) * 100000)
+                             .astype("int64")),
+            **{k: pa.array(planes[f, d][s_idx, m_idx].astype("float64"))
+               for f, k in enumerate(("open", "high", "low", "close", "volume"))}}))
+    rows = sum(t.num_rows for t in tabs)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dp = ingest.to_device_panel(tabs, dev)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    out.update({"ingest_host_path_rows_per_s": round(rows / dt), "ingest_host_path_stock_days_per_s":
+                round(hd * S / dt), "ingest_host_path_sample": f"{hd} day tables x {S} stocks, {rows} rows"})
+    del dp
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,6 +171,8 @@ def main():
     ap.add_argument("--cpu-stocks", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--ingest-days", type=int, default=20)
+    ap.add_argument("--ingest-host-days", type=int, default=4)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -166,6 +250,8 @@ def main():
         ms, _ = timed(lambda: engine.cross_section(val[:4], state[:4], "rank", comm=comm))
         extras["stage3_rank_4factors_ms"] = round(ms, 3)
         del val, state
+        if rank == 0:
+            extras.update(ingest_extras(panel, args.ingest_days, args.ingest_host_days))
 
     if rank == 0:
         res = {

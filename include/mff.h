@@ -55,6 +55,36 @@ int mff_num_factors(void);
 /* name of factor `id` (reference column name, e.g. "mmt_pm"); NULL if out of range */
 const char* mff_factor_name(int id);
 
+/* mff_ingest_rows volume column types */
+#define MFF_VOLUME_F64 0
+#define MFF_VOLUME_I64 1
+#define MFF_VOLUME_F32 2
+#define MFF_VOLUME_I32 3
+
+/* mff_ingest_rows error counters (uint32 errors[5]) */
+#define MFF_INGEST_ERR_INDEX 0  /* stock / day index outside [0,S) x [0,D): row skipped */
+#define MFF_INGEST_ERR_TIME 1   /* time off the 240-bar grid: row skipped */
+#define MFF_INGEST_ERR_DUP 2    /* (stock, day, minute) already present */
+#define MFF_INGEST_ERR_PRICE 3  /* open/high/low/close not finite > 0 */
+#define MFF_INGEST_ERR_VOLUME 4 /* volume not integral in [0, 2^24] */
+
+/*
+ * Ingest: long day-frame rows -> dense panel.
+ * Replaces: the per-file `pl.read_parquet` hand-off (MinuteFrequentFactorCICC.py:22)
+ * and the time -> minute map minute_in_trade (CM:98-106).  Row i: stock[i] / day[i]
+ * (dense indices into the caller's sorted code / date universes, int32), time[i]
+ * (HHMMSSmmm, int64), the four prices (float64) and volume (volume_kind).  Writes the
+ * five fp32 planes `bars` [5][D][S][240] at (day, stock, minute) and ORs the presence
+ * bit into `valid` [D][S][8]; `valid` and `errors` (uint32[5], MFF_INGEST_ERR_*) must be
+ * zeroed by the caller before the first call into a panel, so a panel may be filled by
+ * several calls (day-file batches).  Contract violations are counted, never trapped;
+ * the caller reads `errors` and rejects the panel if any is non-zero.
+ */
+int mff_ingest_rows(const int32_t* stock, const int32_t* day, const int64_t* time,
+                    const double* open, const double* high, const double* low,
+                    const double* close, const void* volume, int volume_kind, int64_t nrows,
+                    int S, int D, float* bars, uint32_t* valid, uint32_t* errors, void* stream);
+
 /*
  * Stage 1: the per-(stock, day) factor kernels.
  * Replaces: every `cal_<name>(df)` of MinuteFrequentFactorCalculateMethodsCICC.py

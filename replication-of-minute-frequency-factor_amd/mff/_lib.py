@@ -26,6 +26,7 @@ SIGNATURES = {
     "mff_last_error": (c_char_p, []),
     "mff_num_factors": (c_int, []),
     "mff_factor_name": (c_char_p, [c_int]),
+    "mff_ingest_rows": (c_int, [P, P, P, P, P, P, P, P, c_int, ctypes.c_int64, c_int, c_int, P, P, P, P]),
     "mff_stage1_workspace_bytes": (c_size_t, [c_int, c_int]),
     "mff_pdf_levels_bytes": (c_size_t, [c_int, c_int]),
     "mff_stage1": (c_int, [P, P, P, P, P, P, c_int, c_int, IP, c_int, P, P, P, P, P, P]),

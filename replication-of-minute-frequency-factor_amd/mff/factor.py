@@ -352,7 +352,7 @@ class MinFreqFactor(Factor):
                     print(f"处理文件 {f} 时出错: {str(e)}")
             if not tables:
                 continue
-            res = compute_long(pa.concat_tables(tables, promote_options="default"), [name], device)
+            res = compute_long(tables, [name], device)
             out.append(res[name])
         return out
 

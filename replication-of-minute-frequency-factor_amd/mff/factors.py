@@ -27,20 +27,22 @@ def _device(device=None):
 
 
 def compute_long(df, names: Sequence[str] | None = None, device=None) -> Dict:
-    """Long frame (one or more days) -> {name: long result frame} for the requested
-    factors, computed in one stage-1 pass."""
+    """Long frame(s) (one or more days; a list of day-file tables is ingested batch by
+    batch without concatenation) -> {name: long result frame} for the requested factors,
+    computed in one stage-1 pass."""
     import torch
 
     from . import engine
 
     names = list(catalog.NAMES if names is None else
                  [n[4:] if n.startswith("cal_") else n for n in names])
-    panel = frames.to_dense(df)
-    dp = engine.DevicePanel.from_host(panel, _device(device))
+    from . import ingest
+
+    dp = ingest.to_device_panel(df, _device(device))  # GPU long -> dense (mff_ingest_rows)
     val, state, _ = engine.compute_factors(dp, names)
     torch.cuda.synchronize(dp.device)
     v, s = val.cpu().numpy(), state.cpu().numpy()
-    return {nm: frames.to_long(v[i], s[i], panel["codes"], panel["dates"], nm,
+    return {nm: frames.to_long(v[i], s[i], dp.codes, dp.dates, nm,
                                first="date" if nm == "shape_skratio" else "code")
             for i, nm in enumerate(names)}
 

@@ -1,0 +1,226 @@
+"""Long day frames -> dense device panel on the GPU.
+
+The reference hands every ``cal_*`` a long frame read from one parquet day file
+(MinuteFrequentFactorCICC.py:22): rows (code, date, time, open, high, low, close,
+volume).  Here the host does only what needs strings or dates: it encodes ``code`` and
+``date`` to dense indices into sorted universes (pyarrow compute kernels, no Python
+loop over rows) and stages the numeric columns in pinned memory.  The device kernel
+``mff_ingest_rows`` (csrc/mff_ingest.hip) maps time -> minute (CM:98-106), casts to the
+fp32 planes, sets the presence bits and counts contract violations.
+
+Batches of day files stream through two pinned staging slots on a side stream: the
+host encodes batch k+1 while batch k is copied (H2D, async) and scattered, and the
+caller's stream waits on the ingest stream only when the panel is handed over.
+
+:func:`frames.to_dense` is the host restatement of the same conversion (and the test
+oracle for this one).
+"""
+from __future__ import annotations
+
+import datetime as _dt
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+
+FIELDS = ("open", "high", "low", "close", "volume")
+ERRORS = ("stock/day index out of range", "bars off the 240-minute grid",
+          "duplicate (code, date, time) rows", "prices must be finite and > 0",
+          "volume must be integral and within [0, 2**24] (fp32-exact)")
+_VOLUME_KIND = {np.dtype(np.float64): 0, np.dtype(np.int64): 1, np.dtype(np.float32): 2,
+                np.dtype(np.int32): 3}
+_EPOCH = _dt.date(1970, 1, 1)
+
+
+def _table(df):
+    """pandas / pyarrow / dict / polars-like (``to_arrow``) -> pyarrow Table."""
+    import pyarrow as pa
+
+    if isinstance(df, pa.Table):
+        return df
+    if hasattr(df, "to_arrow") and not hasattr(df, "to_pandas_dtype"):
+        return df.to_arrow()
+    if isinstance(df, dict):
+        return pa.table({k: np.asarray(v) for k, v in df.items()})
+    return pa.Table.from_pandas(df, preserve_index=False)
+
+
+def _date32(col):
+    """date column (date32 / timestamp / date objects / ISO strings) -> int32 day numbers."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    if isinstance(col, pa.ChunkedArray):
+        col = col.combine_chunks()
+    t = col.type
+    if pa.types.is_date32(t):
+        pass
+    elif pa.types.is_date64(t) or pa.types.is_timestamp(t):
+        col = pc.cast(col, pa.date32())
+    elif pa.types.is_string(t) or pa.types.is_large_string(t):
+        col = pc.cast(pc.utf8_slice_codeunits(col, 0, 10), pa.date32())
+    else:
+        col = pa.array([_as_date(x) for x in col.to_pylist()], type=pa.date32())
+    return col.cast(pa.int32()).to_numpy(zero_copy_only=False)
+
+
+def _as_date(x):
+    from .frames import _as_date as f
+    return f(x)
+
+
+def _numeric(col, dtype):
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    if isinstance(col, pa.ChunkedArray):
+        col = col.combine_chunks()
+    if col.null_count:
+        col = pc.fill_null(col.cast(pa.float64()), float("nan"))
+    return np.ascontiguousarray(col.to_numpy(zero_copy_only=False), dtype=dtype)
+
+
+def _volume(col):
+    import pyarrow as pa
+
+    if isinstance(col, pa.ChunkedArray):
+        col = col.combine_chunks()
+    arr = _numeric(col, None) if col.null_count else col.to_numpy(zero_copy_only=False)
+    arr = np.ascontiguousarray(arr)
+    if arr.dtype not in _VOLUME_KIND:
+        arr = arr.astype(np.float64)
+    return arr, _VOLUME_KIND[arr.dtype]
+
+
+def universes(tables) -> tuple:
+    """Sorted code and date universes of a list of tables (pyarrow.compute unique)."""
+    import pyarrow.compute as pc
+
+    codes, days = set(), set()
+    for t in tables:
+        codes.update(pc.unique(t.column("code")).to_pylist())
+        days.update(np.unique(_date32(t.column("date"))).tolist())
+    return sorted(codes), sorted(days)
+
+
+def encode(t, codes: Sequence[str], day_numbers: Sequence[int]):
+    """One table -> (stock int32, day int32, time int64, 4 x price f64, volume, kind).
+    Codes / dates outside the universes get index -1 (counted by the kernel)."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    for k in ("code", "date", "time") + FIELDS:
+        if k not in t.column_names:
+            raise ValueError(f"missing column {k!r}")
+    code = t.column("code")
+    if not (pa.types.is_string(code.type) or pa.types.is_large_string(code.type)):
+        code = pc.cast(code, pa.string())
+    stock = pc.fill_null(pc.index_in(code, value_set=pa.array(list(codes), pa.string())), -1)
+    stock = np.ascontiguousarray(stock.to_numpy(zero_copy_only=False), dtype=np.int32)
+    dn = _date32(t.column("date"))
+    uday = np.asarray(day_numbers, dtype=np.int32)
+    day = np.searchsorted(uday, dn).astype(np.int32)
+    day[(day >= uday.size) | (uday[np.minimum(day, uday.size - 1)] != dn)] = -1
+    time = _numeric(t.column("time"), np.int64)
+    px = [_numeric(t.column(k), np.float64) for k in FIELDS[:4]]
+    vol, kind = _volume(t.column("volume"))
+    return stock, day, time, px, vol, kind
+
+
+class PanelIngest:
+    """Fill one dense device panel [5][D][S][240] + mask [D][S][8] from long tables.
+
+    ``push(table)`` stages one table (any number of days / stocks of the universes) and
+    launches its H2D copy and scatter asynchronously; ``finish()`` checks the error
+    counters (raising ValueError like :func:`frames.to_dense`) and returns the
+    :class:`mff.engine.DevicePanel`."""
+
+    def __init__(self, codes: Sequence[str], day_numbers: Sequence[int], device,
+                 slots: int = 2):
+        self.lib = _lib.load()
+        self.codes = list(codes)
+        self.day_numbers = [int(x) for x in day_numbers]
+        self.dev = torch.device(device)
+        S, D = len(self.codes), len(self.day_numbers)
+        if S == 0 or D == 0:
+            raise ValueError("empty code or date universe")
+        self.S, self.D = S, D
+        self.bars = torch.empty((5, D, S, 240), dtype=torch.float32, device=self.dev)
+        self.mask = torch.zeros((D, S, 8), dtype=torch.int32, device=self.dev)
+        self.err = torch.zeros(5, dtype=torch.int32, device=self.dev)
+        self.stream = torch.cuda.Stream(self.dev)
+        self.stream.wait_stream(torch.cuda.current_stream(self.dev))  # zero fills first
+        self.slots = [None] * slots  # (pinned, device, event)
+        self.k = 0
+        self.rows = 0
+
+    def _slot(self, nbytes: int):
+        i = self.k % len(self.slots)
+        self.k += 1
+        s = self.slots[i]
+        if s is not None:
+            s[2].synchronize()  # the slot's previous copy has left the pinned buffer
+            if s[0].numel() < nbytes:
+                s = None
+        if s is None:
+            cap = max(nbytes, 1 << 20)
+            with torch.cuda.stream(self.stream):
+                s = (torch.empty(cap, dtype=torch.uint8, pin_memory=True),
+                     torch.empty(cap, dtype=torch.uint8, device=self.dev), torch.cuda.Event())
+            self.slots[i] = s
+        return s
+
+    def push(self, df) -> None:
+        t = _table(df)
+        stock, day, time, px, vol, kind = encode(t, self.codes, self.day_numbers)
+        n = int(stock.size)
+        if n == 0:
+            return
+        cols = [stock, day, time] + px + [vol]
+        offs, o = [], 0
+        for c in cols:
+            offs.append(o)
+            o += (c.nbytes + 15) // 16 * 16
+        pinned, dbuf, ev = self._slot(o)
+        host = pinned.numpy()
+        for c, off in zip(cols, offs):
+            host[off:off + c.nbytes] = c.view(np.uint8).reshape(-1)
+        with torch.cuda.stream(self.stream):
+            dbuf[:o].copy_(pinned[:o], non_blocking=True)
+            ev.record(self.stream)
+            p = [dbuf.data_ptr() + off for off in offs]
+            b = self.bars
+            _lib.check(self.lib.mff_ingest_rows(
+                p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], kind, n, self.S, self.D,
+                b.data_ptr(), self.mask.data_ptr(), self.err.data_ptr(),
+                self.stream.cuda_stream), "mff_ingest_rows")
+        self.rows += n
+
+    def finish(self):
+        from .engine import DevicePanel
+
+        torch.cuda.current_stream(self.dev).wait_stream(self.stream)
+        err = self.err.cpu().numpy()  # synchronises the caller's stream
+        bad = [f"{ERRORS[i]} ({int(err[i])} rows)" for i in range(5) if err[i]]
+        if bad:
+            raise ValueError("; ".join(bad))
+        dates = [_EPOCH + _dt.timedelta(days=x) for x in self.day_numbers]
+        return DevicePanel(self.bars, self.mask, self.codes, dates)
+
+
+def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None):
+    """One or more long tables -> DevicePanel (universes: the tables' sorted codes and
+    dates, or the given code universe)."""
+    tabs = [_table(t) for t in (tables if isinstance(tables, (list, tuple)) else [tables])]
+    ucodes, udays = universes(tabs)
+    if codes is not None:
+        ucodes = list(codes)
+    ing = PanelIngest(ucodes, udays, device)
+    for t in tabs:
+        ing.push(t)
+    return ing.finish()
+
+
+__all__: List[str] = ["PanelIngest", "to_device_panel", "universes", "encode"]
