@@ -166,6 +166,30 @@ int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_
                 const double* val_all, const uint8_t* state_all, int R, int S_all,
                 double* out_val, uint8_t* out_state, void* workspace, void* stream);
 
+/*
+ * Factor IC / rank-IC test.  Replaces Factor.ic_test
+ * (Factor.py:127-229).  Inputs are dense [D][S] (val, state) like stage 1's output rows.
+ * mff_future_return: Factor.py:142-162 — per stock over its present days,
+ *   fut = exp(sum of log(1 + pct) over the next N present days) - 1, NULL unless N such
+ *   days exist with no null among them (rolling_sum min_samples=N, then shift(-N)).
+ *   Requires 1 <= N <= 64.
+ * mff_ic_pairs: the pair set of pl.corr (Factor.py:165-183): x VALUE and not NaN (the
+ *   is_nan filter), y VALUE; writes [2][D][S] rows (x, y) with state VALUE on pairs, else
+ *   ABSENT.  Feed them to mff_ic_moments (IC) or first to mff_xs_rank (rank IC).
+ * mff_ic_moments: per day, the local pair moments partial [D][6] = (n, mean_x, mean_y,
+ *   Cxx, Cyy, Cxy) over pairs whose two states are VALUE.
+ * mff_ic_finalize: combine the R stock shards' partials [R][D][6] (all-gathered) and
+ *   write ic [D] = Cxy / sqrt(Cxx Cyy), NaN when n < 2 or the denominator is 0.
+ */
+int mff_future_return(const double* pct, const uint8_t* state, int D, int S, int N,
+                      double* out_val, uint8_t* out_state, void* stream);
+int mff_ic_pairs(const double* x_val, const uint8_t* x_state, const double* y_val,
+                 const uint8_t* y_state, int D, int S, double* pair_val, uint8_t* pair_state,
+                 void* stream);
+int mff_ic_moments(const double* pair_val, const uint8_t* pair_state, int D, int S,
+                   double* partial, void* stream);
+int mff_ic_finalize(const double* partial_all, int R, int D, double* ic, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

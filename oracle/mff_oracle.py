@@ -1015,3 +1015,57 @@ def oracle_stage3(val: np.ndarray, state: np.ndarray, kind: str):
         else:
             raise ValueError(kind)
     return out_v, out_s
+
+
+# ----------------------------------------------------------------------------
+# IC / rank-IC test (Factor.ic_test, FA:127-229)
+# ----------------------------------------------------------------------------
+
+def oracle_future_return(pct: np.ndarray, state: np.ndarray, N: int):
+    """FA:142-162 on dense [D][S] rows (present stock-days only, date order per code):
+    ``(log(pct + 1).rolling_sum(N, min_samples=N).over('code').exp() - 1)
+    .shift(-N).over('code')``.  rolling value at row j needs rows j-N+1..j all non-null
+    (S13); shift(-N) moves row j+N's value to row j, null past the end (S5)."""
+    D, S = pct.shape
+    out_v = np.zeros((D, S))
+    out_s = state.copy()
+    for s in range(S):
+        rows = [d for d in range(D) if state[d, s] != ABSENT]
+        lg = [None if state[d, s] != VALUE else math.log(pct[d, s] + 1.0) if pct[d, s] + 1.0 > 0
+              else (float("-inf") if pct[d, s] + 1.0 == 0 else float("nan")) for d in rows]
+        roll = []
+        for j in range(len(rows)):
+            win = lg[j - N + 1: j + 1] if j >= N - 1 else None
+            roll.append(None if win is None or any(x is None for x in win)
+                        else math.exp(sum(win)) - 1.0 if not any(math.isnan(x) for x in win)
+                        else float("nan"))
+        for j, d in enumerate(rows):
+            r = roll[j + N] if j + N < len(rows) else None
+            out_s[d, s] = NULLV if r is None else VALUE
+            out_v[d, s] = 0.0 if r is None else r
+    return out_v, out_s
+
+
+def oracle_ic(xv: np.ndarray, xs: np.ndarray, fv: np.ndarray, fs: np.ndarray):
+    """FA:163-186 per date: exposure rows filtered by ``~is_nan()`` (nulls drop too),
+    left-aligned with future_return, ``pl.corr`` Pearson (S3) and Spearman (average ranks
+    of the pairs, S6).  Returns (IC [D], rank_IC [D]); NaN marks a dropped date."""
+    D, S = xv.shape
+    ic = np.full(D, np.nan)
+    ric = np.full(D, np.nan)
+    for d in range(D):
+        ok = (xs[d] == VALUE) & ~np.isnan(xv[d]) & (fs[d] == VALUE)
+        x, y = xv[d, ok], fv[d, ok]
+        ic[d] = pl_corr(list(x), list(y))
+        if not math.isnan(ic[d]):
+            ric[d] = pl_corr(list(avg_rank(x)), list(avg_rank(y)))
+    return ic, ric
+
+
+def oracle_ic_summary(ic: np.ndarray, ric: np.ndarray):
+    """FA:184-190: keep dates with IC non-null/non-NaN; IC, rank_IC means, ICIR, rank_ICIR
+    = mean / std (ddof=1)."""
+    keep = ~np.isnan(ic)
+    a, b = ic[keep], ric[keep]
+    return {"IC": float(a.mean()), "rank_IC": float(b.mean()),
+            "ICIR": float(a.mean() / a.std(ddof=1)), "rank_ICIR": float(b.mean() / b.std(ddof=1))}

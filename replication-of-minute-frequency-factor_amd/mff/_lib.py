@@ -40,6 +40,10 @@ SIGNATURES = {
     "mff_xs_zscore": (c_int, [P, P, c_int, c_int, c_int, P, c_int, P, P, P]),
     "mff_xs_rank_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "mff_xs_rank": (c_int, [P, P, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P, P]),
+    "mff_future_return": (c_int, [P, P, c_int, c_int, c_int, P, P, P]),
+    "mff_ic_pairs": (c_int, [P, P, P, P, c_int, c_int, P, P, P]),
+    "mff_ic_moments": (c_int, [P, P, c_int, c_int, P, P]),
+    "mff_ic_finalize": (c_int, [P, c_int, c_int, P, P]),
 }
 
 _lock = threading.Lock()

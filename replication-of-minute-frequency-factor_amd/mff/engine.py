@@ -212,3 +212,42 @@ def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None):
     else:
         raise ValueError(kind)
     return ov, os_
+
+
+def future_return(pct_val: torch.Tensor, pct_state: torch.Tensor, N: int):
+    """Factor.py:142-162 on dense [D][S] daily pct_change rows: compounded return of the
+    next N present days per stock (mff_future_return).  Returns (val, state) [D][S]."""
+    lib = _lib.load()
+    D, S = pct_val.shape
+    ov = torch.empty_like(pct_val)
+    os_ = torch.empty_like(pct_state)
+    _lib.check(lib.mff_future_return(_lib.ptr(pct_val), _lib.ptr(pct_state), D, S, N, _lib.ptr(ov),
+                                     _lib.ptr(os_), _stream(pct_val.device)), "mff_future_return")
+    return ov, os_
+
+
+def ic_series(x_val: torch.Tensor, x_state: torch.Tensor, y_val: torch.Tensor,
+              y_state: torch.Tensor, comm=None):
+    """Factor.py:163-186: per-date Pearson IC and Spearman rank IC of exposure x [D][S_loc]
+    against future return y [D][S_loc] over the stocks of all ranks.  Returns (ic, rank_ic)
+    float64 [D] on the device; NaN = the reference drops that date."""
+    lib = _lib.load()
+    D, S = x_val.shape
+    dev = x_val.device
+    st = _stream(dev)
+    R = 1 if comm is None else comm.world_size
+    pv = torch.empty((2, D, S), dtype=torch.float64, device=dev)
+    ps = torch.empty((2, D, S), dtype=torch.uint8, device=dev)
+    _lib.check(lib.mff_ic_pairs(_lib.ptr(x_val), _lib.ptr(x_state), _lib.ptr(y_val), _lib.ptr(y_state),
+                                D, S, _lib.ptr(pv), _lib.ptr(ps), st), "mff_ic_pairs")
+    rv, rs = cross_section(pv, ps, "rank", comm=comm)
+    out = []
+    for v, s in ((pv, ps), (rv, rs)):
+        part = torch.empty((D, 6), dtype=torch.float64, device=dev)
+        _lib.check(lib.mff_ic_moments(_lib.ptr(v), _lib.ptr(s), D, S, _lib.ptr(part), st),
+                   "mff_ic_moments")
+        part_all = part if comm is None else comm.all_gather(part)
+        ic = torch.empty(D, dtype=torch.float64, device=dev)
+        _lib.check(lib.mff_ic_finalize(_lib.ptr(part_all), R, D, _lib.ptr(ic), st), "mff_ic_finalize")
+        out.append(ic)
+    return out[0], out[1]

@@ -136,35 +136,32 @@ class Factor:
                 plt.show()
         return cov if return_df else None
 
-    @staticmethod
-    def _future_return(pv, future_days: int):
-        """FA:142-162: exp(rolling_sum(log(1+pct), N, min_samples=N)) - 1, shifted -N,
-        per code in date order."""
-        pv = pv.sort_values(["code", "date"]).reset_index(drop=True)
-        lg = np.log(pv["pct_change"].astype(float) + 1.0)
-        roll = lg.groupby(pv["code"]).transform(
-            lambda s: s.rolling(future_days, min_periods=future_days).sum())
-        rc = np.exp(roll) - 1.0
-        fut = rc.groupby(pv["code"]).shift(-future_days)
-        return pv[["code", "date"]].assign(future_return=fut.to_numpy())
-
     def ic_test(self, future_days: int = 5, plot_out: bool = True, plot_variable: str = "IC",
-                return_df: bool = False, pv_data=None):
-        """Factor.py:127-229: per-date Pearson (IC) and Spearman (rank_IC) of the exposure
-        with the future N-day compounded return; IC/ICIR/rank_IC/rank_ICIR."""
+                return_df: bool = False, pv_data=None, device=None):
+        """Factor.py:127-229 on the GPU: future N-day compounded return per code
+        (mff_future_return, FA:142-162), per-date Pearson IC and Spearman rank IC of the
+        non-null, non-NaN exposure against it (mff_ic_pairs / mff_xs_rank / mff_ic_moments,
+        FA:163-183), dates with a NaN IC dropped (FA:184-186); IC, rank_IC, ICIR, rank_ICIR."""
+        import torch
+
+        from . import engine
+        from .factors import _device
+
         pd = _pd()
         pv = pv_data if pv_data is not None else self._read_daily_pv_data(["code", "date", "pct_change"])
-        fut = self._future_return(pv, future_days)
-        df = self._valid_exposure().merge(fut, on=["code", "date"], how="left")
-        rows = []
-        for date, g in df.groupby("date", sort=True):
-            g = g.dropna(subset=[self.factor_name, "future_return"])
-            x, y = g[self.factor_name].to_numpy(), g["future_return"].to_numpy()
-            ic = _pearson(x, y)
-            ric = _pearson(_avg_rank(x), _avg_rank(y)) if x.size else np.nan
-            rows.append((date, ic, ric))
-        ic_df = pd.DataFrame(rows, columns=["date", "IC", "rank_IC"])
-        ic_df = ic_df[~ic_df["IC"].isna()].sort_values("date").reset_index(drop=True)
+        ex = self.factor_exposure
+        codes = sorted(set(map(str, ex["code"])) | set(map(str, pv["code"])))
+        dates = sorted(set(frames._as_date(x) for x in ex["date"]) | set(frames._as_date(x) for x in pv["date"]))
+        dev = _device(device)
+        xv, xs, _, _ = frames.from_long(ex, self.factor_name, codes=codes, dates=dates)
+        pv_v, pv_s, _, _ = frames.from_long(pv, "pct_change", codes=codes, dates=dates)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        fv, fs = engine.future_return(t(pv_v), t(pv_s), future_days)
+        ic, ric = engine.ic_series(t(xv), t(xs), fv, fs)
+        ic, ric = ic.cpu().numpy(), ric.cpu().numpy()
+        keep = ~np.isnan(ic)
+        ic_df = pd.DataFrame({"date": np.asarray(dates, dtype=object)[keep], "IC": ic[keep],
+                              "rank_IC": ric[keep]}).reset_index(drop=True)
         self.IC = float(ic_df["IC"].mean())
         self.rank_IC = float(ic_df["rank_IC"].mean())
         self.ICIR = self.IC / float(ic_df["IC"].std())
@@ -233,28 +230,6 @@ class Factor:
                 plt.tight_layout()
                 plt.show()
         return group_df if return_df else None
-
-
-def _avg_rank(x):
-    order = np.argsort(x, kind="stable")
-    sx = x[order]
-    r = np.empty(x.size)
-    i = 0
-    while i < x.size:
-        j = i
-        while j + 1 < x.size and sx[j + 1] == sx[i]:
-            j += 1
-        r[order[i:j + 1]] = (i + j + 2) / 2.0
-        i = j + 1
-    return r
-
-
-def _pearson(x, y):
-    if x.size < 2:
-        return np.nan
-    dx, dy = x - x.mean(), y - y.mean()
-    den = np.sqrt((dx * dx).sum() * (dy * dy).sum())
-    return float((dx * dy).sum() / den) if den != 0 else np.nan
 
 
 class MinFreqFactor(Factor):

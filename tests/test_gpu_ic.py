@@ -1,0 +1,137 @@
+"""IC / rank-IC test on the GPU (Factor.ic_test, Factor.py:127-229)
+against the oracle restatement (oracle_future_return / oracle_ic / oracle_ic_summary).
+CPU-only tests pin the oracle itself against direct numpy/pandas computations."""
+import datetime as dt
+
+import numpy as np
+import pandas as pd
+import pytest
+
+import mff_oracle as O
+from parity import compare
+
+torch = pytest.importorskip("torch")
+
+
+def _daily(rng, D=40, S=50):
+    """Dense daily pct_change / exposure rows with suspensions (ABSENT runs), nulls, NaN
+    exposures, a constant-exposure date, a date with one pair and a NaN-return stock-day."""
+    pct = rng.normal(0, 0.02, (D, S))
+    ps = np.full((D, S), O.VALUE, np.uint8)
+    ps[5:9, 3] = O.ABSENT
+    ps[10:30, 7] = O.ABSENT
+    ps[rng.random((D, S)) < 0.01] = O.NULLV
+    pct[12, 4] = np.nan                      # NaN pct -> NaN future returns around it
+    x = rng.normal(size=(D, S))
+    xs = ps.copy()
+    x[rng.random((D, S)) < 0.02] = np.nan    # dropped by the is_nan filter
+    xs[rng.random((D, S)) < 0.02] = O.NULLV
+    x[2] = 1.25                              # constant exposure: IC NaN -> date dropped
+    xs[3] = O.ABSENT
+    xs[3, :1] = O.VALUE                      # one pair: IC NaN
+    return pct, ps, x, xs
+
+
+def test_oracle_future_return_against_pandas():
+    rng = np.random.default_rng(3)
+    D, S, N = 25, 6, 5
+    pct = rng.normal(0, 0.02, (D, S))
+    st = np.full((D, S), O.VALUE, np.uint8)
+    st[4:7, 1] = O.ABSENT
+    fv, fs = O.oracle_future_return(pct, st, N)
+    for s in range(S):
+        rows = np.nonzero(st[:, s] != O.ABSENT)[0]
+        ser = pd.Series(np.log1p(pct[rows, s]))
+        fut = (np.exp(ser.rolling(N, min_periods=N).sum()) - 1).shift(-N).to_numpy()
+        got = np.where(fs[rows, s] == O.VALUE, fv[rows, s], np.nan)
+        np.testing.assert_allclose(got, fut, rtol=1e-12, equal_nan=True)
+
+
+def test_oracle_ic_against_numpy():
+    rng = np.random.default_rng(4)
+    pct, ps, x, xs = _daily(rng)
+    fv, fs = O.oracle_future_return(pct, ps, 5)
+    ic, ric = O.oracle_ic(x, xs, fv, fs)
+    assert np.isnan(ic[2]) and np.isnan(ic[3]) and np.isnan(ic[-5:]).all()
+    d = 20
+    ok = (xs[d] == O.VALUE) & ~np.isnan(x[d]) & (fs[d] == O.VALUE)
+    if np.isnan(fv[d, ok]).any():
+        assert np.isnan(ic[d])
+    else:
+        assert ic[d] == pytest.approx(np.corrcoef(x[d, ok], fv[d, ok])[0, 1], rel=1e-12)
+        rx = pd.Series(x[d, ok]).rank().to_numpy()
+        ry = pd.Series(fv[d, ok]).rank().to_numpy()
+        assert ric[d] == pytest.approx(np.corrcoef(rx, ry)[0, 1], rel=1e-12)
+
+
+# --------------------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [1, 5, 20])
+def test_future_return_matches_oracle(dev, N):
+    from mff import engine
+    pct, ps, _, _ = _daily(np.random.default_rng(5))
+    gv, gs = engine.future_return(_t(pct, dev), _t(ps, dev), N)
+    ov, os_ = O.oracle_future_return(pct, ps, N)
+    assert not compare(gv.cpu().numpy(), gs.cpu().numpy(), ov, os_, "future_return", atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 2, 3])
+def test_ic_series_matches_oracle(dev, R):
+    """R stock shards (threads, mff.dist.ThreadComm): partial moments combined across
+    ranks, ranks through the stage-3 all-gather."""
+    from mff import dist, engine
+    pct, ps, x, xs = _daily(np.random.default_rng(6), D=30, S=61)
+    fv, fs = O.oracle_future_return(pct, ps, 5)
+    oic, oric = O.oracle_ic(x, xs, fv, fs)
+    S = x.shape[1]
+
+    def rank_fn(comm):
+        s0, s1 = dist.shard_bounds(S, R, comm.rank) if comm is not None else (0, S)
+        sl = slice(s0, s1)
+        pv, pst = engine.future_return(_t(pct[:, sl], dev), _t(ps[:, sl], dev), 5)
+        ic, ric = engine.ic_series(_t(x[:, sl], dev), _t(xs[:, sl], dev), pv, pst, comm=comm)
+        torch.cuda.synchronize()
+        return ic.cpu().numpy(), ric.cpu().numpy()
+
+    outs = [rank_fn(None)] if R == 1 else dist.run_threads(R, rank_fn)
+    for ic, ric in outs:
+        assert np.array_equal(np.isnan(ic), np.isnan(oic))
+        k = ~np.isnan(oic)
+        np.testing.assert_allclose(ic[k], oic[k], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(ric[k], oric[k], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_factor_ic_test_end_to_end(dev):
+    """Factor.ic_test on long frames (exposure + daily pv) -> per-date IC / rank_IC frame
+    and the four summary numbers, against the oracle."""
+    from mff import frames
+    from mff.factor import Factor
+    pct, ps, x, xs = _daily(np.random.default_rng(7), D=30, S=40)
+    codes = [f"{i:06d}.SZ" for i in range(x.shape[1])]
+    dates = [dt.date(2024, 1, 1) + dt.timedelta(days=i) for i in range(x.shape[0])]
+    ex = frames.to_long(x, xs, codes, dates, "f")
+    pv = frames.to_long(pct, ps, codes, dates, "pct_change")
+    f = Factor("f", ex)
+    got = f.ic_test(future_days=5, plot_out=False, return_df=True, pv_data=pv, device=dev)
+    fv, fs = O.oracle_future_return(pct, ps, 5)
+    oic, oric = O.oracle_ic(x, xs, fv, fs)
+    k = ~np.isnan(oic)
+    assert list(got["date"]) == [d for d, keep in zip(dates, k) if keep]
+    np.testing.assert_allclose(got["IC"].to_numpy(), oic[k], rtol=1e-9)
+    np.testing.assert_allclose(got["rank_IC"].to_numpy(), oric[k], rtol=1e-9)
+    summ = O.oracle_ic_summary(oic, oric)
+    for key in ("IC", "rank_IC", "ICIR", "rank_ICIR"):
+        assert getattr(f, key) == pytest.approx(summ[key], rel=1e-9)
