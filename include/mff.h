@@ -190,6 +190,36 @@ int mff_ic_moments(const double* pair_val, const uint8_t* pair_state, int D, int
                    double* partial, void* stream);
 int mff_ic_finalize(const double* partial_all, int R, int D, double* ic, void* stream);
 
+/*
+ * Factor group back-test.  Replaces Factor.group_test
+ * (Factor.py:231-350).  Exposure / pct_change / weight rows are dense [D][S] (val, state).
+ * mff_bt_qcut: per date, G quantile groups of the non-null non-NaN exposures of all
+ *   ranks (val_all/state_all [R][D][S_all], each rank's columns padded with ABSENT):
+ *   pandas-qcut edges (linear quantiles, duplicate edges dropped) -> group int8 [D][S_loc]
+ *   in 0..G-1, -1 = null.  workspace: mff_bt_qcut_workspace_bytes bytes.  G <= 63.
+ * mff_bt_periods: per stock over the dates (period_of [D] int32, non-decreasing, every
+ *   period 0..P-1 present): per period the return prod(1 + pct) - 1 over the exposure
+ *   rows with non-null pct, and the group / weight of the previous period the stock held
+ *   (shift(1).over('code')) -> p_ret f64, p_group int8 (-1 = null), p_weight f64 +
+ *   p_weight_state u8, all [P][S].  weight / weight_state NULL = equal weights.
+ * mff_bt_reduce: per (period, group) over local stocks -> partial [P][G][4] = (count,
+ *   sum ret, sum w, sum w*ret).
+ * mff_bt_finalize: sum the R ranks' partials [R][P][G][4] -> ret [P][G] = mean ret, or
+ *   (weighted) sum w*ret / sum w (0 when sum w == 0); present [P][G] u8 = count > 0.
+ */
+size_t mff_bt_qcut_workspace_bytes(int D, int S_all, int R);
+int mff_bt_qcut(const double* val, const uint8_t* state, int D, int S_loc, const double* val_all,
+                const uint8_t* state_all, int R, int S_all, int G, int8_t* group, void* workspace,
+                void* stream);
+int mff_bt_periods(const uint8_t* x_state, const int8_t* group, const double* pct,
+                   const uint8_t* pct_state, const double* weight, const uint8_t* weight_state,
+                   const int32_t* period_of, int D, int S, int P, double* p_ret, int8_t* p_group,
+                   double* p_weight, uint8_t* p_weight_state, void* stream);
+int mff_bt_reduce(const double* p_ret, const int8_t* p_group, const double* p_weight,
+                  const uint8_t* p_weight_state, int P, int S, int G, double* partial, void* stream);
+int mff_bt_finalize(const double* partial_all, int R, int P, int G, int weighted, double* ret,
+                    uint8_t* present, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1069,3 +1069,63 @@ def oracle_ic_summary(ic: np.ndarray, ric: np.ndarray):
     a, b = ic[keep], ric[keep]
     return {"IC": float(a.mean()), "rank_IC": float(b.mean()),
             "ICIR": float(a.mean() / a.std(ddof=1)), "rank_ICIR": float(b.mean() / b.std(ddof=1))}
+
+
+# ----------------------------------------------------------------------------
+# Group back-test (Factor.group_test, FA:231-350)
+# ----------------------------------------------------------------------------
+
+def oracle_qcut(x: np.ndarray, ok: np.ndarray, G: int) -> np.ndarray:
+    """FA:286-294 per date, with pandas qcut as the cut (polars' qcut is not importable;
+    the build's declared semantics): duplicate edges raise, then drop.  -> 0..G-1, -1."""
+    import pandas as pd
+    s = pd.Series(np.where(ok, x, np.nan))
+    try:
+        b = pd.qcut(s, G, labels=False, duplicates="raise")
+    except ValueError:
+        b = pd.qcut(s, G, labels=False, duplicates="drop")
+    return np.where(b.isna(), -1, b.fillna(-1)).astype(np.int64)
+
+
+def oracle_group_test(xv, xs, pct, ps, period_of, P: int, G: int, wv=None, ws=None):
+    """FA:286-324 on dense [D][S] rows: qcut per date; per (code, period) over the
+    exposure rows (align_left): prod(pct + 1) - 1 skipping null pct, last row's group and
+    weight; shift(1) per code over its held periods; drop null groups; per (period,
+    group) mean (or sum(w*pct)/sum(w), 0 if sum(w) == 0, nulls skipped).
+    Returns (ret [P][G], present [P][G])."""
+    D, S = xv.shape
+    grp = np.full((D, S), -1, np.int64)
+    for d in range(D):
+        ok = (xs[d] == VALUE) & ~np.isnan(xv[d])
+        grp[d] = oracle_qcut(xv[d], ok, G)
+    acc = [[[] for _ in range(G)] for _ in range(P)]
+    for s in range(S):
+        prev = None  # (group, w, w_valid) of the previous held period
+        for p in range(P):
+            days = [d for d in range(D) if period_of[d] == p and xs[d, s] != ABSENT]
+            if not days:
+                continue
+            r = 1.0
+            for d in days:
+                if ps[d, s] == VALUE:
+                    r *= pct[d, s] + 1.0
+            last = days[-1]
+            cur = (grp[last, s], None if wv is None else wv[last, s],
+                   wv is not None and ws[last, s] == VALUE)
+            if prev is not None and prev[0] >= 0:
+                acc[p][prev[0]].append((r - 1.0, prev[1], prev[2]))
+            prev = cur
+    ret = np.zeros((P, G))
+    present = np.zeros((P, G), np.uint8)
+    for p in range(P):
+        for g in range(G):
+            rows = acc[p][g]
+            if not rows:
+                continue
+            present[p, g] = 1
+            if wv is None:
+                ret[p, g] = sum(r for r, _, _ in rows) / len(rows)
+            else:
+                sw = sum(w for _, w, ok in rows if ok)
+                ret[p, g] = sum(w * r for r, w, ok in rows if ok) / sw if sw != 0 else 0.0
+    return ret, present

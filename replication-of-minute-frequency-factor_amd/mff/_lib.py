@@ -44,6 +44,11 @@ SIGNATURES = {
     "mff_ic_pairs": (c_int, [P, P, P, P, c_int, c_int, P, P, P]),
     "mff_ic_moments": (c_int, [P, P, c_int, c_int, P, P]),
     "mff_ic_finalize": (c_int, [P, c_int, c_int, P, P]),
+    "mff_bt_qcut_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "mff_bt_qcut": (c_int, [P, P, c_int, c_int, P, P, c_int, c_int, c_int, P, P, P]),
+    "mff_bt_periods": (c_int, [P, P, P, P, P, P, P, c_int, c_int, c_int, P, P, P, P, P]),
+    "mff_bt_reduce": (c_int, [P, P, P, P, c_int, c_int, c_int, P, P]),
+    "mff_bt_finalize": (c_int, [P, c_int, c_int, c_int, c_int, P, P, P]),
 }
 
 _lock = threading.Lock()

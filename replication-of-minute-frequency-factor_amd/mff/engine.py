@@ -251,3 +251,44 @@ def ic_series(x_val: torch.Tensor, x_state: torch.Tensor, y_val: torch.Tensor,
         _lib.check(lib.mff_ic_finalize(_lib.ptr(part_all), R, D, _lib.ptr(ic), st), "mff_ic_finalize")
         out.append(ic)
     return out[0], out[1]
+
+
+def group_returns(x_val: torch.Tensor, x_state: torch.Tensor, pct_val: torch.Tensor,
+                  pct_state: torch.Tensor, period_of: torch.Tensor, P: int, group_num: int = 5,
+                  w_val: Optional[torch.Tensor] = None, w_state: Optional[torch.Tensor] = None,
+                  comm=None):
+    """Factor.py:231-350 on dense [D][S_loc] rows: per-date quantile groups of the
+    exposure (mff_bt_qcut), per-period compounding with the previous period's group and
+    weight (mff_bt_periods), per (period, group) mean / weighted mean over all ranks
+    (mff_bt_reduce + all-gather + mff_bt_finalize).  period_of: int32 [D] on the device.
+    Returns (ret float64 [P][G], present uint8 [P][G])."""
+    lib = _lib.load()
+    D, S = x_val.shape
+    dev = x_val.device
+    st = _stream(dev)
+    R = 1 if comm is None else comm.world_size
+    G = int(group_num)
+    S_all = S if comm is None else _agreed_max(comm, S, dev)
+    v_all = x_val if comm is None else comm.all_gather(_pad_last(x_val, S_all, 0.0))
+    s_all = x_state if comm is None else comm.all_gather(_pad_last(x_state, S_all, ABSENT))
+    ws = torch.empty(lib.mff_bt_qcut_workspace_bytes(D, S_all, R), dtype=torch.uint8, device=dev)
+    group = torch.empty((D, S), dtype=torch.int8, device=dev)
+    _lib.check(lib.mff_bt_qcut(_lib.ptr(x_val), _lib.ptr(x_state), D, S, _lib.ptr(v_all), _lib.ptr(s_all),
+                               R, S_all, G, _lib.ptr(group), _lib.ptr(ws), st), "mff_bt_qcut")
+    p_ret = torch.empty((P, S), dtype=torch.float64, device=dev)
+    p_group = torch.empty((P, S), dtype=torch.int8, device=dev)
+    p_w = torch.empty((P, S), dtype=torch.float64, device=dev)
+    p_ws = torch.empty((P, S), dtype=torch.uint8, device=dev)
+    _lib.check(lib.mff_bt_periods(_lib.ptr(x_state), _lib.ptr(group), _lib.ptr(pct_val), _lib.ptr(pct_state),
+                                  _lib.ptr(w_val), _lib.ptr(w_state), _lib.ptr(period_of), D, S, P,
+                                  _lib.ptr(p_ret), _lib.ptr(p_group), _lib.ptr(p_w), _lib.ptr(p_ws), st),
+               "mff_bt_periods")
+    part = torch.empty((P, G, 4), dtype=torch.float64, device=dev)
+    _lib.check(lib.mff_bt_reduce(_lib.ptr(p_ret), _lib.ptr(p_group), _lib.ptr(p_w), _lib.ptr(p_ws), P, S, G,
+                                 _lib.ptr(part), st), "mff_bt_reduce")
+    part_all = part if comm is None else comm.all_gather(part)
+    ret = torch.empty((P, G), dtype=torch.float64, device=dev)
+    present = torch.empty((P, G), dtype=torch.uint8, device=dev)
+    _lib.check(lib.mff_bt_finalize(_lib.ptr(part_all), R, P, G, int(w_val is not None), _lib.ptr(ret),
+                                   _lib.ptr(present), st), "mff_bt_finalize")
+    return ret, present

@@ -181,43 +181,44 @@ class Factor:
 
     def group_test(self, frequency: Literal["weekly", "monthly", "quarterly", "yearly"] = "monthly",
                    weight_param: Literal["tmc", "cmc", None] = None, group_num: int = 5,
-                   plot_out: bool = True, return_df: bool = False, pv_data=None):
-        """Factor.py:231-350: per-date qcut into `group_num` groups, per-period compounding,
-        one-period lag, equal or cap-weighted group returns."""
+                   plot_out: bool = True, return_df: bool = False, pv_data=None, device=None):
+        """Factor.py:231-350 on the GPU: per-date quantile groups (mff_bt_qcut), per
+        rebalancing period compounding with the previous period's group / weight
+        (mff_bt_periods), per (period, group) equal or tmc/cmc-weighted mean return
+        (mff_bt_reduce / mff_bt_finalize).  Rows: [date (period right edge), group,
+        pct_change] sorted by (date, group)."""
+        import torch
+
+        from . import engine
+        from .factors import _device
+
         pd = _pd()
-        freq = {"weekly": "W-SUN", "monthly": "M", "quarterly": "Q", "yearly": "Y"}[frequency]
+        if weight_param not in (None, "tmc", "cmc"):
+            raise ValueError(f"weight_param must be 'tmc', 'cmc' or None, got {weight_param!r}")
         pv = pv_data if pv_data is not None else self._read_daily_pv_data(
             ["code", "date", "pct_change", "tmc", "cmc"])
-        ex = self.factor_exposure[["code", "date", self.factor_name]].copy()
-        ex[self.factor_name], _ = _float_values(ex[self.factor_name])
-        df = ex.merge(pv, on=["code", "date"], how="left")
-        labels = [f"group_{i + 1}" for i in range(group_num)]
-
-        def qc(s):
-            try:
-                return pd.qcut(s, group_num, labels=labels, duplicates="raise").astype(object)
-            except ValueError:
-                b = pd.qcut(s, group_num, labels=False, duplicates="drop")
-                return b.map(lambda i: None if pd.isna(i) else labels[int(i)])
-        df["group"] = df.groupby("date")[self.factor_name].transform(qc)
-        df["period"] = pd.to_datetime(df["date"]).dt.to_period(freq)
-        df = df.sort_values(["code", "date"])
-        agg = df.groupby(["code", "period"]).agg(
-            pct_change=("pct_change", lambda s: float(np.prod(1.0 + s.astype(float))) - 1.0),
-            group=("group", "last"), tmc=("tmc", "last") if "tmc" in df else ("pct_change", "last"),
-            cmc=("cmc", "last") if "cmc" in df else ("pct_change", "last")).reset_index()
-        agg["date"] = (agg["period"].dt.end_time.dt.normalize() + pd.Timedelta(days=1)).dt.date
-        agg = agg.sort_values(["date", "group"])
-        for c in ("group", "tmc", "cmc"):
-            agg[c] = agg.groupby("code")[c].shift(1)
-        agg = agg[~agg["group"].isna()]
-
-        def wmean(g):
-            if weight_param is None:
-                return g["pct_change"].mean()
-            w = g[weight_param].astype(float)
-            return float((g["pct_change"] * w).sum() / w.sum()) if w.sum() != 0 else 0.0
-        group_df = agg.groupby(["date", "group"]).apply(wmean, include_groups=False).rename("pct_change").reset_index()
+        ex = self.factor_exposure
+        dates = sorted(set(frames._as_date(x) for x in ex["date"]))
+        codes = sorted(set(map(str, ex["code"])))
+        pv = pv[pv["code"].astype(str).isin(set(codes)) &
+                pv["date"].map(frames._as_date).isin(set(dates))]
+        period_of, labels = rebalance_periods(dates, frequency)
+        dev = _device(device)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        xv, xs, _, _ = frames.from_long(ex, self.factor_name, codes=codes, dates=dates)
+        pc_v, pc_s, _, _ = frames.from_long(pv, "pct_change", codes=codes, dates=dates)
+        wv = ws = None
+        if weight_param is not None:
+            w_v, w_s, _, _ = frames.from_long(pv, weight_param, codes=codes, dates=dates)
+            wv, ws = t(w_v), t(w_s)
+        ret, present = engine.group_returns(t(xv), t(xs), t(pc_v), t(pc_s),
+                                            t(period_of.astype(np.int32)), len(labels), group_num,
+                                            wv, ws)
+        ret, present = ret.cpu().numpy(), present.cpu().numpy().astype(bool)
+        p_idx, g_idx = np.nonzero(present)
+        group_df = pd.DataFrame({"date": np.asarray(labels, dtype=object)[p_idx],
+                                 "group": [f"group_{g + 1}" for g in g_idx],
+                                 "pct_change": ret[p_idx, g_idx]})
         group_df = group_df.sort_values(["date", "group"]).reset_index(drop=True)
         if plot_out:
             plt = _plt()
@@ -230,6 +231,19 @@ class Factor:
                 plt.tight_layout()
                 plt.show()
         return group_df if return_df else None
+
+
+def rebalance_periods(dates, frequency: str):
+    """group_by_dynamic(every=1w/1mo/1q/1y, label='right') windows (Factor.py:249-256,
+    295-297) of sorted dates -> (period index per date, right-edge label per period)."""
+    pd = _pd()
+    freq = {"weekly": "W-SUN", "monthly": "M", "quarterly": "Q", "yearly": "Y"}.get(frequency)
+    if freq is None:
+        raise ValueError(f"Unsupported frequency: {frequency}")
+    per = pd.to_datetime(pd.Series(list(dates))).dt.to_period(freq)
+    codes, uniq = pd.factorize(per, sort=True)
+    labels = [(u.end_time.normalize() + pd.Timedelta(days=1)).date() for u in uniq]
+    return np.asarray(codes, dtype=np.int64), labels
 
 
 class MinFreqFactor(Factor):

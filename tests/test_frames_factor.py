@@ -90,11 +90,17 @@ def test_factor_coverage_and_ic():
     assert cov["f"].iloc[0] == 39 and (cov["f"].iloc[1:] == 40).all()   # NaN excluded
 
 
-def test_factor_group_test_runs():
-    rng = np.random.default_rng(2)
-    df, pv = _exposure(rng, D=60)
-    g = Factor("f", df).group_test(frequency="monthly", plot_out=False, return_df=True, pv_data=pv)
-    assert set(g["group"]) <= {f"group_{i}" for i in range(1, 6)} and len(g) > 0
+def test_rebalance_periods_right_edge_labels():
+    from mff.factor import rebalance_periods
+    dates = [dt.date(2024, 1, 30), dt.date(2024, 1, 31), dt.date(2024, 2, 1), dt.date(2024, 3, 4)]
+    p, lab = rebalance_periods(dates, "monthly")
+    assert list(p) == [0, 0, 1, 2] and lab == [dt.date(2024, 2, 1), dt.date(2024, 3, 1), dt.date(2024, 4, 1)]
+    p, lab = rebalance_periods(dates, "weekly")  # Mon-Sun weeks, labelled by the next Monday
+    assert list(p) == [0, 0, 0, 1] and lab == [dt.date(2024, 2, 5), dt.date(2024, 3, 11)]
+    assert rebalance_periods(dates, "quarterly")[1] == [dt.date(2024, 4, 1)]
+    assert rebalance_periods(dates, "yearly")[1] == [dt.date(2025, 1, 1)]
+    with pytest.raises(ValueError):
+        rebalance_periods(dates, "daily")
 
 
 def test_to_parquet_atomic_and_read_exposure(tmp_path):

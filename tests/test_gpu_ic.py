@@ -135,3 +135,110 @@ def test_factor_ic_test_end_to_end(dev):
     summ = O.oracle_ic_summary(oic, oric)
     for key in ("IC", "rank_IC", "ICIR", "rank_ICIR"):
         assert getattr(f, key) == pytest.approx(summ[key], rel=1e-9)
+
+
+# --------------------------------------------------------------------------- group test
+def _qcut_kernel_formula(x, ok, G):
+    """The arithmetic of k_bt_qcut (csrc/mff_bt.hip) in Python, step for step."""
+    v = np.sort(x[ok])
+    n = v.size
+    edges = []
+    if n:
+        step = 1.0 / G
+        for i in range(G + 1):
+            q = 1.0 if i == G else i * step
+            q = (q * 100.0) / 100.0
+            virt = (n - 1) * q
+            prev = np.floor(virt)
+            gam = virt - prev
+            lo = int(prev)
+            hi = lo + 1
+            if virt >= n - 1:
+                lo = hi = n - 1
+            a, b = v[lo], v[hi]
+            e = b - (b - a) * (1.0 - gam) if gam >= 0.5 else a + (b - a) * gam
+            if not edges or e != edges[-1]:
+                edges.append(e)
+    out = np.full(x.size, -1)
+    k = len(edges)
+    for i in np.nonzero(ok)[0]:
+        if k < 2:
+            continue
+        ids = int(np.sum(np.asarray(edges) < x[i]))
+        if x[i] == edges[0]:
+            ids = 1
+        if 1 <= ids <= k - 1:
+            out[i] = ids - 1
+    return out
+
+
+def test_qcut_kernel_formula_matches_pandas():
+    """Pins the kernel's quantile-edge arithmetic to pandas qcut (the oracle) on tie-heavy
+    random columns of many sizes and group counts."""
+    rng = np.random.default_rng(11)
+    for trial in range(400):
+        n = int(rng.integers(1, 120))
+        G = int(rng.integers(1, 12))
+        x = np.round(rng.normal(size=n), int(rng.integers(0, 3)))
+        ok = rng.random(n) > 0.1
+        assert np.array_equal(_qcut_kernel_formula(x, ok, G), O.oracle_qcut(x, ok, G)), (trial, n, G)
+
+
+def _bt_inputs(rng, D=70, S=45):
+    from mff.factor import rebalance_periods
+    pct, ps, x, xs = _daily(rng, D=D, S=S)
+    x = np.round(x, 1)  # ties inside the quantile cut
+    w = rng.uniform(1, 5, (D, S))
+    wst = ps.copy()
+    wst[rng.random((D, S)) < 0.05] = O.NULLV
+    dates = [dt.date(2024, 1, 1) + dt.timedelta(days=i) for i in range(D)]
+    return pct, ps, x, xs, w, wst, dates
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 2])
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("frequency", ["weekly", "monthly"])
+def test_group_returns_match_oracle(dev, R, weighted, frequency):
+    from mff import dist, engine
+    from mff.factor import rebalance_periods
+    pct, ps, x, xs, w, wst, dates = _bt_inputs(np.random.default_rng(12))
+    period_of, labels = rebalance_periods(dates, frequency)
+    P, G, S = len(labels), 5, x.shape[1]
+    oret, opres = O.oracle_group_test(x, xs, pct, ps, period_of, P, G,
+                                      w if weighted else None, wst if weighted else None)
+
+    def rank_fn(comm):
+        s0, s1 = dist.shard_bounds(S, R, comm.rank) if comm is not None else (0, S)
+        sl = slice(s0, s1)
+        args = [_t(a[:, sl], dev) for a in (x, xs, pct, ps)]
+        wa = (_t(w[:, sl], dev), _t(wst[:, sl], dev)) if weighted else (None, None)
+        ret, pres = engine.group_returns(*args, _t(period_of.astype(np.int32), dev), P, G, *wa, comm=comm)
+        torch.cuda.synchronize()
+        return ret.cpu().numpy(), pres.cpu().numpy()
+
+    outs = [rank_fn(None)] if R == 1 else dist.run_threads(R, rank_fn)
+    assert opres.sum() > P  # several groups per period actually held
+    for ret, pres in outs:
+        assert np.array_equal(pres, opres)
+        np.testing.assert_allclose(ret[opres == 1], oret[opres == 1], rtol=1e-9, atol=1e-15)
+
+
+@pytest.mark.gpu
+def test_factor_group_test_end_to_end(dev):
+    from mff import frames
+    from mff.factor import Factor, rebalance_periods
+    pct, ps, x, xs, w, wst, dates = _bt_inputs(np.random.default_rng(13))
+    codes = [f"{i:06d}.SZ" for i in range(x.shape[1])]
+    ex = frames.to_long(x, xs, codes, dates, "f")
+    pv = frames.to_long(pct, ps, codes, dates, "pct_change")
+    pv["tmc"] = frames.to_long(w, wst, codes, dates, "tmc")["tmc"]
+    g = Factor("f", ex).group_test(frequency="monthly", weight_param="tmc", plot_out=False,
+                                   return_df=True, pv_data=pv, device=dev)
+    period_of, labels = rebalance_periods(dates, "monthly")
+    oret, opres = O.oracle_group_test(x, xs, pct, ps, period_of, len(labels), 5, w, wst)
+    p_idx, g_idx = np.nonzero(opres)
+    exp = pd.DataFrame({"date": [labels[p] for p in p_idx], "group": [f"group_{k + 1}" for k in g_idx],
+                        "pct_change": oret[p_idx, g_idx]}).sort_values(["date", "group"]).reset_index(drop=True)
+    assert list(g["date"]) == list(exp["date"]) and list(g["group"]) == list(exp["group"])
+    np.testing.assert_allclose(g["pct_change"].to_numpy(), exp["pct_change"].to_numpy(), rtol=1e-9)
