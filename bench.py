@@ -188,6 +188,7 @@ def main():
     from mff import catalog, dist, engine, synth
 
     comm, local = dist.init_from_env()
+    local = local % torch.cuda.device_count()  # R ranks may share a GPU (1-GPU rehearsal)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     S, D = args.stocks, args.days

@@ -45,19 +45,28 @@ class Comm:
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[*shape] on every rank -> [world, *shape] (rank order)."""
         t = t.contiguous()
-        if self.backend == "gloo":
-            parts = [torch.empty_like(t) for _ in range(self.world_size)]
-            self._dist.all_gather(parts, t, group=self.group)
-            return torch.stack(parts)
+        if self.backend == "gloo":  # host collectives (CPU tests; the 1-GPU rehearsal)
+            h = t.cpu()
+            parts = [torch.empty_like(h) for _ in range(self.world_size)]
+            self._dist.all_gather(parts, h, group=self.group)
+            return torch.stack(parts).to(t.device)
         out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         self._dist.all_gather_into_tensor(out, t, group=self.group)
         return out
 
+    def _all_reduce(self, t: torch.Tensor, op) -> None:
+        if self.backend == "gloo" and t.device.type != "cpu":
+            h = t.cpu()
+            self._dist.all_reduce(h, op=op, group=self.group)
+            t.copy_(h)
+            return
+        self._dist.all_reduce(t, op=op, group=self.group)
+
     def all_reduce_sum(self, t: torch.Tensor) -> None:
-        self._dist.all_reduce(t, op=self._dist.ReduceOp.SUM, group=self.group)
+        self._all_reduce(t, self._dist.ReduceOp.SUM)
 
     def all_reduce_max(self, t: torch.Tensor) -> None:
-        self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX, group=self.group)
+        self._all_reduce(t, self._dist.ReduceOp.MAX)
 
     def barrier(self) -> None:
         self._dist.barrier(group=self.group)
@@ -143,8 +152,9 @@ def init_from_env(backend: Optional[str] = None):
         return None, local
     import torch.distributed as dist
 
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # MFF_DIST_BACKEND=gloo: host collectives, e.g. R ranks on one GPU
+        backend = os.environ.get("MFF_DIST_BACKEND") or (
+            "nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
     if not dist.is_initialized():
