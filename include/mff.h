@@ -118,7 +118,8 @@ int mff_stage1(const float* open, const float* high, const float* low,
  *             -> q_sorted uint64 [nd][M], M = R*5*S_all <= 32767 (total-order keys)
  *   count:    this rank's keys c_last/c_b (from stage 1's pdf_levels: one key per
  *             distinct close of a stock-day, weighted by its bar count) against q_sorted
- *             -> counts uint32 [nd][M][2] (n_less, n_eq) over local keys
+ *             -> counts uint32 [nd][M] = 2 n_less + n_eq over local keys (the
+ *             average rank n_less + (n_eq + 1) / 2 is linear in it)
  *   [R > 1: the caller sums `counts` over ranks (all-reduce), see INTEGRATION.md]
  *   finalize: own queries [5][D][S_loc] -> val/state rows pdf_rows[5] (host, -1 = skip)
  *   rank_local: count + finalize in one pass, for a single rank (R = 1: no exchange)

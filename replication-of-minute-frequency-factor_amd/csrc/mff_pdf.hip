@@ -15,7 +15,8 @@
 //                rank's keys.  The keys are stage 1's flat per-day level list: one key
 //                per distinct close of a stock-day (rows with equal closes have equal
 //                keys), weighted by its bar count, so ~L << 240 keys per stock-day;
-//   [multi-GPU: counts are summed over ranks with one all-reduce]
+//   [multi-GPU: per sorted position each rank writes one word 2 n_less + n_eq (the
+//    average rank is linear in it); the words are summed over ranks by one all-reduce]
 //   3. finalize — each own query looks its position up in its slice (LDS) and writes the
 //                rank.  With one rank, 2 and 3 run as one kernel (mff_pdf_rank_local):
 //                the slice's counters never leave LDS.
@@ -227,7 +228,7 @@ struct PdfArgs {
   const uint8_t* lvl_w;
   size_t cap;
   const uint64_t* q_sorted;
-  uint32_t* counts;       // [nd][M][2] (count phase) or NULL (fused finalize)
+  uint32_t* counts;       // [nd][M] 2 n_less + n_eq (count phase) or NULL (fused finalize)
   const double* q_local;  // fused finalize: own queries [5][D][S]
   double* val;
   uint8_t* state;
@@ -342,7 +343,9 @@ __global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
   } else {
     // per sorted position: the counts of its distinct value (positions holding Q[P0-1]
     // or NaN are never looked up)
-    uint32_t* out = a.counts + ((size_t)dd * a.M + P0) * 2;
+    // one word per position, 2 n_less + n_eq: the average rank n_less + (n_eq + 1) / 2
+    // = (2 n_less + n_eq + 1) / 2 is linear in it, so the ranks' words simply add up
+    uint32_t* out = a.counts + (size_t)dd * a.M + P0;
     for (int i = threadIdx.x; i < nq; i += blockDim.x) {
       const uint64_t x = Q[P0 + i];
       uint64_t cn = 0ull;
@@ -351,8 +354,7 @@ __global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
         sl.range(x, lo, hi);
         cn = C[lower_bound_u64(L + 1, lo, hi, x)];
       }
-      out[2 * i] = (uint32_t)cn;
-      out[2 * i + 1] = (uint32_t)(cn >> 32);
+      out[i] = 2u * (uint32_t)cn + (uint32_t)(cn >> 32);
     }
   }
 }
@@ -372,14 +374,16 @@ __global__ __launch_bounds__(1024) void k_pdf_finalize(PdfArgs a) {
   uint16_t* T = reinterpret_cast<uint16_t*>(C + a.Mz);
   const PdfSlice sl = pdf_slice_setup(Q, a.M, P0, P1, L, C, T, wsum, &occ_s);
   // counts of each distinct value, from its first sorted position
-  const uint32_t* cn = a.counts + ((size_t)dd * a.M + P0) * 2;
+  const uint32_t* cn = a.counts + (size_t)dd * a.M + P0;
   for (int i = threadIdx.x; i < P1 - P0; i += blockDim.x) {
     const uint64_t x = Q[P0 + i];
     const uint64_t xp = i > 0 ? Q[P0 + i - 1] : sl.L0;
     if (x > sl.L0 && x <= sl.qmax && x != xp) {
       int lo, hi;
       sl.range(x, lo, hi);
-      C[lower_bound_u64(L + 1, lo, hi, x)] = (uint64_t)cn[2 * i] | ((uint64_t)cn[2 * i + 1] << 32);
+      // c = 2 n_less + n_eq summed over ranks -> (c >> 1, c & 1): same average rank (c + 1) / 2
+      const uint32_t c = cn[i];
+      C[lower_bound_u64(L + 1, lo, hi, x)] = (uint64_t)(c >> 1) | ((uint64_t)(c & 1u) << 32);
     }
   }
   __syncthreads();

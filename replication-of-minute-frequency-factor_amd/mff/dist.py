@@ -8,7 +8,7 @@ of collective, all through this module:
 
   all_gather  doc_pdf threshold queries [5][D][S_loc] f64 (once per panel)
               stage-3 z moments [rows][D][3] f64; stage-3 rank columns [rows][D][S_loc]
-  all_reduce  doc_pdf (n_less, n_eq) counts per sorted query [nd][M][2] i32 (sum)
+  all_reduce  doc_pdf counts per sorted query [nd][M] i32 = 2 n_less + n_eq (sum)
 
 ``Comm`` wraps torch.distributed ("nccl" = RCCL over xGMI on MI355X, "gloo" on CPU);
 ``ThreadComm`` runs R ranks as threads of one process (tests emulate an R-GPU job on

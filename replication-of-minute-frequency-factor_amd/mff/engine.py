@@ -144,7 +144,7 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
                                               _lib.int_array(rows), _lib.ptr(val), _lib.ptr(state), st),
                        "mff_pdf_rank_local")
             continue
-        counts = torch.empty((nd, M, 2), dtype=torch.int32, device=dev)
+        counts = torch.empty((nd, M), dtype=torch.int32, device=dev)  # 2 n_less + n_eq
         _lib.check(lib.mff_pdf_count(_lib.ptr(levels), S, D, d0, nd,
                                      _lib.ptr(q_sorted), M, _lib.ptr(counts), _lib.ptr(ws), st),
                    "mff_pdf_count")
