@@ -9,6 +9,8 @@ of collective, all through this module:
   all_gather  doc_pdf threshold queries [5][D][S_loc] f64 (once per panel)
               stage-3 z moments [rows][D][3] f64; stage-3 rank columns [rows][D][S_loc]
   all_reduce  doc_pdf counts per sorted query [nd][M] i32 = 2 n_less + n_eq (sum)
+  all_to_all  doc_pdf queries of each rank's day block [R][5][nd][S_all] f64 (the sort
+              of a day's queries runs on one rank, its sorted list is all-gathered)
 
 ``Comm`` wraps torch.distributed ("nccl" = RCCL over xGMI on MI355X, "gloo" on CPU);
 ``ThreadComm`` runs R ranks as threads of one process (tests emulate an R-GPU job on
@@ -52,6 +54,19 @@ class Comm:
             return torch.stack(parts).to(t.device)
         out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         self._dist.all_gather_into_tensor(out, t, group=self.group)
+        return out
+
+    def all_to_all(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *shape]: slice r goes to rank r; returns [world, *shape] with slice r
+        received from rank r."""
+        t = t.contiguous()
+        if self.backend == "gloo":
+            h = t.cpu()
+            out = torch.empty_like(h)
+            self._dist.all_to_all_single(out, h, group=self.group)
+            return out.to(t.device)
+        out = torch.empty_like(t)
+        self._dist.all_to_all_single(out, t, group=self.group)
         return out
 
     def _all_reduce(self, t: torch.Tensor, op) -> None:
@@ -104,6 +119,10 @@ class _RankComm:
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         return torch.stack(self._p._exchange(self.rank, t.contiguous()))
+
+    def all_to_all(self, t: torch.Tensor) -> torch.Tensor:
+        parts = self._p._exchange(self.rank, t.contiguous())
+        return torch.stack([p[self.rank] for p in parts])
 
     def all_reduce_sum(self, t: torch.Tensor) -> None:
         parts = self._p._exchange(self.rank, t)

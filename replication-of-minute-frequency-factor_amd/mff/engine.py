@@ -123,33 +123,71 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
     dev = panel.device
     R = 1 if comm is None else comm.world_size
     S_all = S if comm is None else _agreed_max(comm, S, dev)
-    q_all = pdfq if comm is None else comm.all_gather(_pad_last(pdfq, S_all, float("nan")))
     M = R * 5 * S_all
     if M > PDF_MAX_QUERIES:
         raise _lib.MffError(f"doc_pdf: {M} queries per day exceed {PDF_MAX_QUERIES} "
                             f"(ranks*5*stocks); shard fewer stocks per day")
+    st = _stream(dev)
+    if comm is not None:
+        _pdf_ranks_sharded(lib, panel, pdfq, levels, rows, val, state, comm, S_all, M, st,
+                           day_batch)
+        return
     if day_batch is None:
         per_day = lib.mff_pdf_workspace_bytes(S, R, 1) + M * 8 + M * 8
         day_batch = max(1, min(D, workspace_budget // max(per_day, 1)))
-    st = _stream(dev)
     for d0 in range(0, D, day_batch):
         nd = min(day_batch, D - d0)
         ws = torch.empty(lib.mff_pdf_workspace_bytes(S, R, nd), dtype=torch.uint8, device=dev)
         q_sorted = torch.empty((nd, M), dtype=torch.int64, device=dev)
-        _lib.check(lib.mff_pdf_sort(_lib.ptr(q_all), R, S_all, D, d0, nd, _lib.ptr(q_sorted),
+        _lib.check(lib.mff_pdf_sort(_lib.ptr(pdfq), R, S_all, D, d0, nd, _lib.ptr(q_sorted),
                                     _lib.ptr(ws), st), "mff_pdf_sort")
-        if comm is None:  # single rank: count + finalize fused, no exchange
-            _lib.check(lib.mff_pdf_rank_local(_lib.ptr(levels), _lib.ptr(pdfq), S, D, d0, nd,
-                                              _lib.ptr(q_sorted), M,
-                                              _lib.int_array(rows), _lib.ptr(val), _lib.ptr(state), st),
-                       "mff_pdf_rank_local")
-            continue
+        # single rank: count + finalize fused, no exchange
+        _lib.check(lib.mff_pdf_rank_local(_lib.ptr(levels), _lib.ptr(pdfq), S, D, d0, nd,
+                                          _lib.ptr(q_sorted), M,
+                                          _lib.int_array(rows), _lib.ptr(val), _lib.ptr(state), st),
+                   "mff_pdf_rank_local")
+
+
+def _pdf_ranks_sharded(lib, panel, pdfq, levels, rows, val, state, comm, S_all: int, M: int, st,
+                       day_batch: Optional[int]):
+    """doc_pdf across stock shards: rank r sorts the queries of its own
+    contiguous day block only (all_to_all of the [5][days][S] query blocks), the sorted
+    lists are all-gathered, every rank counts its local level keys against each day's
+    full list, the one-word counts are all-reduced and every rank finalizes its own
+    stock-days.  The sort is not replicated: 1/R of the days per rank."""
+    from .dist import shard_bounds
+
+    D, S = panel.D, panel.S
+    dev = panel.device
+    R = comm.world_size
+    blocks = [shard_bounds(D, R, r) for r in range(R)]
+    nd_max = max(1, max(b1 - b0 for b0, b1 in blocks))
+    q_pad = _pad_last(pdfq, S_all, float("nan"))  # [5][D][S_all]
+    send = torch.full((R, 5, nd_max, S_all), float("nan"), dtype=torch.float64, device=dev)
+    for r, (b0, b1) in enumerate(blocks):
+        send[r, :, :b1 - b0] = q_pad[:, b0:b1]
+    recv = comm.all_to_all(send)  # [R][5][nd_max][S_all]: every rank's queries of my days
+    b0, b1 = blocks[comm.rank]
+    mine = torch.zeros((nd_max, M), dtype=torch.int64, device=dev)
+    if b1 > b0:
+        ws = torch.empty(lib.mff_pdf_workspace_bytes(S_all, R, b1 - b0), dtype=torch.uint8, device=dev)
+        _lib.check(lib.mff_pdf_sort(_lib.ptr(recv), R, S_all, nd_max, 0, b1 - b0, _lib.ptr(mine),
+                                    _lib.ptr(ws), st), "mff_pdf_sort")
+    gathered = comm.all_gather(mine)  # [R][nd_max][M]
+    q_sorted = torch.cat([gathered[r, :e - s] for r, (s, e) in enumerate(blocks)])  # [D][M]
+    del send, recv, gathered, mine
+    if day_batch is None:
+        day_batch = max(1, min(D, (1 << 30) // (M * 4)))
+    for d0 in range(0, D, day_batch):
+        nd = min(day_batch, D - d0)
+        qs = q_sorted[d0:d0 + nd]
+        ws = torch.empty(256, dtype=torch.uint8, device=dev)  # the count phase needs no scratch
         counts = torch.empty((nd, M), dtype=torch.int32, device=dev)  # 2 n_less + n_eq
         _lib.check(lib.mff_pdf_count(_lib.ptr(levels), S, D, d0, nd,
-                                     _lib.ptr(q_sorted), M, _lib.ptr(counts), _lib.ptr(ws), st),
+                                     _lib.ptr(qs), M, _lib.ptr(counts), _lib.ptr(ws), st),
                    "mff_pdf_count")
         comm.all_reduce_sum(counts)
-        _lib.check(lib.mff_pdf_finalize(_lib.ptr(pdfq), _lib.ptr(q_sorted), _lib.ptr(counts), S, D,
+        _lib.check(lib.mff_pdf_finalize(_lib.ptr(pdfq), _lib.ptr(qs), _lib.ptr(counts), S, D,
                                         d0, nd, M, _lib.int_array(rows), _lib.ptr(val),
                                         _lib.ptr(state), st), "mff_pdf_finalize")
 

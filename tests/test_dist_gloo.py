@@ -89,3 +89,36 @@ def test_thread_comm_matches_semantics():
         assert g.tolist() == [[0, 1, 2], [10, 11, 12], [20, 21, 22]]
         assert s == 6 and m == 2.0
     assert dist.shard_bounds(10, 3, 0) == (0, 4) and dist.shard_bounds(10, 3, 2) == (7, 10)
+
+
+def _a2a_worker(rank, world, port, resq):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "replication-of-minute-frequency-factor_amd"))
+    from mff import dist
+    comm, _ = dist.init_from_env(backend="gloo")
+    send = torch.stack([torch.full((2, 3), 10.0 * rank + r) for r in range(world)])
+    recv = comm.all_to_all(send)
+    resq.put((rank, [float(recv[r, 0, 0]) for r in range(world)]))
+    dist_.destroy_process_group()
+
+
+def test_gloo_all_to_all_world2():
+    """all_to_all (the doc_pdf day-block exchange): slice r of rank s arrives as slice s on
+    rank r, for torch.distributed (gloo) and ThreadComm alike."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_a2a_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {0: [0.0, 10.0], 1: [1.0, 11.0]}
+    from mff import dist
+    out = dist.run_threads(3, lambda c: c.all_to_all(
+        torch.stack([torch.tensor([10.0 * c.rank + r]) for r in range(3)])))
+    assert [o.squeeze(1).tolist() for o in out] == [[0.0, 10.0, 20.0], [1.0, 11.0, 21.0], [2.0, 12.0, 22.0]]

@@ -77,7 +77,7 @@ def test_min_freq_factor_gpu_batches_and_rolling(dev, panel_and_oracle, tmp_path
         assert not compare(v, s, rv, rs, name)
 
 
-@pytest.mark.parametrize("R", [2, 3])
+@pytest.mark.parametrize("R", [2, 3, 4])  # 4: uneven stock shards, a rank with no day block
 def test_sharded_ranks_match_unsharded_oracle(dev, panel_and_oracle, R):
     """R ranks (threads sharing the device, mff.dist.ThreadComm) each own a contiguous
     (uneven) stock shard: doc_pdf's frame-wide rank and stage 3 go through the same
