@@ -102,6 +102,15 @@ int mff_ingest_rows(const int32_t* stock, const int32_t* day, const int64_t* tim
  * Environment MFF_STAGE1_IMPL=w64 selects the wave-per-stock-day kernel for everything.
  */
 size_t mff_stage1_workspace_bytes(int S, int D);
+/* mff_stage1 in two calls with the same arguments: part 1 = the sorted families (ORD, LVL,
+ * doc_pdf levels and queries, exact list), part 2 = the serial families.  Once part 1 is
+ * done the mff_pdf_* phases may run on another stream, concurrently with part 2.
+ * part 3 = mff_stage1. */
+int mff_stage1_part(const float* open, const float* high, const float* low,
+                    const float* close, const float* volume, const uint32_t* valid,
+                    int S, int D, const int32_t* factor_ids /* host */, int nf,
+                    double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
+                    void* workspace, void* stream, int part);
 size_t mff_pdf_levels_bytes(int S, int D);
 int mff_stage1(const float* open, const float* high, const float* low,
                const float* close, const float* volume, const uint32_t* valid,

@@ -960,11 +960,15 @@ extern "C" size_t mff_pdf_levels_bytes(int S, int D) {
   return pdf_levels_split(S, D, &a, &b);
 }
 
-extern "C" int mff_stage1(const float* open, const float* high, const float* low, const float* close,
-                          const float* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
-                          int nf, double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
-                          void* workspace, void* stream) {
+// part bit 1: the sorted families (ORD thresholds, LVL/PDF levels + queries) and the exact
+// list kernel — everything the doc_pdf rank needs; part bit 2: the serial families (they
+// read the ORD thresholds of part 1).  mff_stage1 = both, in that order.
+static int stage1_parts(const float* open, const float* high, const float* low, const float* close,
+                        const float* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
+                        int nf, double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
+                        void* workspace, void* stream, int part) {
   clear_error();
+  MFF_REQUIRE(part >= 1 && part <= 3, "mff_stage1_part: part=%d must be 1, 2 or 3", part);
   MFF_REQUIRE(S > 0 && D > 0, "mff_stage1: S=%d D=%d must be positive", S, D);
   MFF_REQUIRE((long long)S * D < (1ll << 31), "mff_stage1: S*D must be < 2^31");
   MFF_REQUIRE(nf > 0 && nf <= NF, "mff_stage1: nf=%d out of range", nf);
@@ -994,6 +998,13 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
   MFF_REQUIRE(!(a.fam & F_PDF) || (pdf_query != nullptr && pdf_levels != nullptr),
               "mff_stage1: doc_pdf requested but pdf_query / pdf_levels is NULL");
   hipStream_t st = as_stream(stream);
+  int* cnt = reinterpret_cast<int*>(workspace);
+  a.fb_count = cnt;
+  a.fb_list = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + 256);
+  a.ord_th = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256 + (size_t)S * D * sizeof(int));
+  const char* impl = getenv("MFF_STAGE1_IMPL");
+  const bool w64 = impl && strcmp(impl, "w64") == 0;
+  if (part == 2) return w64 ? 0 : launch_serial(fld, valid, S, D, a.row, a.fam, val, state, a.ord_th, st);
   if (a.fam & F_PDF) {
     size_t ok, ow;
     pdf_levels_split(S, D, &ok, &ow);
@@ -1003,13 +1014,9 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
     a.lvl_w = reinterpret_cast<uint8_t*>(base + ow);
     MFF_HIP(hipMemsetAsync(a.lvl_count, 0, (size_t)D * 4, st));
   }
-  int* cnt = reinterpret_cast<int*>(workspace);
-  a.fb_count = cnt;
-  a.fb_list = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + 256);
   MFF_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
   const long long nblk = (long long)((S + 63) / 64) * D;
-  const char* impl = getenv("MFF_STAGE1_IMPL");
-  if (impl && strcmp(impl, "w64") == 0) {  // the wave-per-stock-day kernel for everything
+  if (w64) {  // the wave-per-stock-day kernel for everything
     const int rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, nullptr, nullptr, ~0u, 0, st);
     if (rc != 0 || !(a.fam & F_PDF)) return rc;
     g16::GArgs b = a;  // doc_pdf level lists only (no rows, no queries, no exact list)
@@ -1023,13 +1030,8 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
     return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_PDF, 1024, st,
                       a.lvl_count, a.lvl_key, a.lvl_w);
   }
-  a.ord_th = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256 + (size_t)S * D * sizeof(int));
-  // order: the ORD sort (thresholds) before the serial returns kernel (products)
+  // order: the ORD sort (thresholds) before the serial returns kernel (products, part 2)
   for (int gi = 0; gi < 2; ++gi) {
-    if (gi == 1) {
-      const int rc = launch_serial(fld, valid, S, D, a.row, a.fam, val, state, a.ord_th, st);
-      if (rc != 0) return rc;
-    }
     const uint32_t set = g16::kGroups[gi];
     if (!(a.fam & set)) continue;
     g16::GArgs b = a;  // this launch stores its own group's rows (and the queries) only
@@ -1044,8 +1046,26 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
   }
   if (a.fam & (F_LVL | F_PDF)) {
     // exact general path for the listed stock-days (LVL + PDF only)
-    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt,
-                      F_LVL | F_PDF, 1024, st, a.lvl_count, a.lvl_key, a.lvl_w);
+    const int rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt,
+                              F_LVL | F_PDF, 1024, st, a.lvl_count, a.lvl_key, a.lvl_w);
+    if (rc != 0) return rc;
   }
+  if (part & 2) return launch_serial(fld, valid, S, D, a.row, a.fam, val, state, a.ord_th, st);
   return 0;
+}
+
+extern "C" int mff_stage1(const float* open, const float* high, const float* low, const float* close,
+                          const float* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
+                          int nf, double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
+                          void* workspace, void* stream) {
+  return stage1_parts(open, high, low, close, volume, valid, S, D, factor_ids, nf, val, state, pdf_query,
+                      pdf_levels, workspace, stream, 3);
+}
+
+extern "C" int mff_stage1_part(const float* open, const float* high, const float* low, const float* close,
+                               const float* volume, const uint32_t* valid, int S, int D,
+                               const int32_t* factor_ids, int nf, double* val, uint8_t* state,
+                               double* pdf_query, void* pdf_levels, void* workspace, void* stream, int part) {
+  return stage1_parts(open, high, low, close, volume, valid, S, D, factor_ids, nf, val, state, pdf_query,
+                      pdf_levels, workspace, stream, part);
 }

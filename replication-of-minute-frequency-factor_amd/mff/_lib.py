@@ -30,6 +30,7 @@ SIGNATURES = {
     "mff_stage1_workspace_bytes": (c_size_t, [c_int, c_int]),
     "mff_pdf_levels_bytes": (c_size_t, [c_int, c_int]),
     "mff_stage1": (c_int, [P, P, P, P, P, P, c_int, c_int, IP, c_int, P, P, P, P, P, P]),
+    "mff_stage1_part": (c_int, [P, P, P, P, P, P, c_int, c_int, IP, c_int, P, P, P, P, P, P, c_int]),
     "mff_pdf_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mff_pdf_sort": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
     "mff_pdf_count": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),

@@ -13,6 +13,8 @@ Stage map:
 """
 from __future__ import annotations
 
+import os
+import threading
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -99,19 +101,44 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
               if need_pdf else None)
     b = panel.bars
     ws = torch.empty(lib.mff_stage1_workspace_bytes(S, D), dtype=torch.uint8, device=dev)
+    main = torch.cuda.current_stream(dev)
+    args = [_lib.ptr(b[0]), _lib.ptr(b[1]), _lib.ptr(b[2]), _lib.ptr(b[3]), _lib.ptr(b[4]),
+            _lib.ptr(panel.mask), S, D, _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
+            _lib.ptr(pdfq), _lib.ptr(levels), _lib.ptr(ws), main.cuda_stream]
+    rows = [ids.index(i) if i in ids else -1 for i in catalog.PDF_IDS]
     if events is not None:
-        events[0].record()
-    _lib.check(lib.mff_stage1(_lib.ptr(b[0]), _lib.ptr(b[1]), _lib.ptr(b[2]), _lib.ptr(b[3]),
-                              _lib.ptr(b[4]), _lib.ptr(panel.mask), S, D,
-                              _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
-                              _lib.ptr(pdfq), _lib.ptr(levels), _lib.ptr(ws), _stream(dev)),
-               "mff_stage1")
+        events[0].record(main)
+    if need_pdf and PDF_OVERLAP:
+        # part 1 (sorted families: doc_pdf levels + queries), then the doc_pdf rank on a
+        # side stream while part 2 (the serial families) runs on the launch stream
+        _lib.check(lib.mff_stage1_part(*args, 1), "mff_stage1_part(1)")
+        side = _side_stream(dev)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
+        _lib.check(lib.mff_stage1_part(*args, 2), "mff_stage1_part(2)")
+        if events is not None:
+            events[1].record(main)
+        main.wait_stream(side)
+        return val, state, ids
+    _lib.check(lib.mff_stage1(*args), "mff_stage1")
     if events is not None:
-        events[1].record()
+        events[1].record(main)
     if need_pdf:
-        rows = [ids.index(i) if i in ids else -1 for i in catalog.PDF_IDS]
         pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
     return val, state, ids
+
+
+# MFF_PDF_OVERLAP=0: doc_pdf after the whole stage-1 pass on one stream (A/B timing)
+PDF_OVERLAP = os.environ.get("MFF_PDF_OVERLAP", "1") != "0"
+_SIDE = {}
+
+
+def _side_stream(dev) -> torch.cuda.Stream:
+    key = (dev.index, threading.get_ident())
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(dev)
+    return _SIDE[key]
 
 
 def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows: List[int], val, state,
