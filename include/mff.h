@@ -102,8 +102,8 @@ int mff_ingest_rows(const int32_t* stock, const int32_t* day, const int64_t* tim
  * Environment MFF_STAGE1_IMPL=w64 selects the wave-per-stock-day kernel for everything.
  */
 size_t mff_stage1_workspace_bytes(int S, int D);
-/* mff_stage1 in two calls with the same arguments: part 1 = the sorted families (ORD, LVL,
- * doc_pdf levels and queries, exact list), part 2 = the serial families.  Once part 1 is
+/* mff_stage1 in two calls with the same arguments: part 1 = the LVL/PDF group (
+ * doc_pdf levels and queries, exact list), part 2 = ORD + the serial families.  Once part 1 is
  * done the mff_pdf_* phases may run on another stream, concurrently with part 2.
  * part 3 = mff_stage1. */
 int mff_stage1_part(const float* open, const float* high, const float* low,

@@ -960,9 +960,9 @@ extern "C" size_t mff_pdf_levels_bytes(int S, int D) {
   return pdf_levels_split(S, D, &a, &b);
 }
 
-// part bit 1: the sorted families (ORD thresholds, LVL/PDF levels + queries) and the exact
-// list kernel — everything the doc_pdf rank needs; part bit 2: the serial families (they
-// read the ORD thresholds of part 1).  mff_stage1 = both, in that order.
+// part bit 1: the LVL/PDF group (levels + queries) and the exact list kernel — everything
+// the doc_pdf rank needs; part bit 2: the ORD group and the serial families (which read
+// the ORD thresholds).  mff_stage1 = both, in that order.
 static int stage1_parts(const float* open, const float* high, const float* low, const float* close,
                         const float* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
                         int nf, double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
@@ -1004,53 +1004,59 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
   a.ord_th = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256 + (size_t)S * D * sizeof(int));
   const char* impl = getenv("MFF_STAGE1_IMPL");
   const bool w64 = impl && strcmp(impl, "w64") == 0;
-  if (part == 2) return w64 ? 0 : launch_serial(fld, valid, S, D, a.row, a.fam, val, state, a.ord_th, st);
-  if (a.fam & F_PDF) {
-    size_t ok, ow;
-    pdf_levels_split(S, D, &ok, &ow);
-    char* base = reinterpret_cast<char*>(pdf_levels);
-    a.lvl_count = reinterpret_cast<uint32_t*>(base);
-    a.lvl_key = reinterpret_cast<uint64_t*>(base + ok);
-    a.lvl_w = reinterpret_cast<uint8_t*>(base + ow);
-    MFF_HIP(hipMemsetAsync(a.lvl_count, 0, (size_t)D * 4, st));
-  }
-  MFF_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
   const long long nblk = (long long)((S + 63) / 64) * D;
-  if (w64) {  // the wave-per-stock-day kernel for everything
-    const int rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, nullptr, nullptr, ~0u, 0, st);
-    if (rc != 0 || !(a.fam & F_PDF)) return rc;
-    g16::GArgs b = a;  // doc_pdf level lists only (no rows, no queries, no exact list)
-    for (int i = 0; i < NF; ++i) b.row[i] = -1;
-    b.pdfq = nullptr;
-    b.fam = F_PDF;
-    b.fam_exact = 0u;
-    hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b);
-    MFF_LAUNCH_CHECK();
-    // levels of the wide days (listed by the launch above)
-    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_PDF, 1024, st,
-                      a.lvl_count, a.lvl_key, a.lvl_w);
-  }
-  // order: the ORD sort (thresholds) before the serial returns kernel (products, part 2)
-  for (int gi = 0; gi < 2; ++gi) {
+  // one 16-lane group launch; it stores its own group's rows (and the queries) only
+  auto group_launch = [&](int gi) -> int {
     const uint32_t set = g16::kGroups[gi];
-    if (!(a.fam & set)) continue;
-    g16::GArgs b = a;  // this launch stores its own group's rows (and the queries) only
+    if (!(a.fam & set)) return 0;
+    g16::GArgs b = a;
     for (int i = 0; i < NF; ++i)
       if (!(kFactorFamily[i] & set)) b.row[i] = -1;
     if (!(set & F_PDF)) b.pdfq = nullptr;
-    switch (gi) {
-      case 0: hipLaunchKernelGGL(g16::k_stage1g<g16::G_ORD>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
-      default: hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b); break;
-    }
+    if (gi == 0) hipLaunchKernelGGL(g16::k_stage1g<g16::G_ORD>, dim3((unsigned)nblk), dim3(256), 0, st, b);
+    else hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b);
     MFF_LAUNCH_CHECK();
-  }
-  if (a.fam & (F_LVL | F_PDF)) {
-    // exact general path for the listed stock-days (LVL + PDF only)
-    const int rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt,
-                              F_LVL | F_PDF, 1024, st, a.lvl_count, a.lvl_key, a.lvl_w);
+    return 0;
+  };
+  if (part & 1) {  // LVL/PDF group + exact list: everything the doc_pdf phases read
+    if (a.fam & F_PDF) {
+      size_t ok, ow;
+      pdf_levels_split(S, D, &ok, &ow);
+      char* base = reinterpret_cast<char*>(pdf_levels);
+      a.lvl_count = reinterpret_cast<uint32_t*>(base);
+      a.lvl_key = reinterpret_cast<uint64_t*>(base + ok);
+      a.lvl_w = reinterpret_cast<uint8_t*>(base + ow);
+      MFF_HIP(hipMemsetAsync(a.lvl_count, 0, (size_t)D * 4, st));
+    }
+    MFF_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
+    if (w64) {  // the wave-per-stock-day kernel for everything
+      const int rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, nullptr, nullptr, ~0u, 0, st);
+      if (rc != 0 || !(a.fam & F_PDF)) return rc;
+      g16::GArgs b = a;  // doc_pdf level lists only (no rows, no queries, no exact list)
+      for (int i = 0; i < NF; ++i) b.row[i] = -1;
+      b.pdfq = nullptr;
+      b.fam = F_PDF;
+      b.fam_exact = 0u;
+      hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b);
+      MFF_LAUNCH_CHECK();
+      // levels of the wide days (listed by the launch above)
+      return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_PDF, 1024, st,
+                        a.lvl_count, a.lvl_key, a.lvl_w);
+    }
+    int rc = group_launch(1);
     if (rc != 0) return rc;
+    if (a.fam & (F_LVL | F_PDF)) {
+      // exact general path for the listed stock-days (LVL + PDF only)
+      rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt,
+                      F_LVL | F_PDF, 1024, st, a.lvl_count, a.lvl_key, a.lvl_w);
+      if (rc != 0) return rc;
+    }
   }
-  if (part & 2) return launch_serial(fld, valid, S, D, a.row, a.fam, val, state, a.ord_th, st);
+  if ((part & 2) && !w64) {  // the ORD sort (thresholds) before the serial kernels (products)
+    const int rc = group_launch(0);
+    if (rc != 0) return rc;
+    return launch_serial(fld, valid, S, D, a.row, a.fam, val, state, a.ord_th, st);
+  }
   return 0;
 }
 
