@@ -1,7 +1,7 @@
 // mff_stage1s.hip — stage 1, one lane per stock-day: the streaming families.
 //
-// Lane = stock s of day d (a 256-thread block is 256 consecutive stocks of one day, so
-// every factor row store val[row][d][s] is one 512-byte line per wave).  Each lane walks
+// Lane = stock-day sd = d * S + s (a 256-thread block is 256 consecutive stock-days, so
+// every factor row store val[row][sd] is one 512-byte line per wave).  Each lane walks
 // its own 240 bars in order, four at a time (one float4 per plane, the next four
 // prefetched), carrying the previous present bar and the running sums in registers:
 // nothing crosses lanes, no reduction, and every finishing formula runs once per
@@ -118,15 +118,15 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 template <uint32_t SET, bool FULL>
 __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) {
   const uint32_t fam = FULL ? SET : (a.fam & SET);
-  const int ntile = (a.S + 255) / 256;
-  const int d = blockIdx.x / ntile;
-  const int s0 = (blockIdx.x % ntile) * 256;
-  const int s = s0 + (int)threadIdx.x;
-  // every lane walks (with LDS staging a lane also fetches other lanes' rows); lanes past
-  // the last stock walk a copy of it and store nothing
-  const bool act = s < a.S;
+  // a block is 256 consecutive stock-days of the flattened [D][S] order (val, state, the
+  // planes' rows, the mask and the ORD thresholds are all indexed by sd = d * S + s), so
+  // no lanes idle at the end of a day whatever S is (S = 625 per GPU at 8 GPUs)
   const size_t plane = (size_t)a.D * a.S;
-  const size_t sd = (size_t)d * a.S + (act ? s : a.S - 1);
+  const size_t sd0 = (size_t)blockIdx.x * 256;
+  // every lane walks (with LDS staging a lane also fetches other lanes' rows); lanes past
+  // the last stock-day walk a copy of it and store nothing
+  const bool act = sd0 + threadIdx.x < plane;
+  const size_t sd = act ? sd0 + threadIdx.x : plane - 1;
 
   auto put = [&](int f, double x, uint32_t st) {
     const int r = a.row[f];
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
       for (int p = 0; p < 5; ++p)
         if ((PLM >> p) & 1u) pbase[pi++] = a.fld[p];
     }
-    const int rowbase = s0 + 64 * wave;
+    const size_t rowbase = sd0 + 64 * wave;
     auto dma = [&](float4(*sb)[64 * CQ], int c, int img0) {
 #pragma unroll
       for (int pi = 0; pi < NP; ++pi)
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
         for (int i = 0; i < CQ; ++i) {
           const int r = (64 / CQ) * i + lane / CQ;
           const int k = (lane % CQ) ^ swz(r);
-          const size_t row = (size_t)d * a.S + min(rowbase + r, a.S - 1);
+          const size_t row = min(rowbase + r, plane - 1);
           const float* src = pbase[pi] + row * NBAR + BC * c + 4 * k;
           __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)&sb[img0 + pi][64 * i], 16, 0, 0);
         }
@@ -659,7 +659,7 @@ int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D
   a.fam = fam & kSerial;
   for (int i = 0; i < NF; ++i) a.row[i] = (kFactorFamily[i] & kSerial) ? row[i] : (int8_t)-1;
   if (!a.fam) return 0;
-  const long long nblk = (long long)((S + 255) / 256) * D;
+  const long long nblk = ((long long)S * D + 255) / 256;
   // a launch stages every plane of its set: planes the requested factors do not read may
   // be NULL, so they alias one the launch does read (fetched, never used)
   auto patched = [&](uint32_t set) {
