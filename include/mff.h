@@ -159,6 +159,18 @@ int mff_stage2(const double* val, const uint8_t* state, int rows, int D, int S,
                int N, int method, double* out_val, uint8_t* out_state, void* stream);
 
 /*
+ * Calendar resampling, mode='calendar' of cal_final_exposure (MinuteFrequentFactorCICC.py:
+ * 130-186; the reference raises there: group_by_dynamic without index_column, MF:145 —
+ * this is the build's definition): per stock and calendar window p (days
+ * [period_start[p], period_start[p+1]), period_start int32 [P+1] device, date-sorted),
+ * over the window's rows: 'o' last value (null if the last row is null), 'm' mean,
+ * 'std' std (ddof=1), 'z' (last - mean) / std; nulls skipped, NaN propagates.
+ * Output [P][S]: ABSENT where the stock has no row in the window.
+ */
+int mff_calendar(const double* val, const uint8_t* state, const int32_t* period_start, int D,
+                 int S, int P, int method, double* out_val, uint8_t* out_state, void* stream);
+
+/*
  * Stage 3: per-day cross-sectional z-score (ddof=1) or average rank over stocks with
  * state VALUE and non-NaN value.  No single reference function; closest semantics
  * Factor.py:99-105 (coverage), :163-186 (per-date Pearson / Spearman), :285-291 (qcut).

@@ -1129,3 +1129,39 @@ def oracle_group_test(xv, xs, pct, ps, period_of, P: int, G: int, wv=None, ws=No
                 sw = sum(w for _, w, ok in rows if ok)
                 ret[p, g] = sum(w * r for r, w, ok in rows if ok) / sw if sw != 0 else 0.0
     return ret, present
+
+
+# ----------------------------------------------------------------------------
+# Calendar resampling (cal_final_exposure mode='calendar', MF:130-186)
+# ----------------------------------------------------------------------------
+
+def oracle_calendar(val: np.ndarray, state: np.ndarray, pstart: np.ndarray, method: str):
+    """Per code and calendar window [pstart[p], pstart[p+1]) over the window's rows
+    (the reference raises here; the build's definition): 'o' = last row's value
+    (null if null), 'm' = pl.mean, 'std' = pl.std (ddof=1, S1), 'z' = (last - mean) / std
+    with nulls propagating.  Returns [P][S] (val, state); ABSENT without rows."""
+    P = len(pstart) - 1
+    S = val.shape[1]
+    out_v = np.zeros((P, S))
+    out_s = np.zeros((P, S), np.uint8)
+    for p in range(P):
+        for s in range(S):
+            rows = [d for d in range(pstart[p], pstart[p + 1]) if state[d, s] != ABSENT]
+            if not rows:
+                continue
+            xs = [val[d, s] if state[d, s] == VALUE else None for d in rows]
+            last = xs[-1]
+            nn = _nn(xs)
+            mean = _mean_exact(nn) if nn.size else None  # C3/C6: constant window -> z NaN
+            sd = pl_std(xs, ddof=1)
+            if method == "o":
+                r = last
+            elif method == "m":
+                r = mean
+            elif method == "std":
+                r = sd
+            else:
+                r = None if last is None or sd is None else _div(last - mean, sd)
+            out_s[p, s] = NULLV if r is None else VALUE
+            out_v[p, s] = 0.0 if r is None else r
+    return out_v, out_s

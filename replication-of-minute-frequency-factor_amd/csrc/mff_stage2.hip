@@ -93,6 +93,75 @@ __global__ __launch_bounds__(64) void k_stage2(const double* val, const uint8_t*
   }
 }
 
+// Calendar resampling (MF:130-186, mode='calendar'): per (code, calendar window) over the
+// exposure rows of the window — last value ('o'), mean ('m'), (last - mean) / std ('z'),
+// std ('std'), std with ddof=1 (polars default, S1), nulls skipped by mean / std (S9),
+// NaN propagating (S10).  The reference itself raises here (group_by_dynamic without
+// index_column, MF:145), so this is the build's definition of the intended operation
+// (DESIGN.md §7).  Lane = stock, loop over windows; window p holds days
+// [pstart[p], pstart[p+1]).  Two passes per window: the mean shifted by the first finite
+// value (a constant window gives exact 0 deviations, C3), then the squared deviations.
+__global__ __launch_bounds__(256) void k_calendar(const double* val, const uint8_t* state, const int32_t* pstart,
+                                                   int D, int S, int P, int method, double* out_val,
+                                                   uint8_t* out_state) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s >= S) return;
+  for (int p = 0; p < P; ++p) {
+    const int d0 = pstart[p], d1 = pstart[p + 1];
+    bool rows = false;
+    uint8_t lst = MFF_STATE_NULL;
+    double last = 0.0, x0 = 0.0, s1 = 0.0;
+    bool have0 = false;
+    int n = 0;
+    for (int d = d0; d < d1; ++d) {
+      const size_t i = (size_t)d * S + s;
+      const uint8_t st = state[i];
+      if (st == MFF_STATE_ABSENT) continue;
+      rows = true;
+      lst = st;
+      last = val[i];
+      if (st != MFF_STATE_VALUE) continue;
+      if (!have0 && __builtin_isfinite(last)) { x0 = last; have0 = true; }
+      ++n;
+    }
+    for (int d = d0; d < d1; ++d) {
+      const size_t i = (size_t)d * S + s;
+      if (state[i] == MFF_STATE_VALUE) s1 += val[i] - x0;
+    }
+    const double mean = x0 + s1 / (double)n;
+    double m2 = 0.0;
+    for (int d = d0; d < d1; ++d) {
+      const size_t i = (size_t)d * S + s;
+      if (state[i] == MFF_STATE_VALUE) {
+        const double dl = val[i] - mean;
+        m2 += dl * dl;
+      }
+    }
+    const double sd = sqrt(m2 / (double)(n - 1));
+    const size_t o = (size_t)p * S + s;
+    uint8_t ost;
+    double res = 0.0;
+    if (!rows) {
+      ost = MFF_STATE_ABSENT;
+    } else if (method == MFF_ROLL_O) {
+      ost = lst;
+      res = lst == MFF_STATE_VALUE ? last : 0.0;
+    } else if (method == MFF_ROLL_M) {
+      ost = n > 0 ? MFF_STATE_VALUE : MFF_STATE_NULL;
+      res = n > 0 ? mean : 0.0;
+    } else if (method == MFF_ROLL_STD) {
+      ost = n > 1 ? MFF_STATE_VALUE : MFF_STATE_NULL;
+      res = n > 1 ? sd : 0.0;
+    } else {  // z: null when the last value or the std is null
+      const bool ok = n > 1 && lst == MFF_STATE_VALUE;
+      ost = ok ? MFF_STATE_VALUE : MFF_STATE_NULL;
+      res = ok ? (last - mean) / sd : 0.0;
+    }
+    out_val[o] = res;
+    out_state[o] = ost;
+  }
+}
+
 }  // namespace mff
 
 using namespace mff;
@@ -108,6 +177,18 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
   const size_t lds = (size_t)N * 64 * 8;
   hipLaunchKernelGGL(k_stage2, dim3((unsigned)nblk), dim3(64), lds, as_stream(stream), val, state, D, S,
                      N, method, out_val, out_state);
+  MFF_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mff_calendar(const double* val, const uint8_t* state, const int32_t* period_start, int D,
+                            int S, int P, int method, double* out_val, uint8_t* out_state, void* stream) {
+  clear_error();
+  MFF_REQUIRE(D > 0 && S > 0 && P > 0, "mff_calendar: bad sizes D=%d S=%d P=%d", D, S, P);
+  MFF_REQUIRE(method >= MFF_ROLL_O && method <= MFF_ROLL_STD, "mff_calendar: unknown method %d", method);
+  MFF_REQUIRE(val && state && period_start && out_val && out_state, "mff_calendar: NULL buffer");
+  hipLaunchKernelGGL(k_calendar, dim3((S + 255) / 256), dim3(256), 0, as_stream(stream), val, state,
+                     period_start, D, S, P, method, out_val, out_state);
   MFF_LAUNCH_CHECK();
   return 0;
 }

@@ -37,6 +37,7 @@ SIGNATURES = {
     "mff_pdf_finalize": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, IP, P, P, P]),
     "mff_pdf_rank_local": (c_int, [P, P, c_int, c_int, c_int, c_int, P, c_int, IP, P, P, P]),
     "mff_stage2": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
+    "mff_calendar": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, P]),
     "mff_xs_moments": (c_int, [P, P, c_int, c_int, c_int, P, P]),
     "mff_xs_zscore": (c_int, [P, P, c_int, c_int, c_int, P, c_int, P, P, P]),
     "mff_xs_rank_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),

@@ -357,3 +357,17 @@ def group_returns(x_val: torch.Tensor, x_state: torch.Tensor, pct_val: torch.Ten
     _lib.check(lib.mff_bt_finalize(_lib.ptr(part_all), R, P, G, int(w_val is not None), _lib.ptr(ret),
                                    _lib.ptr(present), st), "mff_bt_finalize")
     return ret, present
+
+
+def calendar(val: torch.Tensor, state: torch.Tensor, period_start: torch.Tensor, method: str):
+    """MinFreqFactor.cal_final_exposure(mode='calendar') (MF:130-186, the build's definition):
+    dense [D][S] -> [P][S] per calendar window (period_start int32 [P+1] on the device)."""
+    lib = _lib.load()
+    D, S = val.shape
+    P = int(period_start.numel()) - 1
+    ov = torch.empty((P, S), dtype=torch.float64, device=val.device)
+    os_ = torch.empty((P, S), dtype=torch.uint8, device=val.device)
+    _lib.check(lib.mff_calendar(_lib.ptr(val), _lib.ptr(state), _lib.ptr(period_start), D, S, P,
+                                ROLL_METHODS[method], _lib.ptr(ov), _lib.ptr(os_), _stream(val.device)),
+               "mff_calendar")
+    return ov, os_

@@ -246,6 +246,25 @@ def rebalance_periods(dates, frequency: str):
     return np.asarray(codes, dtype=np.int64), labels
 
 
+def calendar_windows(dates, frequency: str):
+    """group_by_dynamic(every='1w'/'1mo') windows with polars' defaults (closed='left',
+    label='left', windows truncated to Monday / the 1st) over sorted dates ->
+    (period_start int32 [P+1]: first date index of each window, then len(dates); the
+    windows' left-edge labels)."""
+    pd = _pd()
+    freq = {"weekly": "W-SUN", "monthly": "M"}.get(frequency)
+    if freq is None:
+        raise ValueError(f"Unsupported frequency for calendar: {frequency}")
+    per = pd.to_datetime(pd.Series(list(dates))).dt.to_period(freq)
+    codes, uniq = pd.factorize(per, sort=True)
+    codes = np.asarray(codes)
+    if np.any(np.diff(codes) < 0):
+        raise ValueError("dates must be sorted")
+    start = np.searchsorted(codes, np.arange(len(uniq)), side="left")
+    pstart = np.append(start, len(dates)).astype(np.int32)
+    return pstart, [u.start_time.date() for u in uniq]
+
+
 class MinFreqFactor(Factor):
     """MinuteFrequentFactorCICC.py:8-245."""
 
@@ -347,9 +366,12 @@ class MinFreqFactor(Factor):
 
     def cal_final_exposure(self, frequency, method: str, mode: str = "calendar", pool="full"):
         """MF:114-245.  mode='days': per-code rolling over present rows on the GPU
-        (stage 2).  mode='calendar': the reference raises inside polars here
-        (group_by_dynamic without index_column, MF:145-178), so its semantics are
-        undefined; argument validation matches, then NotImplementedError."""
+        (stage 2).  mode='calendar': per code and calendar window (weekly: Monday-based
+        weeks, monthly: calendar months; polars group_by_dynamic defaults closed='left',
+        label='left') the last value / mean / (last - mean) / std / std (ddof=1) of the
+        window's rows on the GPU (mff_calendar).  The reference raises inside polars there
+        (group_by_dynamic without index_column, MF:145-178): this is the build's
+        definition of the intended operation, argument checks as MF:131-140."""
         if mode == "calendar":
             if frequency not in ("weekly", "monthly"):
                 raise ValueError(f"Unsupported frequency for calendar: {frequency}")
@@ -357,9 +379,19 @@ class MinFreqFactor(Factor):
                 raise ValueError(f"不支持的股票池: {pool}")
             if method not in ("o", "m", "z", "std"):
                 raise ValueError("Unknown method")
-            raise NotImplementedError(
-                "calendar resampling: the reference fails here (group_by_dynamic without "
-                "index_column, MinuteFrequentFactorCICC.py:145); use mode='days'")
+            import torch
+
+            from . import engine
+            from .factors import _device
+
+            name = f"{frequency}_{self.factor_name}_{method}"  # MF:141
+            val, state, codes, dates = frames.from_long(self.factor_exposure, self.factor_name)
+            pstart, labels = calendar_windows(dates, frequency)
+            dev = _device(None)
+            ov, os_ = engine.calendar(torch.from_numpy(val).to(dev), torch.from_numpy(state).to(dev),
+                                      torch.from_numpy(pstart).to(dev), method)
+            torch.cuda.synchronize(dev)
+            return frames.to_long(ov.cpu().numpy(), os_.cpu().numpy(), codes, labels, name)
         if mode != "days":
             raise ValueError(f"Unknown mode: {mode}")
         if not isinstance(frequency, int):

@@ -120,8 +120,8 @@ def test_final_exposure_argument_errors():
         f.cal_final_exposure(5, "m", mode="calendar")
     with pytest.raises(ValueError, match="不支持的股票池"):
         f.cal_final_exposure("weekly", "m", mode="calendar", pool="300")
-    with pytest.raises(NotImplementedError):
-        f.cal_final_exposure("weekly", "m", mode="calendar")
+    with pytest.raises(ValueError, match="Unknown method"):
+        f.cal_final_exposure("weekly", "q", mode="calendar")
     with pytest.raises(ValueError, match="Unsupported frequency for days"):
         f.cal_final_exposure("weekly", "m", mode="days")
     with pytest.raises(ValueError, match="Unknown method"):

@@ -242,3 +242,46 @@ def test_factor_group_test_end_to_end(dev):
                         "pct_change": oret[p_idx, g_idx]}).sort_values(["date", "group"]).reset_index(drop=True)
     assert list(g["date"]) == list(exp["date"]) and list(g["group"]) == list(exp["group"])
     np.testing.assert_allclose(g["pct_change"].to_numpy(), exp["pct_change"].to_numpy(), rtol=1e-9)
+
+
+# --------------------------------------------------------------------------- calendar mode
+def test_calendar_windows_left_labels():
+    from mff.factor import calendar_windows
+    dates = [dt.date(2024, 1, 30), dt.date(2024, 1, 31), dt.date(2024, 2, 1), dt.date(2024, 2, 5)]
+    ps, lab = calendar_windows(dates, "monthly")
+    assert list(ps) == [0, 2, 4] and lab == [dt.date(2024, 1, 1), dt.date(2024, 2, 1)]
+    ps, lab = calendar_windows(dates, "weekly")
+    assert list(ps) == [0, 3, 4] and lab == [dt.date(2024, 1, 29), dt.date(2024, 2, 5)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", ["o", "m", "z", "std"])
+@pytest.mark.parametrize("frequency", ["weekly", "monthly"])
+def test_calendar_matches_oracle(dev, method, frequency):
+    """mff_calendar against oracle_calendar: nulls, NaN, suspensions, a constant window
+    (z -> NaN), single-row windows (std null)."""
+    from mff import engine
+    from mff.factor import calendar_windows
+    _, _, x, xs = _daily(np.random.default_rng(21), D=75, S=37)
+    x[10:17, 5] = 2.5                                  # constant week for stock 5
+    dates = [dt.date(2024, 1, 1) + dt.timedelta(days=i) for i in range(x.shape[0])]
+    ps, _ = calendar_windows(dates, frequency)
+    gv, gs = engine.calendar(_t(x, dev), _t(xs, dev), _t(ps, dev), method)
+    ov, os_ = O.oracle_calendar(x, xs, ps, method)
+    assert not compare(gv.cpu().numpy(), gs.cpu().numpy(), ov, os_, f"calendar-{method}", atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_cal_final_exposure_calendar_end_to_end(dev):
+    from mff import frames
+    from mff.factor import MinFreqFactor, calendar_windows
+    _, _, x, xs = _daily(np.random.default_rng(22), D=40, S=20)
+    codes = [f"{i:06d}.SZ" for i in range(x.shape[1])]
+    dates = [dt.date(2024, 3, 1) + dt.timedelta(days=i) for i in range(x.shape[0])]
+    f = MinFreqFactor("f", frames.to_long(x, xs, codes, dates, "f"))
+    got = f.cal_final_exposure("monthly", "z", mode="calendar")
+    assert list(got.columns) == ["code", "date", "monthly_f_z"]
+    ps, labels = calendar_windows(dates, "monthly")
+    ov, os_ = O.oracle_calendar(x, xs, ps, "z")
+    v, s, _, _ = frames.from_long(got, "monthly_f_z", codes=codes, dates=labels)
+    assert not compare(v, s, ov, os_, "calendar-z", atol=1e-12)
