@@ -18,6 +18,7 @@ oracle for this one).
 from __future__ import annotations
 
 import datetime as _dt
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -52,8 +53,7 @@ def _date32(col):
     import pyarrow as pa
     import pyarrow.compute as pc
 
-    if isinstance(col, pa.ChunkedArray):
-        col = col.combine_chunks()
+    col = _one(col)
     t = col.type
     if pa.types.is_date32(t):
         pass
@@ -71,22 +71,28 @@ def _as_date(x):
     return f(x)
 
 
+def _one(col):
+    """ChunkedArray -> Array without a copy when it has one chunk (a parquet day file
+    read whole usually does)."""
+    import pyarrow as pa
+
+    if isinstance(col, pa.ChunkedArray):
+        return col.chunk(0) if col.num_chunks == 1 else col.combine_chunks()
+    return col
+
+
 def _numeric(col, dtype):
     import pyarrow as pa
     import pyarrow.compute as pc
 
-    if isinstance(col, pa.ChunkedArray):
-        col = col.combine_chunks()
+    col = _one(col)
     if col.null_count:
         col = pc.fill_null(col.cast(pa.float64()), float("nan"))
     return np.ascontiguousarray(col.to_numpy(zero_copy_only=False), dtype=dtype)
 
 
 def _volume(col):
-    import pyarrow as pa
-
-    if isinstance(col, pa.ChunkedArray):
-        col = col.combine_chunks()
+    col = _one(col)
     arr = _numeric(col, None) if col.null_count else col.to_numpy(zero_copy_only=False)
     arr = np.ascontiguousarray(arr)
     if arr.dtype not in _VOLUME_KIND:
@@ -94,13 +100,59 @@ def _volume(col):
     return arr, _VOLUME_KIND[arr.dtype]
 
 
-def universes(tables) -> tuple:
-    """Sorted code and date universes of a list of tables (pyarrow.compute unique)."""
+def _dict_codes(t):
+    """The table with its code column dictionary-encoded (one hash pass over the strings;
+    the universe and the per-row stock index then come from the small dictionary)."""
+    import pyarrow as pa
     import pyarrow.compute as pc
 
+    if "code" not in t.column_names:
+        return t
+    col = _one(t.column("code"))
+    if pa.types.is_dictionary(col.type):
+        return t
+    if not (pa.types.is_string(col.type) or pa.types.is_large_string(col.type)):
+        col = pc.cast(col, pa.string())
+    return t.set_column(t.column_names.index("code"), "code", pc.dictionary_encode(col))
+
+
+def _code_values(col):
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    col = _one(col)
+    if pa.types.is_dictionary(col.type):
+        return [x for x in col.dictionary.to_pylist() if x is not None]
+    return [x for x in pc.unique(col).to_pylist() if x is not None]
+
+
+def _stock_index(col, codes) -> np.ndarray:
+    """code column -> int32 index into the sorted universe `codes` (-1: not in it / null)."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    vs = pa.array(list(codes), pa.string())
+    col = _one(col)
+    if pa.types.is_dictionary(col.type):
+        dic = col.dictionary
+        if not (pa.types.is_string(dic.type) or pa.types.is_large_string(dic.type)):
+            dic = pc.cast(dic, pa.string())
+        m = np.asarray(pc.fill_null(pc.index_in(dic, value_set=vs), -1).to_numpy(zero_copy_only=False),
+                       dtype=np.int32)
+        m = np.append(m, np.int32(-1))  # slot for null rows
+        idx = pc.fill_null(col.indices, len(dic)).to_numpy(zero_copy_only=False)
+        return np.ascontiguousarray(m[idx], dtype=np.int32)
+    if not (pa.types.is_string(col.type) or pa.types.is_large_string(col.type)):
+        col = pc.cast(col, pa.string())
+    stock = pc.fill_null(pc.index_in(col, value_set=vs), -1)
+    return np.ascontiguousarray(stock.to_numpy(zero_copy_only=False), dtype=np.int32)
+
+
+def universes(tables) -> tuple:
+    """Sorted code and date universes of a list of tables."""
     codes, days = set(), set()
     for t in tables:
-        codes.update(pc.unique(t.column("code")).to_pylist())
+        codes.update(_code_values(t.column("code")))
         days.update(np.unique(_date32(t.column("date"))).tolist())
     return sorted(codes), sorted(days)
 
@@ -114,15 +166,16 @@ def encode(t, codes: Sequence[str], day_numbers: Sequence[int]):
     for k in ("code", "date", "time") + FIELDS:
         if k not in t.column_names:
             raise ValueError(f"missing column {k!r}")
-    code = t.column("code")
-    if not (pa.types.is_string(code.type) or pa.types.is_large_string(code.type)):
-        code = pc.cast(code, pa.string())
-    stock = pc.fill_null(pc.index_in(code, value_set=pa.array(list(codes), pa.string())), -1)
-    stock = np.ascontiguousarray(stock.to_numpy(zero_copy_only=False), dtype=np.int32)
+    stock = _stock_index(t.column("code"), codes)
     dn = _date32(t.column("date"))
     uday = np.asarray(day_numbers, dtype=np.int32)
-    day = np.searchsorted(uday, dn).astype(np.int32)
-    day[(day >= uday.size) | (uday[np.minimum(day, uday.size - 1)] != dn)] = -1
+    lo, hi = (int(dn.min()), int(dn.max())) if dn.size else (0, 0)
+    if lo == hi:  # a day file: one date
+        k = int(np.searchsorted(uday, lo))
+        day = np.full(dn.size, k if k < uday.size and uday[k] == lo else -1, dtype=np.int32)
+    else:
+        day = np.searchsorted(uday, dn).astype(np.int32)
+        day[(day >= uday.size) | (uday[np.minimum(day, uday.size - 1)] != dn)] = -1
     time = _numeric(t.column("time"), np.int64)
     px = [_numeric(t.column(k), np.float64) for k in FIELDS[:4]]
     vol, kind = _volume(t.column("volume"))
@@ -173,8 +226,11 @@ class PanelIngest:
         return s
 
     def push(self, df) -> None:
-        t = _table(df)
-        stock, day, time, px, vol, kind = encode(t, self.codes, self.day_numbers)
+        self.push_encoded(encode(_table(df), self.codes, self.day_numbers))
+
+    def push_encoded(self, enc) -> None:
+        """Stage and launch one table already encoded by :func:`encode`."""
+        stock, day, time, px, vol, kind = enc
         n = int(stock.size)
         if n == 0:
             return
@@ -213,13 +269,25 @@ class PanelIngest:
 def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None):
     """One or more long tables -> DevicePanel (universes: the tables' sorted codes and
     dates, or the given code universe)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     tabs = [_table(t) for t in (tables if isinstance(tables, (list, tuple)) else [tables])]
-    ucodes, udays = universes(tabs)
-    if codes is not None:
-        ucodes = list(codes)
-    ing = PanelIngest(ucodes, udays, device)
-    for t in tabs:
-        ing.push(t)
+    # pyarrow / numpy kernels release the GIL: tables are encoded by a few host threads
+    # (in order, a bounded window ahead) while earlier ones are copied and scattered
+    workers = max(1, min(4, len(tabs), os.cpu_count() or 1))
+    with ThreadPoolExecutor(workers) as pool:
+        tabs = list(pool.map(_dict_codes, tabs))
+        ucodes, udays = universes(tabs)
+        if codes is not None:
+            ucodes = list(codes)
+        ing = PanelIngest(ucodes, udays, device)
+        futs = [pool.submit(encode, t, ing.codes, ing.day_numbers) for t in tabs[:workers]]
+        for i in range(len(tabs)):
+            enc = futs[i].result()
+            if i + workers < len(tabs):
+                futs.append(pool.submit(encode, tabs[i + workers], ing.codes, ing.day_numbers))
+            ing.push_encoded(enc)
+            futs[i] = None
     return ing.finish()
 
 
