@@ -237,6 +237,7 @@ def main():
         val, state, _ = step()
         torch.cuda.synchronize()
         def timed(fn):
+            fn()  # first call sizes the caching allocator; the timed call reuses its blocks
             torch.cuda.synchronize()
             t = time.perf_counter()
             r = fn()
@@ -246,8 +247,12 @@ def main():
         extras["step_ms_rank0"] = round(elapsed / args.steps * 1e3, 3)
         ms, _ = timed(lambda: engine.rolling(val, state, 20, "z"))
         extras["stage2_z20_all58_ms"] = round(ms, 3)
+        # algorithmic bytes of stage 2 / stage-3 z: 8 + 1 B in and out per (factor, day, stock)
+        xs_bytes = 18.0 * val.numel()
+        extras["stage2_z20_GBps"] = round(xs_bytes / (ms * 1e-3) / 1e9, 1)
         ms, _ = timed(lambda: engine.cross_section(val, state, "z", comm=comm))
         extras["stage3_z_all58_ms"] = round(ms, 3)
+        extras["stage3_z_GBps"] = round(xs_bytes / (ms * 1e-3) / 1e9, 1)
         ms, _ = timed(lambda: engine.cross_section(val[:4], state[:4], "rank", comm=comm))
         extras["stage3_rank_4factors_ms"] = round(ms, 3)
         del val, state

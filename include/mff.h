@@ -183,6 +183,11 @@ int mff_xs_moments(const double* val, const uint8_t* state, int rows, int D, int
 int mff_xs_zscore(const double* val, const uint8_t* state, int rows, int D, int S,
                   const double* moments_all, int R, double* out_val,
                   uint8_t* out_state, void* stream);
+/* Single-rank z in one pass (same result contract as moments + zscore with R = 1):
+ * one workgroup per (row, day) holds the column in registers; S <= max_stocks(). */
+int mff_xs_zscore_local(const double* val, const uint8_t* state, int rows, int D, int S,
+                        double* out_val, uint8_t* out_state, void* stream);
+int mff_xs_zscore_local_max_stocks(void);
 size_t mff_xs_rank_workspace_bytes(int rows, int D, int S_all, int R);
 int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_loc,
                 const double* val_all, const uint8_t* state_all, int R, int S_all,

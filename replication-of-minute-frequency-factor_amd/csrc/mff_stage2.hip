@@ -93,6 +93,106 @@ __global__ __launch_bounds__(64) void k_stage2(const double* val, const uint8_t*
   }
 }
 
+// Register-window variant for the common window lengths (N a template constant): the
+// last N present values live in VGPRs as a shift register (w[N-1] = newest, w[0] =
+// oldest, shifted on present days only), so the per-day recompute reads no LDS, and the
+// days are loaded S2_U at a time one chunk ahead (S2_U loads in flight per lane instead
+// of 1).  Same window arithmetic as k_stage2 (mean shifted by the oldest value when
+// finite, two passes over the window), summed oldest -> newest, the two divisions by N
+// as products with 1/N (a constant window still gives s1 = s2 = 0 exactly: std 0, z NaN).
+constexpr int S2_U = 4;  // 4 in flight + 4 processed: <= 96 VGPRs at N = 20 (5 waves/SIMD)
+constexpr int S2_THREADS = 256;
+
+template <int N>
+__global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, const uint8_t* state, int D, int S,
+                                                         int method, double* out_val, uint8_t* out_state) {
+  const int nsb = (S + S2_THREADS - 1) / S2_THREADS;
+  const int row = blockIdx.x / nsb;
+  const int s = (blockIdx.x % nsb) * S2_THREADS + (int)threadIdx.x;
+  if (s >= S) return;
+  const size_t plane = (size_t)D * S;
+  const double* v = val + row * plane + s;
+  const uint8_t* st = state + row * plane + s;
+  double* ov = out_val + row * plane + s;
+  uint8_t* os = out_state + row * plane + s;
+
+  double w[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) w[k] = 0.0;
+  uint64_t nullm = 0;  // bit k: w[k] is null
+  int cnt = 0;
+  double xb[S2_U];
+  uint8_t sb[S2_U];
+#pragma unroll
+  for (int u = 0; u < S2_U; ++u) {
+    xb[u] = u < D ? v[(size_t)u * S] : 0.0;
+    sb[u] = u < D ? st[(size_t)u * S] : (uint8_t)MFF_STATE_ABSENT;
+  }
+  for (int d0 = 0; d0 < D; d0 += S2_U) {
+    double xc[S2_U];
+    uint8_t sc[S2_U];
+#pragma unroll
+    for (int u = 0; u < S2_U; ++u) {
+      xc[u] = xb[u];
+      sc[u] = sb[u];
+    }
+#pragma unroll
+    for (int u = 0; u < S2_U; ++u) {  // next chunk in flight while this one is processed
+      const int d = d0 + S2_U + u;
+      xb[u] = d < D ? v[(size_t)d * S] : 0.0;
+      sb[u] = d < D ? st[(size_t)d * S] : (uint8_t)MFF_STATE_ABSENT;
+    }
+#pragma unroll
+    for (int u = 0; u < S2_U; ++u) {
+      const int d = d0 + u;
+      if (d >= D) break;
+      const size_t o = (size_t)d * S;
+      const double x = xc[u];
+      const uint8_t sx = sc[u];
+      if (sx == MFF_STATE_ABSENT) {
+        os[o] = MFF_STATE_ABSENT;
+        ov[o] = 0.0;
+        continue;
+      }
+      const bool isnull = sx == MFF_STATE_NULL;
+      if (method == MFF_ROLL_O) {
+        ov[o] = isnull ? 0.0 : x;
+        os[o] = sx;
+        continue;
+      }
+#pragma unroll
+      for (int k = 0; k + 1 < N; ++k) w[k] = w[k + 1];
+      w[N - 1] = isnull ? 0.0 : x;
+      nullm = (nullm >> 1) | ((uint64_t)isnull << (N - 1));
+      cnt = cnt < N ? cnt + 1 : N;
+      if (cnt < N || nullm != 0) {
+        ov[o] = 0.0;
+        os[o] = MFF_STATE_NULL;
+        continue;
+      }
+      const double x0 = __builtin_isfinite(w[0]) ? w[0] : 0.0;
+      double s1 = 0.0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) s1 += w[k] - x0;
+      constexpr double inv_n = 1.0 / (double)N;
+      const double mean = x0 + s1 * inv_n;
+      double s2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        const double dlt = w[k] - mean;
+        s2 += dlt * dlt;
+      }
+      const double sd = sqrt(s2 * inv_n);
+      double res;
+      if (method == MFF_ROLL_M) res = mean;
+      else if (method == MFF_ROLL_STD) res = sd;
+      else res = (x - mean) / sd;
+      ov[o] = res;
+      os[o] = MFF_STATE_VALUE;
+    }
+  }
+}
+
 // Calendar resampling (MF:130-186, mode='calendar'): per (code, calendar window) over the
 // exposure rows of the window — last value ('o'), mean ('m'), (last - mean) / std ('z'),
 // std ('std'), std with ddof=1 (polars default, S1), nulls skipped by mean / std (S9),
@@ -173,6 +273,25 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
   MFF_REQUIRE(N >= 1 && N <= S2_MAXN, "mff_stage2: N=%d outside [1, %d]", N, S2_MAXN);
   MFF_REQUIRE(method >= MFF_ROLL_O && method <= MFF_ROLL_STD, "mff_stage2: unknown method %d", method);
   MFF_REQUIRE(val && state && out_val && out_state, "mff_stage2: NULL buffer");
+  const long long nreg = (long long)rows * ((S + S2_THREADS - 1) / S2_THREADS);
+#define MFF_S2_REG(NN)                                                                                      \
+  case NN:                                                                                                  \
+    hipLaunchKernelGGL(k_stage2_reg<NN>, dim3((unsigned)nreg), dim3(S2_THREADS), 0, as_stream(stream), val, \
+                       state, D, S, method, out_val, out_state);                                            \
+    MFF_LAUNCH_CHECK();                                                                                     \
+    return 0;
+  switch (N) {  // the usual windows: register shift window; other N: the LDS ring below
+    MFF_S2_REG(1)
+    MFF_S2_REG(2)
+    MFF_S2_REG(3)
+    MFF_S2_REG(5)
+    MFF_S2_REG(10)
+    MFF_S2_REG(20)
+    MFF_S2_REG(60)
+    default:
+      break;
+  }
+#undef MFF_S2_REG
   const long long nblk = (long long)rows * ((S + 63) / 64);
   const size_t lds = (size_t)N * 64 * 8;
   hipLaunchKernelGGL(k_stage2, dim3((unsigned)nblk), dim3(64), lds, as_stream(stream), val, state, D, S,

@@ -113,6 +113,102 @@ __global__ __launch_bounds__(256) void k_xs_zscore(const double* val, const uint
   out_state[o] = MFF_STATE_VALUE;
 }
 
+// Single-rank z in one pass: one 256-thread workgroup per (row, day) keeps the day's
+// column in registers (element t + 256 i of thread t, coalesced), so val/state are read
+// once and written once (k_xs_moments + k_xs_zscore read them twice).  Same statistics:
+// x0 = first included value in stock order (0 if not finite), mean shifted by x0, then
+// the squared deviations; block sums through LDS.
+constexpr int XZ_THREADS = 256;
+constexpr int XZ_PER = 32;  // S <= 8192 per day (PER: the smallest instantiation >= S / 256)
+
+__device__ __forceinline__ double xz_block_sum(double x, double* red) {
+  x = wsum(x);
+  const int wave = threadIdx.x >> 6;
+  if (lane_id() == 0) red[wave] = x;
+  __syncthreads();
+  const double t = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return t;
+}
+
+template <int PER>
+__global__ __launch_bounds__(XZ_THREADS) void k_xs_zscore_local(const double* val, const uint8_t* state, int S,
+                                                               double* out_val, uint8_t* out_state) {
+  __shared__ double red[4];
+  __shared__ int first_s;
+  __shared__ double x0_s;
+  const size_t base = (size_t)blockIdx.x * S;
+  const double* v = val + base;
+  const uint8_t* st = state + base;
+  const int t = (int)threadIdx.x;
+  if (t == 0) first_s = 0x7fffffff;
+  double x[PER];
+  uint32_t isval = 0u, isnul = 0u, inc = 0u;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int s = t + i * XZ_THREADS;
+    const bool in = s < S;
+    x[i] = in ? v[s] : 0.0;
+    const uint8_t sx = in ? st[s] : (uint8_t)MFF_STATE_ABSENT;
+    isval |= (uint32_t)(sx == MFF_STATE_VALUE) << i;
+    isnul |= (uint32_t)(sx == MFF_STATE_NULL) << i;
+    inc |= (uint32_t)(sx == MFF_STATE_VALUE && !__builtin_isnan(x[i])) << i;
+  }
+  __syncthreads();
+  if (inc) atomicMin(&first_s, t + __builtin_ctz(inc) * XZ_THREADS);
+  __syncthreads();
+  const int f = first_s;
+  if (f != 0x7fffffff && t == (f & (XZ_THREADS - 1))) {
+    double c = 0.0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      if (i == f / XZ_THREADS) c = x[i];
+    x0_s = __builtin_isfinite(c) ? c : 0.0;
+  }
+  __syncthreads();
+  const double x0 = f != 0x7fffffff ? x0_s : 0.0;
+  double s1 = 0.0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+    if ((inc >> i) & 1u) s1 += x[i] - x0;
+  const double n = xz_block_sum((double)__builtin_popcount(inc), red);
+  s1 = xz_block_sum(s1, red);
+  const double mean = n > 0.0 ? x0 + s1 / n : 0.0;
+  double s2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    if ((inc >> i) & 1u) {
+      const double dl = x[i] - mean;
+      s2 += dl * dl;
+    }
+  }
+  s2 = xz_block_sum(s2, red);
+  const double sd = sqrt(s2 / (n - 1.0));
+  double* ov = out_val + base;
+  uint8_t* os = out_state + base;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int s = t + i * XZ_THREADS;
+    if (s >= S) break;
+    const bool in = (inc >> i) & 1u;
+    const bool vl = (isval >> i) & 1u;
+    uint8_t so;
+    double r;
+    if (!in) {
+      r = vl ? x[i] : 0.0;  // NaN stays NaN
+      so = vl ? MFF_STATE_VALUE : (((isnul >> i) & 1u) ? MFF_STATE_NULL : MFF_STATE_ABSENT);
+    } else if (n < 2.0) {
+      r = 0.0;
+      so = MFF_STATE_NULL;
+    } else {
+      r = (x[i] - mean) / sd;
+      so = MFF_STATE_VALUE;
+    }
+    ov[s] = r;
+    os[s] = so;
+  }
+}
+
 struct XsLoader {
   const double* v;   // [R][rows][D][S_loc]
   const uint8_t* st;
@@ -206,6 +302,26 @@ int mff_xs_zscore(const double* val, const uint8_t* state, int rows, int D, int 
   }
   return 0;
 }
+
+int mff_xs_zscore_local(const double* val, const uint8_t* state, int rows, int D, int S, double* out_val,
+                        uint8_t* out_state, void* stream) {
+  clear_error();
+  MFF_REQUIRE(rows > 0 && D > 0 && S > 0 && S <= XZ_THREADS * XZ_PER,
+              "mff_xs_zscore_local: bad sizes rows=%d D=%d S=%d (S <= %d)", rows, D, S, XZ_THREADS * XZ_PER);
+  MFF_REQUIRE(val && state && out_val && out_state, "mff_xs_zscore_local: NULL buffer");
+  const long long nseg = (long long)rows * D;
+  MFF_REQUIRE(nseg < (1ll << 31), "mff_xs_zscore_local: too many segments");
+  const int per = (S + XZ_THREADS - 1) / XZ_THREADS;
+  auto kern = per <= 4 ? k_xs_zscore_local<4> : per <= 8 ? k_xs_zscore_local<8> : per <= 12 ? k_xs_zscore_local<12>
+            : per <= 16 ? k_xs_zscore_local<16> : per <= 20 ? k_xs_zscore_local<20> : per <= 24 ? k_xs_zscore_local<24>
+            : k_xs_zscore_local<32>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nseg), dim3(XZ_THREADS), 0, as_stream(stream), val, state, S, out_val,
+                     out_state);
+  MFF_LAUNCH_CHECK();
+  return 0;
+}
+
+int mff_xs_zscore_local_max_stocks(void) { return XZ_THREADS * XZ_PER; }
 
 size_t mff_xs_rank_workspace_bytes(int rows, int D, int S_all, int R) {
   const long long nseg = (long long)rows * D;

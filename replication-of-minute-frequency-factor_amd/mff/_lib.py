@@ -40,6 +40,8 @@ SIGNATURES = {
     "mff_calendar": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, P]),
     "mff_xs_moments": (c_int, [P, P, c_int, c_int, c_int, P, P]),
     "mff_xs_zscore": (c_int, [P, P, c_int, c_int, c_int, P, c_int, P, P, P]),
+    "mff_xs_zscore_local": (c_int, [P, P, c_int, c_int, c_int, P, P, P]),
+    "mff_xs_zscore_local_max_stocks": (c_int, []),
     "mff_xs_rank_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "mff_xs_rank": (c_int, [P, P, c_int, c_int, c_int, P, P, c_int, c_int, P, P, P, P]),
     "mff_future_return": (c_int, [P, P, c_int, c_int, c_int, P, P, P]),

@@ -258,7 +258,10 @@ def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None):
     ov = torch.empty_like(val)
     os_ = torch.empty_like(state)
     R = 1 if comm is None else comm.world_size
-    if kind == "z":
+    if kind == "z" and R == 1 and S <= lib.mff_xs_zscore_local_max_stocks():
+        _lib.check(lib.mff_xs_zscore_local(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(ov),
+                                           _lib.ptr(os_), st), "mff_xs_zscore_local")
+    elif kind == "z":
         mom = torch.empty((rows, D, 3), dtype=torch.float64, device=dev)
         _lib.check(lib.mff_xs_moments(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(mom), st),
                    "mff_xs_moments")

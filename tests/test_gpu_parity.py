@@ -176,11 +176,12 @@ def _random_long_panel(D, S, seed):
     return val, state
 
 
-@pytest.mark.parametrize("N", [1, 5, 20])
+@pytest.mark.parametrize("N", [1, 5, 7, 20, 60])
 def test_stage2_live(dev, N):
+    """N in {1, 2, 3, 5, 10, 20, 60}: register shift window (k_stage2_reg); 7: LDS ring."""
     import mff_oracle as O
     from mff import engine
-    val, state = _random_long_panel(70, 130, N)
+    val, state = _random_long_panel(150 if N > 20 else 70, 130, N)
     bad = []
     for meth in ("o", "m", "z", "std"):
         ov, os_ = O.oracle_stage2(val, state, N, meth)
@@ -192,8 +193,9 @@ def test_stage2_live(dev, N):
 
 
 @pytest.mark.parametrize("kind", ["z", "rank"])
-@pytest.mark.parametrize("S", [130, 9000])
+@pytest.mark.parametrize("S", [130, 5000, 9000])
 def test_stage3_live(dev, kind, S):
+    """z: S <= 8192 runs the one-pass k_xs_zscore_local, 9000 moments + zscore."""
     import mff_oracle as O
     from mff import engine
     val, state = _random_long_panel(6, S, 3)
