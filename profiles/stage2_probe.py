@@ -39,6 +39,10 @@ def main():
     for N, meth in [(20, "o"), (20, "m"), (20, "z"), (20, "std"), (5, "z"), (60, "z"), (7, "z")]:
         res[f"stage2_N{N}_{meth}"] = t(lambda: engine.rolling(val, state, N, meth))
     res["stage3_z"] = t(lambda: engine.cross_section(val, state, "z"))
+    nb = nbytes
+    nbytes = nb * 8 / 58
+    res["stage3_rank_8factors"] = t(lambda: engine.cross_section(val[:8], state[:8], "rank"))
+    nbytes = nb
     print(json.dumps(res), flush=True)
 
 

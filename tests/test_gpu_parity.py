@@ -193,7 +193,7 @@ def test_stage2_live(dev, N):
 
 
 @pytest.mark.parametrize("kind", ["z", "rank"])
-@pytest.mark.parametrize("S", [130, 5000, 9000])
+@pytest.mark.parametrize("S", [130, 3000, 5000, 9000])
 def test_stage3_live(dev, kind, S):
     """z: S <= 8192 runs the one-pass k_xs_zscore_local, 9000 moments + zscore."""
     import mff_oracle as O
