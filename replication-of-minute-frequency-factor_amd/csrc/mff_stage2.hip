@@ -121,14 +121,21 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
   for (int k = 0; k < N; ++k) w[k] = 0.0;
   uint64_t nullm = 0;  // bit k: w[k] is null
   int cnt = 0;
-  double xb[S2_U];
+  // Stores are deferred by one chunk and issued together, before the next chunk's loads:
+  // gfx9 counts stores in vmcnt, so the wait for a chunk's loads also waits for every
+  // store issued before them -- issued a whole chunk earlier, they are long complete.
+  const int Dm = D - D % S2_U;  // whole chunks; the last D % S2_U days after the loop
+  double xb[S2_U], rp[S2_U];
   uint8_t sb[S2_U];
+  uint32_t sp = 0u;  // the deferred chunk's states, one byte per day
 #pragma unroll
   for (int u = 0; u < S2_U; ++u) {
-    xb[u] = u < D ? v[(size_t)u * S] : 0.0;
-    sb[u] = u < D ? st[(size_t)u * S] : (uint8_t)MFF_STATE_ABSENT;
+    const int d = min(u, D - 1);
+    xb[u] = v[(size_t)d * S];
+    sb[u] = st[(size_t)d * S];
+    rp[u] = 0.0;
   }
-  for (int d0 = 0; d0 < D; d0 += S2_U) {
+  for (int d0 = 0; d0 < Dm; d0 += S2_U) {
     double xc[S2_U];
     uint8_t sc[S2_U];
 #pragma unroll
@@ -136,28 +143,31 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
       xc[u] = xb[u];
       sc[u] = sb[u];
     }
+    if (d0 > 0) {
 #pragma unroll
-    for (int u = 0; u < S2_U; ++u) {  // next chunk in flight while this one is processed
-      const int d = d0 + S2_U + u;
-      xb[u] = d < D ? v[(size_t)d * S] : 0.0;
-      sb[u] = d < D ? st[(size_t)d * S] : (uint8_t)MFF_STATE_ABSENT;
+      for (int u = 0; u < S2_U; ++u) {
+        const size_t o = (size_t)(d0 - S2_U + u) * S;
+        ov[o] = rp[u];
+        os[o] = (uint8_t)(sp >> (8 * u));
+      }
     }
 #pragma unroll
+    for (int u = 0; u < S2_U; ++u) {  // next chunk in flight while this one is processed
+      const int d = min(d0 + S2_U + u, D - 1);
+      xb[u] = v[(size_t)d * S];
+      sb[u] = st[(size_t)d * S];
+    }
+    sp = 0u;
+#pragma unroll
     for (int u = 0; u < S2_U; ++u) {
-      const int d = d0 + u;
-      if (d >= D) break;
-      const size_t o = (size_t)d * S;
       const double x = xc[u];
       const uint8_t sx = sc[u];
-      if (sx == MFF_STATE_ABSENT) {
-        os[o] = MFF_STATE_ABSENT;
-        ov[o] = 0.0;
-        continue;
-      }
+      rp[u] = 0.0;
+      if (sx == MFF_STATE_ABSENT) continue;  // state byte 0
       const bool isnull = sx == MFF_STATE_NULL;
       if (method == MFF_ROLL_O) {
-        ov[o] = isnull ? 0.0 : x;
-        os[o] = sx;
+        rp[u] = isnull ? 0.0 : x;
+        sp |= (uint32_t)sx << (8 * u);
         continue;
       }
 #pragma unroll
@@ -166,8 +176,7 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
       nullm = (nullm >> 1) | ((uint64_t)isnull << (N - 1));
       cnt = cnt < N ? cnt + 1 : N;
       if (cnt < N || nullm != 0) {
-        ov[o] = 0.0;
-        os[o] = MFF_STATE_NULL;
+        sp |= (uint32_t)MFF_STATE_NULL << (8 * u);
         continue;
       }
       const double x0 = __builtin_isfinite(w[0]) ? w[0] : 0.0;
@@ -187,9 +196,57 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
       if (method == MFF_ROLL_M) res = mean;
       else if (method == MFF_ROLL_STD) res = sd;
       else res = (x - mean) / sd;
-      ov[o] = res;
-      os[o] = MFF_STATE_VALUE;
+      rp[u] = res;
+      sp |= (uint32_t)MFF_STATE_VALUE << (8 * u);
     }
+  }
+  if (Dm > 0) {
+#pragma unroll
+    for (int u = 0; u < S2_U; ++u) {
+      const size_t o = (size_t)(Dm - S2_U + u) * S;
+      ov[o] = rp[u];
+      os[o] = (uint8_t)(sp >> (8 * u));
+    }
+  }
+  for (int d = Dm; d < D; ++d) {  // the last D % S2_U days, one at a time
+    const size_t o = (size_t)d * S;
+    const double x = v[o];
+    const uint8_t sx = st[o];
+    double res = 0.0;
+    uint8_t so = MFF_STATE_ABSENT;
+    if (sx != MFF_STATE_ABSENT) {
+      const bool isnull = sx == MFF_STATE_NULL;
+      if (method == MFF_ROLL_O) {
+        res = isnull ? 0.0 : x;
+        so = sx;
+      } else {
+#pragma unroll
+        for (int k = 0; k + 1 < N; ++k) w[k] = w[k + 1];
+        w[N - 1] = isnull ? 0.0 : x;
+        nullm = (nullm >> 1) | ((uint64_t)isnull << (N - 1));
+        cnt = cnt < N ? cnt + 1 : N;
+        so = MFF_STATE_NULL;
+        if (cnt >= N && nullm == 0) {
+          const double x0 = __builtin_isfinite(w[0]) ? w[0] : 0.0;
+          double s1 = 0.0;
+#pragma unroll
+          for (int k = 0; k < N; ++k) s1 += w[k] - x0;
+          constexpr double inv_n = 1.0 / (double)N;
+          const double mean = x0 + s1 * inv_n;
+          double s2 = 0.0;
+#pragma unroll
+          for (int k = 0; k < N; ++k) {
+            const double dlt = w[k] - mean;
+            s2 += dlt * dlt;
+          }
+          const double sd = sqrt(s2 * inv_n);
+          res = method == MFF_ROLL_M ? mean : method == MFF_ROLL_STD ? sd : (x - mean) / sd;
+          so = MFF_STATE_VALUE;
+        }
+      }
+    }
+    ov[o] = res;
+    os[o] = so;
   }
 }
 
