@@ -43,24 +43,29 @@ __global__ __launch_bounds__(64) void k_stage2(const double* val, const uint8_t*
     xn = v[s];
     sn = st[s];
   }
+  if (!act) return;
+  // each day's result is stored one day later, just before the next prefetch (stores
+  // count in vmcnt: a fresh store ahead of the wait for the next load would be waited on)
+  double rprev = 0.0;
+  uint8_t sprev = MFF_STATE_ABSENT;
   for (int d = 0; d < D; ++d) {
     const double x = xn;
     const uint8_t sx = sn;
-    if (act && d + 1 < D) {  // prefetch next day
+    if (d > 0) {
+      const size_t op = (size_t)(d - 1) * S + s;
+      ov[op] = rprev;
+      os[op] = sprev;
+    }
+    if (d + 1 < D) {  // prefetch next day
       xn = v[(size_t)(d + 1) * S + s];
       sn = st[(size_t)(d + 1) * S + s];
     }
-    if (!act) continue;
-    const size_t o = (size_t)d * S + s;
-    if (sx == MFF_STATE_ABSENT) {
-      os[o] = MFF_STATE_ABSENT;
-      ov[o] = 0.0;
-      continue;
-    }
+    rprev = 0.0;
+    sprev = sx;
+    if (sx == MFF_STATE_ABSENT) continue;
     const bool isnull = sx == MFF_STATE_NULL;
     if (method == MFF_ROLL_O) {
-      ov[o] = isnull ? 0.0 : x;
-      os[o] = sx;
+      rprev = isnull ? 0.0 : x;
       continue;
     }
     ring[pos * 64 + lane] = isnull ? 0.0 : x;
@@ -69,8 +74,7 @@ __global__ __launch_bounds__(64) void k_stage2(const double* val, const uint8_t*
     pos = oldest;
     ++cnt;
     if (cnt < N || nullm != 0) {
-      ov[o] = 0.0;
-      os[o] = MFF_STATE_NULL;
+      sprev = MFF_STATE_NULL;
       continue;
     }
     double x0 = ring[oldest * 64 + lane];
@@ -88,9 +92,12 @@ __global__ __launch_bounds__(64) void k_stage2(const double* val, const uint8_t*
     if (method == MFF_ROLL_M) res = mean;
     else if (method == MFF_ROLL_STD) res = sd;
     else res = (x - mean) / sd;  // MFF_ROLL_Z, x not null here
-    ov[o] = res;
-    os[o] = MFF_STATE_VALUE;
+    rprev = res;
+    sprev = MFF_STATE_VALUE;
   }
+  const size_t ol = (size_t)(D - 1) * S + s;
+  ov[ol] = rprev;
+  os[ol] = sprev;
 }
 
 // Register-window variant for the common window lengths (N a template constant): the
