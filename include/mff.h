@@ -124,13 +124,22 @@ int mff_stage1(const float* open, const float* high, const float* low,
  * out over all D days.
  *   sort:     queries of R ranks, float64 [R][5][D][S_all] (NaN = none; each rank's
  *             [5][D][S_loc] padded to S_all with NaN)
- *             -> q_sorted uint64 [nd][M], M = R*5*S_all <= 32767 (total-order keys)
+ *             -> q_sorted uint64 [nd][M], M = R*5*S_all (total-order keys; any M: beyond
+ *             32768 per day the sort finishes with global merge passes)
  *   count:    this rank's keys c_last/c_b (from stage 1's pdf_levels: one key per
  *             distinct close of a stock-day, weighted by its bar count) against q_sorted
  *             -> counts uint32 [nd][M] = 2 n_less + n_eq over local keys (the
  *             average rank n_less + (n_eq + 1) / 2 is linear in it)
- *   [R > 1: the caller sums `counts` over ranks (all-reduce), see INTEGRATION.md]
- *   finalize: own queries [5][D][S_loc] -> val/state rows pdf_rows[5] (host, -1 = skip)
+ *   [R > 1: the caller sums `counts` over ranks (reduce-scatter to each day's owner, or
+ *    an all-reduce), see INTEGRATION.md]
+ *   finalize: own queries [5][D][S_loc] -> val/state rows pdf_rows[5] (host, -1 = skip),
+ *             looking each query up in the day's sorted list and the summed counts
+ *   origin_counts: day-owner side of the reduce-scatter exchange: the summed counts of
+ *             the owned days at each query of q_all [R][5][D][S_all] (days [d0, d0+nd)),
+ *             written in that origin layout -> out uint32 [R][5][nd][S_all] (0 for NaN);
+ *             one all_to_all then hands every rank its own queries' counts
+ *   finalize_own: own queries [5][D][S_loc] with their counts in the same layout
+ *             (2 n_less + n_eq summed over ranks) -> val/state (rank (c + 1) / 2)
  *   rank_local: count + finalize in one pass, for a single rank (R = 1: no exchange)
  * workspace: mff_pdf_workspace_bytes(S_loc, R, nd) bytes of device scratch (sort).
  */
@@ -144,6 +153,12 @@ int mff_pdf_finalize(const double* q_local, const uint64_t* q_sorted,
                      const uint32_t* counts, int S_loc, int D, int d0, int nd, int M,
                      const int32_t* pdf_rows /* host, 5 entries, -1 = skip */,
                      double* val, uint8_t* state, void* stream);
+int mff_pdf_origin_counts(const double* q_all, int R, int S_all, int D, int d0, int nd,
+                          const uint64_t* q_sorted, const uint32_t* counts, int M, uint32_t* out,
+                          void* stream);
+int mff_pdf_finalize_own(const double* q_local, const uint32_t* own_counts, int S_loc, int D,
+                         const int32_t* pdf_rows /* host, 5 entries, -1 = skip */, double* val,
+                         uint8_t* state, void* stream);
 int mff_pdf_rank_local(const void* pdf_levels, const double* q_local,
                        int S, int D, int d0, int nd, const uint64_t* q_sorted, int M,
                        const int32_t* pdf_rows /* host, 5 entries */, double* val,
@@ -153,7 +168,7 @@ int mff_pdf_rank_local(const void* pdf_levels, const double* q_local,
  * Stage 2: N-day rolling post-processing over present days, per stock.
  * Replaces: MinFreqFactor.cal_final_exposure(frequency=N, method, mode='days')
  * (MinuteFrequentFactorCICC.py:187-240).  rows = number of factor rows.
- * Requires 1 <= N <= 64.
+ * Any N >= 1, like the reference's `frequency: int` (MF:188-189, 205).
  */
 int mff_stage2(const double* val, const uint8_t* state, int rows, int D, int S,
                int N, int method, double* out_val, uint8_t* out_state, void* stream);
@@ -199,7 +214,7 @@ int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_
  * mff_future_return: Factor.py:142-162 — per stock over its present days,
  *   fut = exp(sum of log(1 + pct) over the next N present days) - 1, NULL unless N such
  *   days exist with no null among them (rolling_sum min_samples=N, then shift(-N)).
- *   Requires 1 <= N <= 64.
+ *   Any N >= 1 (Factor.py:149 takes any future_days).
  * mff_ic_pairs: the pair set of pl.corr (Factor.py:165-183): x VALUE and not NaN (the
  *   is_nan filter), y VALUE; writes [2][D][S] rows (x, y) with state VALUE on pairs, else
  *   ABSENT.  Feed them to mff_ic_moments (IC) or first to mff_xs_rank (rank IC).

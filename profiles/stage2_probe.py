@@ -36,8 +36,13 @@ def main():
         ms = a.elapsed_time(b) / reps
         return round(ms, 3), round(nbytes / (ms * 1e-3) / 1e9, 1)
 
-    for N, meth in [(20, "o"), (20, "m"), (20, "z"), (20, "std"), (5, "z"), (60, "z"), (7, "z")]:
+    for N, meth in [(20, "o"), (20, "m"), (20, "z"), (20, "std"), (5, "z"), (60, "z"), (7, "z"),
+                    (120, "z"), (250, "z")]:
         res[f"stage2_N{N}_{meth}"] = t(lambda: engine.rolling(val, state, N, meth))
+    os.environ["MFF_STAGE2_IMPL"] = "slide"
+    for N, meth in [(20, "m"), (20, "z"), (20, "std"), (5, "z"), (60, "z")]:
+        res[f"stage2_slide_N{N}_{meth}"] = t(lambda: engine.rolling(val, state, N, meth))
+    del os.environ["MFF_STAGE2_IMPL"]
     res["stage3_z"] = t(lambda: engine.cross_section(val, state, "z"))
     nb = nbytes
     nbytes = nb * 8 / 58

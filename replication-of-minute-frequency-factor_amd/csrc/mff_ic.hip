@@ -9,9 +9,10 @@
 //
 // Dense form: pct / exposure are [D][S] (val f64, state u8) with rows only for present
 // stock-days, so "over(code)" walks the present days of a stock in date order.
-//   k_future_return  lane = stock, days walked backwards with an LDS ring of the next N
-//                    present rows' log(1+pct): fut(r) = exp(sum of rows r+1..r+N) - 1, NULL
-//                    unless N further rows exist and none is null (min_samples=N).
+//   k_future_return  lane = stock, days walked backwards with a double-double sliding sum
+//                    of the next N present rows' log(1+pct): fut(r) = exp(sum of rows
+//                    r+1..r+N) - 1, NULL unless N further rows exist and none is null
+//                    (min_samples=N); any N >= 1.
 //   k_ic_pairs       the pair set of pl.corr: x VALUE and not NaN, fut VALUE (NaN kept, it
 //                    poisons the date as in polars); both rows written [2][D][S].
 //   k_ic_moments     wave per day: (n, mean_x, mean_y, Cxx, Cyy, Cxy) by two passes over the
@@ -20,45 +21,69 @@
 //                    Cxy / sqrt(Cxx Cyy); n < 2 or zero denominator -> NaN (S3).
 // rank_IC = the same moments over the pair set's average ranks (mff_xs_rank, S6).
 #include "../../include/mff.h"
+#include "mff_dd.h"
 #include "mff_internal.h"
 #include "mff_wave.h"
 
 namespace mff {
 
-constexpr int FR_MAXN = 64;
-
-__global__ __launch_bounds__(64) void k_future_return(const double* pct, const uint8_t* state, int D, int S,
-                                                       int N, double* out, uint8_t* out_state) {
-  __shared__ double ring[FR_MAXN][64];  // [slot][lane]: bank = lane
-  const int lane = lane_id();
-  const int s = blockIdx.x * 64 + lane;
-  const bool act = s < S;
-  int cnt = 0, pos = 0;      // rows held (<= N), next slot to write
-  uint64_t nullm = 0;        // slot holds a null
+// lane = stock, days walked backwards; the window = the next N present rows after the
+// current one, kept as a double-double sliding sum of log(1 + pct) (mff_dd.h) with
+// counts of nulls, NaN, +inf, -inf; the row leaving the window (the farthest, at the
+// `lead` day) is re-read.  Any N >= 1.
+__global__ __launch_bounds__(256) void k_future_return(const double* pct, const uint8_t* state, int D, int S,
+                                                        int N, double* out, uint8_t* out_state) {
+  const int s = blockIdx.x * 256 + (int)threadIdx.x;
+  if (s >= S) return;
+  auto lg = [&](int d) { return log(pct[(size_t)d * S + s] + 1.0); };
+  auto ST = [&](int d) { return state[(size_t)d * S + s]; };
+  int cnt = 0, lead = 0, nnull = 0, nnan = 0, npi = 0, nni = 0;
+  DD sum{0.0, 0.0};
   for (int d = D - 1; d >= 0; --d) {
-    if (!act) continue;
     const size_t i = (size_t)d * S + s;
-    const uint8_t st = state[i];
+    const uint8_t st = ST(d);
     if (st == MFF_STATE_ABSENT) {
       out_state[i] = MFF_STATE_ABSENT;
       out[i] = 0.0;
       continue;
     }
-    // window = the next N present rows, summed in date order (nearest first)
-    if (cnt == N && nullm == 0) {
-      double sum = 0.0;
-      for (int k = 1; k <= N; ++k) sum += ring[(pos - k + N) % N][lane];
-      out[i] = exp(sum) - 1.0;
+    if (cnt == N && nnull == 0) {
+      double sm;
+      if (nnan > 0 || (npi > 0 && nni > 0)) sm = qnan();
+      else if (npi > 0) sm = __builtin_inf();
+      else if (nni > 0) sm = -__builtin_inf();
+      else sm = sum.hi + sum.lo;
+      out[i] = exp(sm) - 1.0;
       out_state[i] = MFF_STATE_VALUE;
     } else {
       out[i] = 0.0;
       out_state[i] = MFF_STATE_NULL;
     }
-    const bool isnull = st != MFF_STATE_VALUE;
-    ring[pos][lane] = isnull ? 0.0 : log(pct[i] + 1.0);
-    nullm = isnull ? (nullm | (1ull << pos)) : (nullm & ~(1ull << pos));
-    pos = pos + 1 == N ? 0 : pos + 1;
-    cnt = cnt < N ? cnt + 1 : N;
+    // row d enters; with N rows held, the farthest leaves
+    if (cnt == N) {
+      if (ST(lead) != MFF_STATE_VALUE) {
+        --nnull;
+      } else {
+        const double y = lg(lead);
+        if (__builtin_isnan(y)) --nnan;
+        else if (y == __builtin_inf()) --npi;
+        else if (y == -__builtin_inf()) --nni;
+        else sum = dd_add(sum, -y);
+      }
+      do { --lead; } while (ST(lead) == MFF_STATE_ABSENT);
+    } else {
+      if (cnt == 0) lead = d;
+      ++cnt;
+    }
+    if (st != MFF_STATE_VALUE) {
+      ++nnull;
+    } else {
+      const double y = lg(d);
+      if (__builtin_isnan(y)) ++nnan;
+      else if (y == __builtin_inf()) ++npi;
+      else if (y == -__builtin_inf()) ++nni;
+      else sum = dd_add(sum, y);
+    }
   }
 }
 
@@ -161,9 +186,9 @@ int mff_future_return(const double* pct, const uint8_t* state, int D, int S, int
   using namespace mff;
   clear_error();
   MFF_REQUIRE(D > 0 && S > 0, "mff_future_return: bad sizes D=%d S=%d", D, S);
-  MFF_REQUIRE(N >= 1 && N <= FR_MAXN, "mff_future_return: N=%d outside [1, %d]", N, FR_MAXN);
+  MFF_REQUIRE(N >= 1, "mff_future_return: N=%d < 1", N);
   MFF_REQUIRE(pct && state && out_val && out_state, "mff_future_return: null pointer");
-  hipLaunchKernelGGL(k_future_return, dim3((S + 63) / 64), dim3(64), 0, as_stream(stream), pct, state, D,
+  hipLaunchKernelGGL(k_future_return, dim3((S + 255) / 256), dim3(256), 0, as_stream(stream), pct, state, D,
                      S, N, out_val, out_state);
   MFF_LAUNCH_CHECK();
   return 0;

@@ -30,7 +30,7 @@ namespace mff {
 
 size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w);  // mff_stage1g.hip
 
-constexpr int PDF_MAXM = 32767;  // queries per day (all ranks)
+constexpr int PDF_MAXM = 1 << 24;  // queries per day (all ranks): 2 n_less + n_eq stays in u32
 constexpr int PDF_ZQ = 9160;     // sorted queries per count workgroup (LDS: 16 B each)
 constexpr int PDF_PAD = 64;      // ~0 sentinels after the slice's distinct values
 constexpr int PDF_NBK = 8192;    // bucket table over the workgroup's distinct query values
@@ -220,6 +220,10 @@ __device__ __forceinline__ void pdf_slice_resolve(const PdfSlice& sl, const uint
   }
 }
 
+struct Rows5 {
+  int r[5];
+};
+
 struct PdfArgs {
   // level side channel written by stage 1 (mff_pdf_levels_bytes): per-day entry counts,
   // flat key / weight lists of capacity `cap` per day
@@ -390,6 +394,46 @@ __global__ __launch_bounds__(1024) void k_pdf_finalize(PdfArgs a) {
   pdf_slice_resolve(sl, C, a.q_local, a.S, a.D, d, a.rows, a.val, a.state);
 }
 
+// multi-rank, day-owner side: the counts of day d's sorted list (summed over ranks) at
+// each query's first sorted position, written in the queries' origin layout
+// [R][5][nd][S_all] (the all_to_all receive buffer of mff_pdf_sort), so one all_to_all
+// returns every rank the counts of its own queries.  Thread per query, binary search
+// over the day's sorted list (L2-resident).
+__global__ __launch_bounds__(256) void k_pdf_origin(const double* q_all, int RT, int S, int D, int d0, int nd,
+                                                     const uint64_t* q_sorted, const uint32_t* counts, int M,
+                                                     uint32_t* out) {
+  const size_t n = (size_t)RT * nd * S;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int s = (int)(i % S);
+  const size_t rd = i / S;
+  const int dd = (int)(rd % nd);
+  const int rt = (int)(rd / nd);
+  const double x = q_all[((size_t)rt * D + d0 + dd) * S + s];
+  uint32_t c = 0u;
+  if (!__builtin_isnan(x)) {
+    const uint64_t* Q = q_sorted + (size_t)dd * M;
+    const int j = lower_bound_u64(Q, 0, M, ord64(x));
+    c = counts[(size_t)dd * M + j];
+  }
+  out[i] = c;
+}
+
+// own queries [5][D][S] with their counts in the same layout (2 n_less + n_eq summed over
+// ranks) -> average rank (c + 1) / 2 (S6); NaN queries keep stage 1's null / absent
+__global__ __launch_bounds__(256) void k_pdf_finalize_own(const double* q, const uint32_t* cnt, int S, int D,
+                                                           Rows5 rows, double* val, uint8_t* state) {
+  const size_t plane = (size_t)D * S;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= 5 * plane) return;
+  const int t = (int)(i / plane);
+  const size_t j = i - (size_t)t * plane;
+  if (rows.r[t] < 0 || __builtin_isnan(q[i])) return;
+  const size_t o = (size_t)rows.r[t] * plane + j;
+  val[o] = ((double)cnt[i] + 1.0) * 0.5;
+  state[o] = MFF_STATE_VALUE;
+}
+
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace mff
@@ -482,6 +526,34 @@ int mff_pdf_finalize(const double* q_local, const uint64_t* q_sorted, const uint
   for (int t = 0; t < 5; ++t) a.rows[t] = pdf_rows[t];
   a.S = S_loc; a.D = D; a.d0 = d0; a.nd = nd;
   return pdf_launch(a, q_sorted, M, as_stream(stream), 2);
+}
+
+int mff_pdf_origin_counts(const double* q_all, int R, int S_all, int D, int d0, int nd,
+                          const uint64_t* q_sorted, const uint32_t* counts, int M, uint32_t* out,
+                          void* stream) {
+  clear_error();
+  MFF_REQUIRE(R >= 1 && S_all > 0 && D > 0 && nd > 0 && d0 >= 0 && d0 + nd <= D && M == R * 5 * S_all,
+              "mff_pdf_origin_counts: bad sizes R=%d S=%d D=%d d0=%d nd=%d M=%d", R, S_all, D, d0, nd, M);
+  MFF_REQUIRE(q_all && q_sorted && counts && out, "mff_pdf_origin_counts: NULL buffer");
+  const size_t n = (size_t)R * 5 * nd * S_all;
+  hipLaunchKernelGGL(k_pdf_origin, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), q_all,
+                     R * 5, S_all, D, d0, nd, q_sorted, counts, M, out);
+  MFF_LAUNCH_CHECK();
+  return 0;
+}
+
+int mff_pdf_finalize_own(const double* q_local, const uint32_t* own_counts, int S_loc, int D,
+                         const int32_t* pdf_rows, double* val, uint8_t* state, void* stream) {
+  clear_error();
+  MFF_REQUIRE(S_loc > 0 && D > 0, "mff_pdf_finalize_own: bad sizes S=%d D=%d", S_loc, D);
+  MFF_REQUIRE(q_local && own_counts && pdf_rows && val && state, "mff_pdf_finalize_own: NULL buffer");
+  Rows5 rows;
+  for (int t = 0; t < 5; ++t) rows.r[t] = pdf_rows[t];
+  const size_t n = (size_t)5 * D * S_loc;
+  hipLaunchKernelGGL(k_pdf_finalize_own, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     q_local, own_counts, S_loc, D, rows, val, state);
+  MFF_LAUNCH_CHECK();
+  return 0;
 }
 
 int mff_pdf_rank_local(const void* pdf_levels, const double* q_local, int S, int D,

@@ -5,107 +5,180 @@
 // min_samples=N (S13).  Rows exist only for present stock-days, so ABSENT days are
 // skipped, not counted; a window holding a null has < N samples -> null.
 //
-// Layout: one wavefront per (factor row, 64 consecutive stocks); lane = stock, loop
-// over days reading val[row][d][s0..s0+63] (512 coalesced bytes per day).  Each lane
-// keeps its last N present values in an LDS ring [N][64] (bank = lane, conflict-free)
-// and a 64-bit null mask, and recomputes the window from scratch each present day:
-// mean = x0 + sum(x - x0)/N (x0 = oldest value when finite, C3), var = sum((x-mean)^2)/N.
-// From scratch (not a sliding sum) so NaN/inf affect only the windows holding them,
-// and a constant window gives std exactly 0 (C6: z = 0/0 = NaN).
+// Layout: lane = stock, loop over days reading val[row][d][s..] (coalesced across the
+// lanes).  Two kernels:
+//  * k_stage2_reg<N> (N in {1, 2, 3, 5, 10, 20, 60}): the last N present values in VGPRs,
+//    each window recomputed from scratch by two passes (x0-shifted mean, squared
+//    deviations);
+//  * k_stage2_slide (any N >= 1): double-double sliding sums with exact constant-window
+//    detection and in-window null / NaN / inf counts.
+// Both give: NaN/inf affect only the windows holding them, and a constant window has std
+// exactly 0 (C6: z = 0/0 = NaN).
+#include <stdlib.h>
+
 #include "../../include/mff.h"
+#include "mff_dd.h"
 #include "mff_internal.h"
 #include "mff_wave.h"
 
 namespace mff {
 
-constexpr int S2_MAXN = 64;
+// Sliding variant for any window length N (every N without a register template): one
+// add and one remove per present row instead of an O(N) recompute.  Lane = stock, loop
+// over days; the row leaving the window is re-read from HBM / cache at the `lag` cursor
+// (the day of the window's oldest row; it advances over absent days).  Window state:
+//  * S1 = sum (x - c), S2 = sum (x - c)^2 over the window's finite non-null values as
+//    double-doubles (mff_dd.h), c = the first finite value entering an empty window; a
+//    value leaves with the same shifted image it entered with, so it cancels exactly
+//  * counts of nulls (min_samples=N: any null -> null), NaN, +inf, -inf in the window:
+//    a window holding a non-finite value has mean NaN / +-inf and std NaN, as the
+//    from-scratch two-pass gives (so NaN/inf affect only the windows holding them)
+//  * the present-row index of the last change (a row that is null, non-finite or differs
+//    from the row before): a window without one has identical values, std exactly 0 and
+//    mean exactly the value (C6: z = 0/0 = NaN)
+// If removing a row cancels S2 by more than 2^-30 (an outlier left the window), the
+// sums are rebuilt from the window's rows with a fresh shift, so the outlier's rounding
+// residue cannot swamp the remaining values.
+constexpr int S2_SLIDE_THREADS = 256;
 
-__global__ __launch_bounds__(64) void k_stage2(const double* val, const uint8_t* state, int D, int S, int N,
-                                                int method, double* out_val, uint8_t* out_state) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* ring = reinterpret_cast<double*>(smem);  // [N][64]
-  const int nsb = (S + 63) / 64;
+__global__ __launch_bounds__(S2_SLIDE_THREADS) void k_stage2_slide(const double* val, const uint8_t* state, int D,
+                                                                   int S, int N, int method, double* out_val,
+                                                                   uint8_t* out_state) {
+  const int nsb = (S + S2_SLIDE_THREADS - 1) / S2_SLIDE_THREADS;
   const int row = blockIdx.x / nsb;
-  const int s = (blockIdx.x % nsb) * 64 + lane_id();
-  const bool act = s < S;
+  const int s = (blockIdx.x % nsb) * S2_SLIDE_THREADS + (int)threadIdx.x;
+  if (s >= S) return;
   const size_t plane = (size_t)D * S;
-  const double* v = val + row * plane;
-  const uint8_t* st = state + row * plane;
-  double* ov = out_val + row * plane;
-  uint8_t* os = out_state + row * plane;
-  const int lane = lane_id();
+  const double* v = val + row * plane + s;
+  const uint8_t* st = state + row * plane + s;
+  double* ov = out_val + row * plane + s;
+  uint8_t* os = out_state + row * plane + s;
+  auto X = [&](int d) { return v[(size_t)d * S]; };
+  auto ST = [&](int d) { return st[(size_t)d * S]; };
 
-  int cnt = 0, pos = 0;
-  uint64_t nullm = 0;
-  double xn = 0.0;
-  uint8_t sn = MFF_STATE_ABSENT;
-  if (act) {
-    xn = v[s];
-    sn = st[s];
-  }
-  if (!act) return;
-  // each day's result is stored one day later, just before the next prefetch (stores
-  // count in vmcnt: a fresh store ahead of the wait for the next load would be waited on)
-  double rprev = 0.0;
-  uint8_t sprev = MFF_STATE_ABSENT;
+  int cnt = 0, lag = 0;                        // rows in the window, day of its oldest row
+  int nnull = 0, nnan = 0, npi = 0, nni = 0, nfin = 0;
+  int k = 0, lastchg = 0;                      // present-row index, last change
+  double prev = 0.0, c = 0.0;
+  bool prevok = false;
+  DD S1{0.0, 0.0}, S2{0.0, 0.0};
+  auto rebuild = [&](int upto) {  // sums over the window rows on days [lag, upto)
+    S1 = DD{0.0, 0.0};
+    S2 = DD{0.0, 0.0};
+    bool have = false;
+    for (int e = lag; e < upto; ++e) {
+      if (ST(e) != MFF_STATE_VALUE) continue;
+      const double xe = X(e);
+      if (!__builtin_isfinite(xe)) continue;
+      if (!have) { c = xe; have = true; }
+      const double y = xe - c;
+      S1 = dd_add(S1, y);
+      S2 = dd_add(S2, two_prod(y, y));
+    }
+  };
   for (int d = 0; d < D; ++d) {
-    const double x = xn;
-    const uint8_t sx = sn;
-    if (d > 0) {
-      const size_t op = (size_t)(d - 1) * S + s;
-      ov[op] = rprev;
-      os[op] = sprev;
+    const uint8_t sx = ST(d);
+    const size_t o = (size_t)d * S;
+    if (sx == MFF_STATE_ABSENT) {
+      ov[o] = 0.0;
+      os[o] = MFF_STATE_ABSENT;
+      continue;
     }
-    if (d + 1 < D) {  // prefetch next day
-      xn = v[(size_t)(d + 1) * S + s];
-      sn = st[(size_t)(d + 1) * S + s];
-    }
-    rprev = 0.0;
-    sprev = sx;
-    if (sx == MFF_STATE_ABSENT) continue;
     const bool isnull = sx == MFF_STATE_NULL;
+    const double x = isnull ? 0.0 : X(d);
     if (method == MFF_ROLL_O) {
-      rprev = isnull ? 0.0 : x;
+      ov[o] = x;
+      os[o] = sx;
       continue;
     }
-    ring[pos * 64 + lane] = isnull ? 0.0 : x;
-    nullm = isnull ? (nullm | (1ull << pos)) : (nullm & ~(1ull << pos));
-    const int oldest = (pos + 1 == N) ? 0 : pos + 1;
-    pos = oldest;
-    ++cnt;
-    if (cnt < N || nullm != 0) {
-      sprev = MFF_STATE_NULL;
+    const bool fin = !isnull && __builtin_isfinite(x);
+    if (!(fin && prevok && x == prev)) lastchg = k;
+    prev = x;
+    prevok = fin;
+    if (cnt == N) {  // the oldest row leaves
+      const uint8_t so = ST(lag);
+      if (so == MFF_STATE_NULL) {
+        --nnull;
+      } else {
+        const double xo = X(lag);
+        if (__builtin_isnan(xo)) --nnan;
+        else if (xo == __builtin_inf()) --npi;
+        else if (xo == -__builtin_inf()) --nni;
+        else {
+          --nfin;
+          const double y = xo - c;
+          const double before = S2.hi;
+          S1 = dd_add(S1, -y);
+          const DD p = two_prod(y, y);
+          S2 = dd_add(S2, dd_neg(p));
+          if (nfin > 0 && before > 0.0 && !(S2.hi > before * 0x1p-30)) {
+            do { ++lag; } while (ST(lag) == MFF_STATE_ABSENT);
+            rebuild(d);
+            goto entered;
+          }
+        }
+      }
+      do { ++lag; } while (ST(lag) == MFF_STATE_ABSENT);
+    } else {
+      if (cnt == 0) lag = d;
+      ++cnt;
+    }
+  entered:
+    if (isnull) ++nnull;
+    else if (__builtin_isnan(x)) ++nnan;
+    else if (x == __builtin_inf()) ++npi;
+    else if (x == -__builtin_inf()) ++nni;
+    else {
+      if (nfin == 0) {  // empty of finite values: fresh shift, exact zero sums
+        c = x;
+        S1 = DD{0.0, 0.0};
+        S2 = DD{0.0, 0.0};
+      }
+      ++nfin;
+      const double y = x - c;
+      S1 = dd_add(S1, y);
+      S2 = dd_add(S2, two_prod(y, y));
+    }
+    ++k;
+    if (cnt < N || nnull > 0) {
+      ov[o] = 0.0;
+      os[o] = MFF_STATE_NULL;
       continue;
     }
-    double x0 = ring[oldest * 64 + lane];
-    if (!__builtin_isfinite(x0)) x0 = 0.0;
-    double s1 = 0.0;
-    for (int i = 0; i < N; ++i) s1 += ring[i * 64 + lane] - x0;
-    const double mean = x0 + s1 / (double)N;
-    double s2 = 0.0;
-    for (int i = 0; i < N; ++i) {
-      const double dlt = ring[i * 64 + lane] - mean;
-      s2 += dlt * dlt;
+    double mean, sd;
+    if (nnan > 0 || (npi > 0 && nni > 0)) {
+      mean = qnan();
+      sd = qnan();
+    } else if (npi > 0 || nni > 0) {
+      mean = npi > 0 ? __builtin_inf() : -__builtin_inf();
+      sd = qnan();
+    } else if (lastchg <= k - N) {  // rows k-N .. k-1 (0-based) identical
+      mean = x;
+      sd = 0.0;
+    } else {
+      const double inv_n = 1.0 / (double)N;
+      const double m1 = (S1.hi + S1.lo) * inv_n;
+      mean = c + m1;
+      const DD q = dd_add(S2, dd_neg(dd_sq_div(S1, (double)N)));
+      const double var = q.hi + q.lo;
+      sd = sqrt(var > 0.0 ? var * inv_n : 0.0);
+      if (method == MFF_ROLL_Z) {
+        ov[o] = (((x - c) - m1)) / sd;
+        os[o] = MFF_STATE_VALUE;
+        continue;
+      }
     }
-    const double sd = sqrt(s2 / (double)N);
-    double res;
-    if (method == MFF_ROLL_M) res = mean;
-    else if (method == MFF_ROLL_STD) res = sd;
-    else res = (x - mean) / sd;  // MFF_ROLL_Z, x not null here
-    rprev = res;
-    sprev = MFF_STATE_VALUE;
+    ov[o] = method == MFF_ROLL_M ? mean : method == MFF_ROLL_STD ? sd : (x - mean) / sd;
+    os[o] = MFF_STATE_VALUE;
   }
-  const size_t ol = (size_t)(D - 1) * S + s;
-  ov[ol] = rprev;
-  os[ol] = sprev;
 }
 
 // Register-window variant for the common window lengths (N a template constant): the
 // last N present values live in VGPRs as a shift register (w[N-1] = newest, w[0] =
 // oldest, shifted on present days only), so the per-day recompute reads no LDS, and the
 // days are loaded S2_U at a time one chunk ahead (S2_U loads in flight per lane instead
-// of 1).  Same window arithmetic as k_stage2 (mean shifted by the oldest value when
-// finite, two passes over the window), summed oldest -> newest, the two divisions by N
+// of 1).  Window arithmetic: mean shifted by the oldest value when finite, two passes
+// over the window summed oldest -> newest, the two divisions by N
 // as products with 1/N (a constant window still gives s1 = s2 = 0 exactly: std 0, z NaN).
 constexpr int S2_U = 4;  // 4 in flight + 4 processed: <= 96 VGPRs at N = 20 (5 waves/SIMD)
 constexpr int S2_THREADS = 256;
@@ -334,7 +407,7 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
                           int method, double* out_val, uint8_t* out_state, void* stream) {
   clear_error();
   MFF_REQUIRE(rows > 0 && D > 0 && S > 0, "mff_stage2: bad sizes rows=%d D=%d S=%d", rows, D, S);
-  MFF_REQUIRE(N >= 1 && N <= S2_MAXN, "mff_stage2: N=%d outside [1, %d]", N, S2_MAXN);
+  MFF_REQUIRE(N >= 1, "mff_stage2: N=%d < 1", N);
   MFF_REQUIRE(method >= MFF_ROLL_O && method <= MFF_ROLL_STD, "mff_stage2: unknown method %d", method);
   MFF_REQUIRE(val && state && out_val && out_state, "mff_stage2: NULL buffer");
   const long long nreg = (long long)rows * ((S + S2_THREADS - 1) / S2_THREADS);
@@ -344,7 +417,10 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
                        state, D, S, method, out_val, out_state);                                            \
     MFF_LAUNCH_CHECK();                                                                                     \
     return 0;
-  switch (N) {  // the usual windows: register shift window; other N: the LDS ring below
+  // MFF_STAGE2_IMPL=slide: the sliding kernel for every N (A/B timing)
+  const char* impl = getenv("MFF_STAGE2_IMPL");
+  const bool force_slide = impl && impl[0] == 's';
+  switch (force_slide ? -1 : N) {  // the usual windows: register shift window; other N: sliding sums
     MFF_S2_REG(1)
     MFF_S2_REG(2)
     MFF_S2_REG(3)
@@ -356,10 +432,9 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
       break;
   }
 #undef MFF_S2_REG
-  const long long nblk = (long long)rows * ((S + 63) / 64);
-  const size_t lds = (size_t)N * 64 * 8;
-  hipLaunchKernelGGL(k_stage2, dim3((unsigned)nblk), dim3(64), lds, as_stream(stream), val, state, D, S,
-                     N, method, out_val, out_state);
+  const long long nsl = (long long)rows * ((S + S2_SLIDE_THREADS - 1) / S2_SLIDE_THREADS);
+  hipLaunchKernelGGL(k_stage2_slide, dim3((unsigned)nsl), dim3(S2_SLIDE_THREADS), 0, as_stream(stream), val, state,
+                     D, S, N, method, out_val, out_state);
   MFF_LAUNCH_CHECK();
   return 0;
 }

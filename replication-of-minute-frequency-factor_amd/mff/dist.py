@@ -4,13 +4,15 @@ Replaces the reference's only parallelism, a joblib process pool over day files
 (MinuteFrequentFactorCICC.py:85-94), with contiguous stock shards per GPU
 (SURVEY.md §8(e)).  Stage 1 is independent per stock-day except doc_pdf's frame-wide
 rank, and stage 3 is a per-day cross-section, so the engine calls exactly three kinds
-of collective, all through this module:
+of collective (plus reduce_scatter), all through this module:
 
-  all_gather  doc_pdf threshold queries [5][D][S_loc] f64 (once per panel)
+  all_gather  doc_pdf sorted day lists [nd][M] u64 (once per panel)
               stage-3 z moments [rows][D][3] f64; stage-3 rank columns [rows][D][S_loc]
-  all_reduce  doc_pdf counts per sorted query [nd][M] i32 = 2 n_less + n_eq (sum)
+  reduce_scatter  doc_pdf counts per sorted query [R][nd][M] i32 = 2 n_less + n_eq, summed
+              and scattered by day block to the day's owner
   all_to_all  doc_pdf queries of each rank's day block [R][5][nd][S_all] f64 (the sort
-              of a day's queries runs on one rank, its sorted list is all-gathered)
+              of a day's queries runs on one rank, its sorted list is all-gathered), and
+              the owner's counts back to the queries' ranks [R][5][nd][S_all] i32
 
 ``Comm`` wraps torch.distributed ("nccl" = RCCL over xGMI on MI355X, "gloo" on CPU);
 ``ThreadComm`` runs R ranks as threads of one process (tests emulate an R-GPU job on
@@ -69,6 +71,19 @@ class Comm:
         self._dist.all_to_all_single(out, t, group=self.group)
         return out
 
+    def reduce_scatter_sum(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *shape] on every rank -> slice `rank` summed over the ranks, [*shape]
+        (RCCL reduce-scatter: each rank sends (world-1)/world of the input once, half
+        the bytes of a ring all-reduce of the same array)."""
+        t = t.contiguous()
+        if self.backend == "gloo":  # host collectives: all-reduce, keep the own slice
+            h = t.cpu()
+            self._dist.all_reduce(h, op=self._dist.ReduceOp.SUM, group=self.group)
+            return h[self.rank].to(t.device)
+        out = torch.empty(tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        self._dist.reduce_scatter_tensor(out, t, op=self._dist.ReduceOp.SUM, group=self.group)
+        return out
+
     def _all_reduce(self, t: torch.Tensor, op) -> None:
         if self.backend == "gloo" and t.device.type != "cpu":
             h = t.cpu()
@@ -101,16 +116,28 @@ class ThreadComm:
         return _RankComm(self, rank)
 
     def _exchange(self, rank: int, t: torch.Tensor) -> List[torch.Tensor]:
-        if t.is_cuda:
-            torch.cuda.synchronize(t.device)
-        self._slots[rank] = t.clone()
+        # The clone is queued on this rank thread's current stream (a non-blocking side
+        # stream under the doc_pdf overlap), so the device is synchronised after it:
+        # a peer reads it on its own stream right after the barrier.
+        c = t.clone()
+        _sync(c)
+        self._slots[rank] = c
         self._barrier.wait()
         parts = list(self._slots)
         self._barrier.wait()
         return parts
 
 
+def _sync(t: torch.Tensor) -> None:
+    if t.is_cuda:
+        torch.cuda.synchronize(t.device)
+
+
 class _RankComm:
+    """One rank's view of a ThreadComm.  Every collective synchronises the device before
+    it returns: the peers' clones it read are freed into their owners' stream pools when
+    the references drop, so no kernel of this rank may still be reading them."""
+
     def __init__(self, parent: ThreadComm, rank: int):
         self._p = parent
         self.rank = rank
@@ -118,11 +145,24 @@ class _RankComm:
         self.backend = "thread"
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
-        return torch.stack(self._p._exchange(self.rank, t.contiguous()))
+        out = torch.stack(self._p._exchange(self.rank, t.contiguous()))
+        _sync(out)
+        return out
 
     def all_to_all(self, t: torch.Tensor) -> torch.Tensor:
         parts = self._p._exchange(self.rank, t.contiguous())
-        return torch.stack([p[self.rank] for p in parts])
+        out = torch.stack([p[self.rank] for p in parts])
+        _sync(out)
+        return out
+
+    def reduce_scatter_sum(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *shape] on every rank -> slice `rank` summed over ranks, [*shape]."""
+        parts = self._p._exchange(self.rank, t.contiguous())
+        acc = parts[0][self.rank].clone()
+        for x in parts[1:]:
+            acc += x[self.rank]
+        _sync(acc)
+        return acc
 
     def all_reduce_sum(self, t: torch.Tensor) -> None:
         parts = self._p._exchange(self.rank, t)
@@ -130,10 +170,12 @@ class _RankComm:
         for x in parts[1:]:
             acc += x
         t.copy_(acc)
+        _sync(t)
 
     def all_reduce_max(self, t: torch.Tensor) -> None:
         parts = self._p._exchange(self.rank, t)
         t.copy_(torch.stack(parts).amax(0))
+        _sync(t)
 
     def barrier(self) -> None:
         self._p._barrier.wait()

@@ -26,7 +26,6 @@ from .synth import pack_mask, stack_fields
 
 ABSENT, NULL, VALUE = 0, 1, 2
 ROLL_METHODS = {"o": 0, "m": 1, "z": 2, "std": 3}
-PDF_MAX_QUERIES = 32767  # per day, all ranks (mff_pdf_count LDS bins)
 
 
 def _stream(device) -> int:
@@ -151,13 +150,9 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
     R = 1 if comm is None else comm.world_size
     S_all = S if comm is None else _agreed_max(comm, S, dev)
     M = R * 5 * S_all
-    if M > PDF_MAX_QUERIES:
-        raise _lib.MffError(f"doc_pdf: {M} queries per day exceed {PDF_MAX_QUERIES} "
-                            f"(ranks*5*stocks); shard fewer stocks per day")
     st = _stream(dev)
     if comm is not None:
-        _pdf_ranks_sharded(lib, panel, pdfq, levels, rows, val, state, comm, S_all, M, st,
-                           day_batch)
+        _pdf_ranks_sharded(comm, pdfq, S_all, PdfKernels(lib, levels, S, D, rows, val, state, st))
         return
     if day_batch is None:
         per_day = lib.mff_pdf_workspace_bytes(S, R, 1) + M * 8 + M * 8
@@ -175,18 +170,73 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
                    "mff_pdf_rank_local")
 
 
-def _pdf_ranks_sharded(lib, panel, pdfq, levels, rows, val, state, comm, S_all: int, M: int, st,
-                       day_batch: Optional[int]):
-    """doc_pdf across stock shards: rank r sorts the queries of its own
-    contiguous day block only (all_to_all of the [5][days][S] query blocks), the sorted
-    lists are all-gathered, every rank counts its local level keys against each day's
-    full list, the one-word counts are all-reduced and every rank finalizes its own
-    stock-days.  The sort is not replicated: 1/R of the days per rank."""
+class PdfKernels:
+    """The device phases of the stock-sharded doc_pdf rank (libmff, this rank's stream).
+    `_pdf_ranks_sharded` only moves tensors between these phases and the collectives, so
+    tests drive the same exchange with CPU stand-ins for the phases (gloo, world 2)."""
+
+    def __init__(self, lib, levels, S_loc: int, D: int, rows, val, state, st):
+        self.lib, self.levels, self.S, self.D = lib, levels, S_loc, D
+        self.rows, self.val, self.state, self.st = rows, val, state, st
+
+    def sort(self, q_all, R: int, S_all: int, nd: int):
+        """q_all [R][5][nd_max][S_all] -> total-order keys of days 0..nd sorted, int64 [nd][M]."""
+        lib, dev = self.lib, q_all.device
+        M = R * 5 * S_all
+        out = torch.empty((nd, M), dtype=torch.int64, device=dev)
+        ws = torch.empty(lib.mff_pdf_workspace_bytes(S_all, R, nd), dtype=torch.uint8, device=dev)
+        _lib.check(lib.mff_pdf_sort(_lib.ptr(q_all), R, S_all, int(q_all.shape[2]), 0, nd, _lib.ptr(out),
+                                    _lib.ptr(ws), self.st), "mff_pdf_sort")
+        return out
+
+    def count(self, q_sorted):
+        """This rank's level keys against every day's full sorted list: int32 [D][M] =
+        2 n_less + n_eq at each value's first sorted position."""
+        D, M = q_sorted.shape
+        counts = torch.empty((D, M), dtype=torch.int32, device=q_sorted.device)
+        ws = torch.empty(256, dtype=torch.uint8, device=q_sorted.device)
+        _lib.check(self.lib.mff_pdf_count(_lib.ptr(self.levels), self.S, self.D, 0, D, _lib.ptr(q_sorted), M,
+                                          _lib.ptr(counts), _lib.ptr(ws), self.st), "mff_pdf_count")
+        return counts
+
+    def origin(self, q_all, R: int, S_all: int, q_sorted, counts):
+        """Counts of the owned days' lists at every query's position, in the queries'
+        origin layout int32 [R][5][nd_max][S_all]."""
+        nd_max, M = q_sorted.shape
+        out = torch.empty((R, 5, nd_max, S_all), dtype=torch.int32, device=q_all.device)
+        _lib.check(self.lib.mff_pdf_origin_counts(_lib.ptr(q_all), R, S_all, nd_max, 0, nd_max,
+                                                  _lib.ptr(q_sorted), _lib.ptr(counts), M, _lib.ptr(out),
+                                                  self.st), "mff_pdf_origin_counts")
+        return out
+
+    def finalize(self, q_local, own_counts):
+        """own_counts int32 [5][D][S_loc] -> the doc_pdf rows of val / state."""
+        _lib.check(self.lib.mff_pdf_finalize_own(_lib.ptr(q_local), _lib.ptr(own_counts), self.S, self.D,
+                                                 _lib.int_array(self.rows), _lib.ptr(self.val),
+                                                 _lib.ptr(self.state), self.st), "mff_pdf_finalize_own")
+
+
+def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern):
+    """doc_pdf across stock shards.  Day d is owned by the rank whose
+    contiguous day block holds it:
+      1. all_to_all: every rank's queries of the owner's days -> the owner, which sorts
+         them (the sort is not replicated: 1/R of the days per rank);
+      2. all_gather of the sorted day lists [D][M];
+      3. every rank counts its own level keys against each day's full list -> [D][M]
+         (one word per sorted query, 2 n_less + n_eq: linear in the average rank);
+      4. reduce_scatter (sum) of the counts by day block: each owner gets its days' totals;
+      5. the owner looks every query of its days up (origin layout) and one all_to_all
+         returns each rank the counts of its own queries; each rank finalizes its
+         stock-days (rank = (c + 1) / 2).
+    Only step 2 moves O(D x M) bytes per rank; step 4 replaces a ring all-reduce of the
+    whole [D][M] (2x the bytes per rank on a link-bound ring).  pdfq: [5][D][S_loc]."""
     from .dist import shard_bounds
 
-    D, S = panel.D, panel.S
-    dev = panel.device
-    R = comm.world_size
+    D = int(pdfq.shape[1])
+    S_loc = int(pdfq.shape[2])
+    dev = pdfq.device
+    R, rank = comm.world_size, comm.rank
+    M = R * 5 * S_all
     blocks = [shard_bounds(D, R, r) for r in range(R)]
     nd_max = max(1, max(b1 - b0 for b0, b1 in blocks))
     q_pad = _pad_last(pdfq, S_all, float("nan"))  # [5][D][S_all]
@@ -194,29 +244,30 @@ def _pdf_ranks_sharded(lib, panel, pdfq, levels, rows, val, state, comm, S_all: 
     for r, (b0, b1) in enumerate(blocks):
         send[r, :, :b1 - b0] = q_pad[:, b0:b1]
     recv = comm.all_to_all(send)  # [R][5][nd_max][S_all]: every rank's queries of my days
-    b0, b1 = blocks[comm.rank]
+    del send, q_pad
+    b0, b1 = blocks[rank]
+    nd = b1 - b0
     mine = torch.zeros((nd_max, M), dtype=torch.int64, device=dev)
-    if b1 > b0:
-        ws = torch.empty(lib.mff_pdf_workspace_bytes(S_all, R, b1 - b0), dtype=torch.uint8, device=dev)
-        _lib.check(lib.mff_pdf_sort(_lib.ptr(recv), R, S_all, nd_max, 0, b1 - b0, _lib.ptr(mine),
-                                    _lib.ptr(ws), st), "mff_pdf_sort")
+    if nd > 0:
+        mine[:nd] = kern.sort(recv, R, S_all, nd)
     gathered = comm.all_gather(mine)  # [R][nd_max][M]
     q_sorted = torch.cat([gathered[r, :e - s] for r, (s, e) in enumerate(blocks)])  # [D][M]
-    del send, recv, gathered, mine
-    if day_batch is None:
-        day_batch = max(1, min(D, (1 << 30) // (M * 4)))
-    for d0 in range(0, D, day_batch):
-        nd = min(day_batch, D - d0)
-        qs = q_sorted[d0:d0 + nd]
-        ws = torch.empty(256, dtype=torch.uint8, device=dev)  # the count phase needs no scratch
-        counts = torch.empty((nd, M), dtype=torch.int32, device=dev)  # 2 n_less + n_eq
-        _lib.check(lib.mff_pdf_count(_lib.ptr(levels), S, D, d0, nd,
-                                     _lib.ptr(qs), M, _lib.ptr(counts), _lib.ptr(ws), st),
-                   "mff_pdf_count")
-        comm.all_reduce_sum(counts)
-        _lib.check(lib.mff_pdf_finalize(_lib.ptr(pdfq), _lib.ptr(qs), _lib.ptr(counts), S, D,
-                                        d0, nd, M, _lib.int_array(rows), _lib.ptr(val),
-                                        _lib.ptr(state), st), "mff_pdf_finalize")
+    del gathered
+    counts = kern.count(q_sorted)  # [D][M], this rank's keys
+    del q_sorted
+    cs = torch.zeros((R, nd_max, M), dtype=torch.int32, device=dev)
+    for r, (s, e) in enumerate(blocks):
+        cs[r, :e - s] = counts[s:e]
+    del counts
+    my_counts = comm.reduce_scatter_sum(cs)  # [nd_max][M], summed over ranks
+    del cs
+    origin = kern.origin(recv, R, S_all, mine, my_counts)  # [R][5][nd_max][S_all]
+    back = comm.all_to_all(origin)  # slice r: my queries' counts on rank r's days
+    del origin, recv, mine, my_counts
+    own = torch.empty((5, D, S_loc), dtype=torch.int32, device=dev)
+    for r, (s, e) in enumerate(blocks):
+        own[:, s:e] = back[r, :, :e - s, :S_loc]
+    kern.finalize(pdfq, own)
 
 
 def _agreed_max(comm, n: int, dev) -> int:

@@ -77,10 +77,14 @@ def _t(a, dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N", [1, 5, 20])
+@pytest.mark.parametrize("N", [1, 2, 5, 20, 64, 65, 120, 250])
 def test_future_return_matches_oracle(dev, N):
+    """Any future_days (Factor.py:149): the sliding double-double window of
+    k_future_return, through suspension runs, nulls, NaN and a -100 % day (log -inf)."""
     from mff import engine
-    pct, ps, _, _ = _daily(np.random.default_rng(5))
+    pct, ps, _, _ = _daily(np.random.default_rng(5), D=max(40, N + 80))
+    pct[30, 9] = -1.0   # log(1 + pct) = -inf: every window holding it gives -1
+    pct[33, 11] = np.inf
     gv, gs = engine.future_return(_t(pct, dev), _t(ps, dev), N)
     ov, os_ = O.oracle_future_return(pct, ps, N)
     assert not compare(gv.cpu().numpy(), gs.cpu().numpy(), ov, os_, "future_return", atol=1e-12)

@@ -176,20 +176,32 @@ def _random_long_panel(D, S, seed):
     return val, state
 
 
-@pytest.mark.parametrize("N", [1, 5, 7, 20, 60])
-def test_stage2_live(dev, N):
-    """N in {1, 2, 3, 5, 10, 20, 60}: register shift window (k_stage2_reg); 7: LDS ring."""
+@pytest.mark.parametrize("N,D", [(1, 70), (2, 70), (3, 70), (5, 70), (7, 70), (10, 70), (20, 70), (60, 150),
+                                  (64, 150), (65, 150), (120, 300), (250, 400),
+                                  (20, 1), (20, 3), (5, 4), (3, 8), (7, 8)])
+def test_stage2_live(dev, N, D):
+    """N in {1, 2, 3, 5, 10, 20, 60}: register shift window (k_stage2_reg); any other N
+    (7, 64, 65, 120, 250): the sliding double-double kernel (k_stage2_slide).  D covers
+    D < 4 (no whole register chunk), D % 4 == 0 (last chunk flushed after the loop) and
+    D < N; two factor rows exercise the per-row plane offsets."""
     import mff_oracle as O
     from mff import engine
-    val, state = _random_long_panel(150 if N > 20 else 70, 130, N)
+    val, state = _random_long_panel(D, 130, N)
+    val2, state2 = _random_long_panel(D, 130, N + 1000)
+    val2[:, 5] = 1e6 + 0.25 * np.arange(D)  # trend drifting away from the shift
+    if D > 40:
+        val2[20, 6] = 1e15                 # outlier leaving the window (S2 cancellation)
+    v = np.ascontiguousarray(np.stack([val, val2]))
+    st = np.ascontiguousarray(np.stack([state, state2]))
     bad = []
     for meth in ("o", "m", "z", "std"):
-        ov, os_ = O.oracle_stage2(val, state, N, meth)
-        rv, rs = engine.rolling(torch.from_numpy(val[None]).to(dev), torch.from_numpy(state[None]).to(dev),
-                                N, meth)
+        rv, rs = engine.rolling(torch.from_numpy(v).to(dev), torch.from_numpy(st).to(dev), N, meth)
         torch.cuda.synchronize()
-        bad += compare(rv[0].cpu().numpy(), rs[0].cpu().numpy(), ov, os_, f"N{N}/{meth}", atol=1e-9)
-    assert not bad, "\n".join(bad)
+        rv, rs = rv.cpu().numpy(), rs.cpu().numpy()
+        for r in range(2):
+            ov, os_ = O.oracle_stage2(v[r], st[r], N, meth)
+            bad += compare(rv[r], rs[r], ov, os_, f"N{N}/D{D}/row{r}/{meth}", atol=1e-9)
+    assert not bad, "\n".join(bad[:20])
 
 
 @pytest.mark.parametrize("kind", ["z", "rank"])

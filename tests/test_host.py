@@ -53,8 +53,8 @@ def test_library_catalogue_and_errors_without_gpu():
     assert [lib.mff_factor_name(i).decode() for i in range(58)] == catalog.NAMES
     assert lib.mff_factor_name(58) is None
     # argument validation happens before any device work
-    rc = lib.mff_stage2(None, None, 1, 1, 1, 99, 1, None, None, None)
-    assert rc < 0 and b"N=99" in lib.mff_last_error()
+    rc = lib.mff_stage2(None, None, 1, 1, 1, 0, 1, None, None, None)
+    assert rc < 0 and b"N=0" in lib.mff_last_error()
     with pytest.raises(_lib.MffError):
         _lib.check(rc, "mff_stage2")
     assert lib.mff_pdf_workspace_bytes(300, 1, 10) > 0
