@@ -143,6 +143,21 @@ def test_doc_pdf_four_slices(dev):
     assert not bad, "\n".join(bad)
 
 
+def test_doc_pdf_beyond_32768_queries(dev):
+    """S = 7,000 codes: M = 35,000 queries per day, past the bucketed sort's 32,768 (global
+    merge passes) and over four count slices; the round-1 cap (32,767) is gone."""
+    import mff_oracle as O
+    from mff import synth
+    panel = synth.make_panel(7000, 1, config=15)
+    names = ["doc_pdf60", "doc_pdf95"]
+    ov, os_ = O.oracle_stage1(panel, names)
+    gv, gs, _ = _run_stage1(panel, dev, names)
+    bad = []
+    for r, nm in enumerate(names):
+        bad += compare(gv[r], gs[r], ov[r], os_[r], nm, atol=0.0, rtol=0.0)
+    assert not bad, "\n".join(bad)
+
+
 def test_stage2_golden(dev):
     from golden.make_golden import STAGE23_FACTORS
     from mff import engine, catalog
