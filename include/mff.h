@@ -119,6 +119,23 @@ int mff_stage1(const float* open, const float* high, const float* low,
                void* workspace, void* stream);
 
 /*
+ * Multi-day frame semantics of the four factors whose reference windows run over('code')
+ * only: liq_amihud_1min (CM:745-746 pct_change over code), corr_prvr (CM:855-867),
+ * trade_bottom20retRatio (CM:1212-1216 volume.sum().over('code')) and
+ * trade_bottom50retRatio (CM:1233-1241).  The reference driver calls cal_* per day file
+ * (MinuteFrequentFactorCICC.py:22), where they are per-day; a cal_* handed a frame of
+ * several dates reaches across them.  Given the panel of such a frame (days = the frame's
+ * dates, rows of a code in (date, time) order) and stage 1's output rows, this call
+ * overwrites the rows of those four factors (when present in factor_ids) with the frame
+ * semantics: the first bar of a day compares with the code's last close of the previous
+ * day, and the 14:40+ / 14:10+ volume share uses the code's total over the whole frame.
+ * open may be NULL unless a trade_bottom* row is requested.
+ */
+int mff_stage1_frame(const float* open, const float* close, const float* volume,
+                     const uint32_t* valid, int S, int D, const int32_t* factor_ids /* host */,
+                     int nf, double* val, uint8_t* state, void* stream);
+
+/*
  * doc_pdf60..95 frame-wide rank (CM:1015-1017: `.rank()` over ALL rows of the day
  * frame, every code).  Device phases; each works on days [d0, d0+nd) of arrays laid
  * out over all D days.

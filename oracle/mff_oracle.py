@@ -947,6 +947,59 @@ def oracle_stage1(panel, names: Sequence[str] = None):
     return val, state
 
 
+FRAME_XDAY_NAMES = ["liq_amihud_1min", "corr_prvr", "trade_bottom20retRatio", "trade_bottom50retRatio"]
+
+
+def oracle_frame_xday(panel):
+    """The four cal_* whose windows cross days when the reference function is handed a
+    MULTI-day long frame (all days of `panel` as one frame, rows of a code in (date, time)
+    order): ``.over('code')`` spans the whole frame instead of one day.
+      liq_amihud_1min CM:739-760, corr_prvr CM:855-874, trade_bottom20retRatio
+      CM:1211-1223, trade_bottom50retRatio CM:1232-1247.
+    Returns {name: (val [D][S], state [D][S])}."""
+    D, S = panel["present"].shape[:2]
+    out = {n: (np.zeros((D, S)), np.zeros((D, S), np.uint8)) for n in FRAME_XDAY_NAMES}
+
+    def put(name, d, s, x):
+        v, st = out[name]
+        st[d, s] = NULLV if x is None else VALUE
+        v[d, s] = 0.0 if x is None else x
+
+    for s in range(S):
+        dd, mm = np.nonzero(panel["present"][:, s])  # rows of the code, (date, time) order
+        if dd.size == 0:
+            continue
+        g = lambda k: panel[k][dd, s, mm].astype(np.float64)
+        o, c, v = g("open"), g("close"), g("volume")
+        # liq_amihud_1min: pct_change().over('code').abs().fill_null(0); v > 0 ? pct / v : 0
+        pc = pl_pct_change(c)
+        am = [(_div(0.0 if p is None else abs(p), vv) if vv > 0 else 0.0) for p, vv in zip(pc, v)]
+        for d in np.unique(dd):
+            put("liq_amihud_1min", d, s, pl_sum([a for a, e in zip(am, dd) if e == d]))
+        # corr_prvr: filter(volume != 0), pct_change of close and volume over('code'),
+        # then pl.corr per (code, date)
+        nz = v != 0
+        cc, vc = pl_pct_change(c[nz]), pl_pct_change(v[nz])
+        dz = dd[nz]
+        for d in np.unique(dz):
+            sel = [i for i in range(dz.size) if dz[i] == d]
+            put("corr_prvr", d, s, pl_corr([cc[i] for i in sel], [vc[i] for i in sel]))
+        # trade_bottom20 / 50: filter(time >= 14:40 / 14:10), volume_d over('code')
+        for name, m0, plus_one in (("trade_bottom20retRatio", 220, True), ("trade_bottom50retRatio", 190, False)):
+            t = mm >= m0
+            if not t.any():
+                continue
+            tot = pl_sum(v[t])
+            den = tot + 1.0 if plus_one else (1.0 if tot == 0 else tot)
+            with np.errstate(all="ignore"):
+                ret = c[t] / o[t] - 1.0
+                vd = v[t] / den
+            for d in np.unique(dd[t]):
+                k = dd[t] == d
+                put(name, d, s, pl_sum(vd[k] * ret[k]))
+    return out
+
+
 def oracle_stage2(val: np.ndarray, state: np.ndarray, N: int, method: str):
     """MF:187-240, ``cal_final_exposure(N, method, mode='days')`` on one factor.
 

@@ -360,7 +360,7 @@ class MinFreqFactor(Factor):
                     print(f"处理文件 {f} 时出错: {str(e)}")
             if not tables:
                 continue
-            res = compute_long(tables, [name], device)
+            res = compute_long(tables, [name], device, per_day=True)  # one reference call per file
             out.append(res[name])
         return out
 

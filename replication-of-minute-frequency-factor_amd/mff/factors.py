@@ -26,20 +26,42 @@ def _device(device=None):
     return torch.device("cuda", torch.cuda.current_device())
 
 
-def compute_long(df, names: Sequence[str] | None = None, device=None) -> Dict:
-    """Long frame(s) (one or more days; a list of day-file tables is ingested batch by
-    batch without concatenation) -> {name: long result frame} for the requested factors,
-    computed in one stage-1 pass."""
+# factors whose reference windows over('code') cross days on a multi-day frame
+# (mff_stage1_frame, csrc/mff_frame.hip)
+FRAME_XDAY = ("liq_amihud_1min", "corr_prvr", "trade_bottom20retRatio", "trade_bottom50retRatio")
+
+
+def compute_long(df, names: Sequence[str] | None = None, device=None, per_day: bool | None = None) -> Dict:
+    """Long frame(s) -> {name: long result frame} for the requested factors, computed in
+    one stage-1 pass.
+
+    ``df`` is one long frame (any number of dates) or a list of day-file tables (ingested
+    batch by batch without concatenation).  A single frame holding several dates is ONE
+    reference frame: the four functions whose windows run over('code') only
+    (liq_amihud_1min CM:746, corr_prvr CM:862-867, trade_bottom20/50retRatio CM:1216,
+    1238-1240) then reach across days exactly as the reference does on that frame (rows of
+    a code in (date, time) order).  A list of tables is a list of day files, each its own
+    reference call (MinuteFrequentFactorCICC.py:22): per-day semantics.  ``per_day``
+    overrides the choice."""
     import torch
 
-    from . import engine
+    from . import _lib, engine
 
     names = list(catalog.NAMES if names is None else
                  [n[4:] if n.startswith("cal_") else n for n in names])
     from . import ingest
 
+    if per_day is None:
+        per_day = isinstance(df, (list, tuple))
     dp = ingest.to_device_panel(df, _device(device))  # GPU long -> dense (mff_ingest_rows)
-    val, state, _ = engine.compute_factors(dp, names)
+    val, state, ids = engine.compute_factors(dp, names)
+    if not per_day and dp.D > 1 and any(n in FRAME_XDAY for n in names):
+        lib = _lib.load()
+        b = dp.bars
+        _lib.check(lib.mff_stage1_frame(_lib.ptr(b[0]), _lib.ptr(b[3]), _lib.ptr(b[4]), _lib.ptr(dp.mask),
+                                        dp.S, dp.D, _lib.int_array(ids), len(ids), _lib.ptr(val),
+                                        _lib.ptr(state), torch.cuda.current_stream(dp.device).cuda_stream),
+                   "mff_stage1_frame")
     torch.cuda.synchronize(dp.device)
     v, s = val.cpu().numpy(), state.cpu().numpy()
     return {nm: frames.to_long(v[i], s[i], dp.codes, dp.dates, nm,

@@ -37,16 +37,30 @@ def test_cal_functions_on_long_frames(dev, panel_and_oracle):
     """Every cal_* through the reference calling convention (one long multi-day frame)."""
     import MinuteFrequentFactorCalculateMethodsCICC as CM
     from mff import catalog
+    import mff_oracle as O
     panel, (ov, os_) = panel_and_oracle
     df = long_frame(panel)
     res = CM.compute_long(df)
+    xday = O.oracle_frame_xday(panel)  # one 3-day frame: over('code') spans the dates
     bad = []
     for i, nm in enumerate(catalog.NAMES):
         out = res[nm]
         assert list(out.columns) == (["date", "code", nm] if nm == "shape_skratio" else ["code", "date", nm])
         v, s = _dense(out, nm, panel)
-        bad += compare(v, s, ov[i], os_[i], nm)
+        ev, es = xday[nm] if nm in xday else (ov[i], os_[i])
+        bad += compare(v, s, ev, es, nm)
     assert not bad, "\n".join(bad)
+    # the same days as a list of day files: one reference call per file, per-day values
+    per_file = CM.compute_long([long_frame(panel, d) for d in range(len(panel["dates"]))], list(xday))
+    for nm in xday:
+        i = catalog.ID[nm]
+        v, s = _dense(per_file[nm], nm, panel)
+        bad += compare(v, s, ov[i], os_[i], f"{nm}/per-file")
+    assert not bad, "\n".join(bad)
+    # the frame values really differ from the per-day ones on days after the first
+    v, s = _dense(res["liq_amihud_1min"], "liq_amihud_1min", panel)
+    i = catalog.ID["liq_amihud_1min"]
+    assert (np.abs(v[1:] - ov[i][1:]) > 0).any()
     one = CM.cal_mmt_pm(long_frame(panel, 0))  # single day, single factor
     v, s = _dense(one, "mmt_pm", {"codes": panel["codes"], "dates": panel["dates"][:1]})
     assert not compare(v, s, ov[0][:1], os_[0][:1], "mmt_pm")
