@@ -12,14 +12,16 @@ so "scaling" is "strong".  value = S*D*K / max-over-ranks(wall time of the K ste
 
 roofline: the stage-1 pass (one mff_stage1 call = five launches: k_stage1s for the
 streaming / OLS families x3, k_stage1g for the sorted families x2, plus the small exact
-list kernel), algorithmic bytes per pass = 5,354 B/stock-day (4,832 B OHLCV+mask in,
-58 x 9 B out) x local stock-days, over the pass's average duration from HIP
-events on its launch stream; peak 8.0 TB/s (MI355X_MICROARCH.md).  traffic: HBM bytes per
-pass from the committed rocprofv3 PMC passes (profiles/pmc_stage1.json: FETCH_SIZE x 2 per
-the gfx950 correction + WRITE_SIZE, summed over the launches), or null;
-traffic_calibrated: the same with the LDS-DMA kernels' factor measured by
-profiles/ubench/rowload.hip.  valu_util: SQ_INSTS_VALU x 4 cycles / (1,024 SIMDs x 2.4 GHz
-x pass time) from the same PMC passes (the pass is VALU / latency bound, not HBM bound).
+list kernel; and the doc_pdf sort / count on the side stream, whose tail the window
+includes), algorithmic bytes per pass = 5,354 B/stock-day (4,832 B OHLCV+mask in, 58 x
+9 B out) x local stock-days, over the pass's average duration from HIP
+events on its launch stream; peak 8.0 TB/s (MI355X_MICROARCH.md).  bound stays "hbm":
+the north star prices the pass against HBM bandwidth.  traffic: HBM bytes per pass from
+the committed rocprofv3 PMC passes (profiles/pmc_stage1.json: FETCH_SIZE x 2 per the
+gfx950 correction + WRITE_SIZE, summed over the launches), or null; traffic_calibrated:
+the same with the LDS-DMA kernels' factor measured by profiles/ubench/rowload.hip.
+valu: the issue side from the same PMC passes (VALU wave-instructions per stock-day,
+f64 share, fraction of the chip's VALU issue cycles) -- what actually binds the pass.
 
 cpu_baseline: the CPU oracle (oracle/mff_oracle.py, a numpy restatement of the reference
 cal_* functions) timed on this host, rank 0 at N=1, on a bounded sample of the same
@@ -55,6 +57,16 @@ def _oracle_day(args):
     return d
 
 
+def host_workers() -> int:
+    """Every host core this process may run on, like the reference's joblib
+    Parallel(n_jobs=-1) (MinuteFrequentFactorCICC.py:85-86): the CPU affinity set, capped by
+    the job's CPU share where the launcher states one (OMP_NUM_THREADS: the GPU box gives a
+    one-GPU job 16 of the host's cores while os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("MFF_CPU_WORKERS") or os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(share))) if share else max(1, n)
+
+
 def cpu_baseline(days: int, stocks: int, workers: int):
     """Oracle over `days` day-frames of `stocks` stocks, one task per day (fork pool)."""
     from mff import synth
@@ -66,7 +78,28 @@ def cpu_baseline(days: int, stocks: int, workers: int):
     dt = time.perf_counter() - t0
     return {"value": days * stocks / dt, "unit": "stock-days/s", "cores": workers, "kind": "port",
             "sample": f"{days} days x {stocks} stocks (all 58 factors, numpy oracle), "
-                      f"{workers} worker processes, one day frame per task; wall {dt:.2f} s"}
+                      f"{workers} worker processes (host reports {os.cpu_count()} CPUs), one day "
+                      f"frame per task; wall {dt:.2f} s"}
+
+
+def valu_roofline(pmc, k_ms: float, stock_days: int):
+    """The issue side of the pass from the committed PMC passes (profiles/pmc_stage1.json):
+    VALU wave-instructions per stock-day and the fraction of the chip's VALU issue
+    cycles they occupy (wave64 on a 32-lane SIMD: 2 cycles for 32-bit ops, 4 for f64 ops
+    at the 16-lane f64 rate; 1,024 SIMDs at 2.4 GHz)."""
+    if not pmc:
+        return None
+    sq = pmc.get("sq", {})
+    n = sq.get("SQ_INSTS_VALU")
+    if not n:
+        return None
+    f64 = sum(sq.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                        "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+    cyc = 2.0 * (n - f64) + 4.0 * f64
+    return {"valu_instr_per_stock_day": round(n / stock_days, 1),
+            "f64_share": round(f64 / n, 3),
+            "issue_frac": round(cyc / (1024 * 2.4e9 * k_ms * 1e-3), 3),
+            "pmc_round": pmc.get("round")}
 
 
 def load_pmc(S_loc: int, D: int):
@@ -167,7 +200,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--stocks", type=int, default=5000)
     ap.add_argument("--days", type=int, default=2500)
-    ap.add_argument("--cpu-days", type=int, default=16)
+    ap.add_argument("--cpu-days", type=int, default=32)
     ap.add_argument("--cpu-stocks", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
@@ -181,8 +214,7 @@ def main():
     # CPU baseline first, before anything touches the GPU (the pool forks).
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        workers = max(1, min(16, os.cpu_count() or 1, args.cpu_days))
-        cpu = cpu_baseline(args.cpu_days, args.cpu_stocks, workers)
+        cpu = cpu_baseline(args.cpu_days, args.cpu_stocks, host_workers())
 
     import torch
     from mff import catalog, dist, engine, synth
@@ -229,35 +261,57 @@ def main():
     pmc = load_pmc(S_loc, D)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     traffic_cal = pmc.get("hbm_bytes_calibrated") if pmc else None
-    valu = pmc.get("sq", {}).get("SQ_INSTS_VALU") if pmc else None
-    valu_util = round(valu * 4 / (1024 * 2.4e9 * k_ms * 1e-3), 3) if valu else None
+    valu = valu_roofline(pmc, k_ms, S_loc * D)
 
     extras = {}
     if not args.no_extras:
         val, state, _ = step()
         torch.cuda.synchronize()
-        def timed(fn):
-            fn()  # first call sizes the caching allocator; the timed call reuses its blocks
+
+        def timed(fn, reps=5):
+            """median wall ms of `reps` calls after one sizing call (the caching allocator)"""
+            fn()
             torch.cuda.synchronize()
-            t = time.perf_counter()
-            r = fn()
-            torch.cuda.synchronize()
-            return (time.perf_counter() - t) * 1e3, r
-        extras["stage1_kernel_ms"] = round(k_ms, 3)
+            ts = []
+            for _ in range(reps):
+                t = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append((time.perf_counter() - t) * 1e3)
+            return float(np.median(ts))
+        extras["stage1_pass_ms"] = round(k_ms, 3)
         extras["step_ms_rank0"] = round(elapsed / args.steps * 1e3, 3)
-        ms, _ = timed(lambda: engine.rolling(val, state, 20, "z"))
-        extras["stage2_z20_all58_ms"] = round(ms, 3)
-        # algorithmic bytes of stage 2 / stage-3 z: 8 + 1 B in and out per (factor, day, stock)
+        # algorithmic bytes of stage 2 / stage-3: 8 + 1 B in and out per (factor, day, stock)
         xs_bytes = 18.0 * val.numel()
+        ms = timed(lambda: engine.rolling(val, state, 20, "z"))
+        extras["stage2_z20_all58_ms"] = round(ms, 3)
         extras["stage2_z20_GBps"] = round(xs_bytes / (ms * 1e-3) / 1e9, 1)
-        ms, _ = timed(lambda: engine.cross_section(val, state, "z", comm=comm))
+        ms = timed(lambda: engine.cross_section(val, state, "z", comm=comm))
         extras["stage3_z_all58_ms"] = round(ms, 3)
         extras["stage3_z_GBps"] = round(xs_bytes / (ms * 1e-3) / 1e9, 1)
-        ms, _ = timed(lambda: engine.cross_section(val[:4], state[:4], "rank", comm=comm))
-        extras["stage3_rank_4factors_ms"] = round(ms, 3)
+        ms = timed(lambda: engine.cross_section(val, state, "rank", comm=comm), reps=3)
+        extras["stage3_rank_all58_ms"] = round(ms, 3)
+        extras["stage3_rank_GBps"] = round(xs_bytes / (ms * 1e-3) / 1e9, 1)
         del val, state
         if rank == 0:
             extras.update(ingest_extras(panel, args.ingest_days, args.ingest_host_days))
+        # c5: the same panel made ragged in place (suspension runs, missing bars, gap and
+        # flat zero-volume stock-days), one stage-1 pass timed like the headline
+        g = torch.Generator(device=dev)
+        g.manual_seed(20251029 + rank)
+        synth.make_ragged_device(panel.bars, panel.mask, g)
+        torch.cuda.synchronize()
+        step()
+        torch.cuda.synchronize()
+        if comm is not None:
+            comm.barrier()
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        t = time.perf_counter()
+        step(ev)
+        torch.cuda.synchronize()
+        rag_ms = (time.perf_counter() - t) * 1e3
+        extras["c5_ragged_stage1_ms"] = round(rag_ms, 3)
+        extras["c5_ragged_stock_days_per_s"] = round(S * D / (rag_ms * 1e-3))
 
     if rank == 0:
         res = {
@@ -287,9 +341,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_calibrated": traffic_cal,
-                "valu_util": valu_util,
+                "valu": valu,
                 "kernel": "stage-1 pass: k_stage1s<SEG|MOMR|TRD>, <MOMV|SUMV|SUMC|CORR>, <OLS|MOMH>, "
-                          "k_stage1g<ORD|ORDV>, <LVL|PDF> (+ k_stage1 exact list)",
+                          "k_stage1g<ORD|ORDV>, <LVL|PDF> (+ k_stage1 exact list) + doc_pdf "
+                          "sort/count (side stream, inside the window)",
                 "bytes_per_launch": bytes_launch,
                 "avg_kernel_ms": round(k_ms, 3),
             },

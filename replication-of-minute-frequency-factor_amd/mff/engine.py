@@ -86,7 +86,8 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
     """Stage 1 for the requested factors (default: all 58, reference order).
 
     ``events``: optional (start, end) torch.cuda.Event pair recorded on the launch stream
-    around the fused stage-1 kernel alone (bench.py's roofline timing).
+    around the whole stage-1 pass: every stage-1 launch and the doc_pdf rank phases
+    (the end event follows the side stream's doc_pdf tail; bench.py's roofline timing).
     Returns (val float64 [nf][D][S], state uint8 [nf][D][S], ids)."""
     lib = _lib.load()
     ids = catalog.resolve(names)
@@ -116,15 +117,15 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
         with torch.cuda.stream(side):
             pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
         _lib.check(lib.mff_stage1_part(*args, 2), "mff_stage1_part(2)")
-        if events is not None:
-            events[1].record(main)
         main.wait_stream(side)
+        if events is not None:  # after the doc_pdf tail on the side stream
+            events[1].record(main)
         return val, state, ids
     _lib.check(lib.mff_stage1(*args), "mff_stage1")
-    if events is not None:
-        events[1].record(main)
     if need_pdf:
         pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
+    if events is not None:
+        events[1].record(main)
     return val, state, ids
 
 

@@ -198,12 +198,49 @@ def make_panel_device(S: int, D: int, device, config: int = 3, day_chunk: int = 
     mask = torch.full((D, S, 8), -1, device=device, dtype=torch.int32)
     mask[..., 7] = 0xFFFF  # bars 224..239; bits 240..255 stay clear
     if ragged:
-        # suspended stock-days (3 %) and random missing bars (0.5 %)
-        sus = torch.rand((D, S), generator=g, device=device) < 0.03
-        keep = torch.rand((D, S, MINUTES), generator=g, device=device) >= 0.005
-        keep &= ~sus[..., None]
-        padded = torch.zeros((D, S, 256), dtype=torch.int64, device=device)
-        padded[..., :MINUTES] = keep.to(torch.int64)
-        words = (padded.view(D, S, 8, 32) << torch.arange(32, device=device, dtype=torch.int64)).sum(-1)
-        mask = torch.where(words >= 2 ** 31, words - 2 ** 32, words).to(torch.int32)
+        make_ragged_device(bars, mask, g, day_chunk=day_chunk)
     return bars, mask
+
+
+def make_ragged_device(bars, mask, g, day_chunk: int = 50) -> None:
+    """The c5 ragged panel, in place on a dense device panel, same recipe
+    as the host :func:`_make_ragged`: 3 % of stock-days suspended in contiguous runs of
+    1..10 days, 0.5 % of bars missing at random, 5 contiguous-gap stock-days (a 5..59-bar
+    hole) per 1,000, 0.2 % flat stock-days with zero volume.  Works day-chunk by
+    day-chunk (the bit masks of a chunk only)."""
+    import torch
+
+    dev = bars.device
+    _, D, S, _ = bars.shape
+    # suspension runs: start (d0, s) with probability 0.03 / 5.5 (mean run 5.5 days)
+    start = torch.rand((D, S), generator=g, device=dev) < 0.03 / 5.5
+    run = torch.randint(1, 11, (D, S), generator=g, device=dev)
+    sus = torch.zeros((D, S), dtype=torch.bool, device=dev)
+    dd, ss = start.nonzero(as_tuple=True)
+    rr = run[dd, ss]
+    for k in range(10):  # day offset k of every run that is longer than k
+        sel = rr > k
+        d = dd[sel] + k
+        ok = d < D
+        sus[d[ok], ss[sel][ok]] = True
+    gap = torch.rand((D, S), generator=g, device=dev) < 0.005
+    ga = torch.randint(0, MINUTES - 10, (D, S), generator=g, device=dev)
+    gl = torch.randint(5, 60, (D, S), generator=g, device=dev)
+    flat = torch.rand((D, S), generator=g, device=dev) < 0.002
+    mm = torch.arange(MINUTES, device=dev)
+    shifts = torch.arange(32, device=dev, dtype=torch.int64)
+    for d0 in range(0, D, day_chunk):
+        d1 = min(D, d0 + day_chunk)
+        keep = torch.rand((d1 - d0, S, MINUTES), generator=g, device=dev) >= 0.005
+        hole = gap[d0:d1, :, None] & (mm >= ga[d0:d1, :, None]) & (mm < ga[d0:d1, :, None] + gl[d0:d1, :, None])
+        keep &= ~hole & ~sus[d0:d1, :, None]
+        padded = torch.zeros((d1 - d0, S, 256), dtype=torch.int64, device=dev)
+        padded[..., :MINUTES] = keep.to(torch.int64)
+        words = (padded.view(d1 - d0, S, 8, 32) << shifts).sum(-1)
+        mask[d0:d1] = torch.where(words >= 2 ** 31, words - 2 ** 32, words).to(torch.int32)
+        fd, fs = flat[d0:d1].nonzero(as_tuple=True)
+        if fd.numel():
+            px = bars[3, d0 + fd, fs, 0]
+            for k in range(4):
+                bars[k, d0 + fd, fs, :] = px[:, None]
+            bars[4, d0 + fd, fs, :] = 0.0

@@ -1,0 +1,124 @@
+"""GPU parity at the benchmark sizes (BASELINE configs c4 and c5), by sampling.
+
+c4: the bench panel itself, 5,000 stocks x 240 min x 2,500 days resident in HBM (plane
+    index of the last stock-day ~3.0e9 > 2^31): one stage-1 pass of all 58 factors;
+    256 sampled stock-days (early, middle and the last days, the first and last stock)
+    against the oracle for every non-doc_pdf factor, and doc_pdf (frame-wide rank over
+    all 5,000 codes) on the last day.
+c5: the ragged panel (suspension runs, missing bars, gap days, flat zero-volume days),
+    5,000 x 250: stage 1 sampled the same way, doc_pdf on one day, and the 20-day rolling
+    m / z / std (stage 2) of the correlation family and realized vol over the whole
+    history of 12 stocks against oracle_stage1 -> oracle_stage2.
+"""
+import numpy as np
+import pytest
+
+from parity import compare
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def _host_sub(bars, mask, days, stocks):
+    """Device panel -> host panel dict (oracle input) for the given days x stocks."""
+    from mff import synth
+    di = torch.as_tensor(days, device=bars.device)
+    si = torch.as_tensor(stocks, device=bars.device)
+    b = bars.index_select(1, di).index_select(2, si).cpu().numpy()
+    m = mask.index_select(0, di).index_select(1, si).cpu().numpy().view(np.uint32)
+    pres = synth.unpack_mask(m)
+    out = {k: np.where(pres, b[f], np.float32(np.nan)).astype(np.float32)
+           for f, k in enumerate(("open", "high", "low", "close", "volume"))}
+    out["present"] = pres
+    out["codes"] = [f"{s:06d}.SZ" for s in stocks]
+    out["dates"] = list(days)
+    return out
+
+
+def _gpu_rows(val, state, days, stocks, rows):
+    di = torch.as_tensor(days, device=val.device)
+    si = torch.as_tensor(stocks, device=val.device)
+    ri = torch.as_tensor(rows, device=val.device)
+    pick = lambda t: t.index_select(0, ri).index_select(1, di).index_select(2, si).cpu().numpy()
+    return pick(val), pick(state)
+
+
+def _sampled_stage1(bars, mask, val, state, days, stocks):
+    import mff_oracle as O
+    from mff import catalog
+    names = [n for n in catalog.NAMES if not n.startswith("doc_pdf")]
+    ov, os_ = O.oracle_stage1(_host_sub(bars, mask, days, stocks), names)
+    gv, gs = _gpu_rows(val, state, days, stocks, [catalog.ID[n] for n in names])
+    bad = []
+    for r, nm in enumerate(names):
+        bad += compare(gv[r], gs[r], ov[r], os_[r], nm)
+    return bad
+
+
+def _pdf_day(bars, mask, val, state, d):
+    import mff_oracle as O
+    from mff import catalog
+    S = bars.shape[2]
+    names = [n for n in catalog.NAMES if n.startswith("doc_pdf")]
+    ov, os_ = O.oracle_stage1(_host_sub(bars, mask, [d], list(range(S))), names)
+    gv, gs = _gpu_rows(val, state, [d], list(range(S)), [catalog.ID[n] for n in names])
+    bad = []
+    for r, nm in enumerate(names):
+        bad += compare(gv[r], gs[r], ov[r], os_[r], f"{nm}/day{d}", rtol=0.0, atol=0.0)
+    return bad
+
+
+def test_c4_full_panel_sampled(dev):
+    from mff import engine, synth
+    S, D = 5000, 2500
+    assert (D - 1) * S * 240 > 2 ** 31  # the far end of a plane is past 32-bit indexing
+    bars, mask = synth.make_panel_device(S, D, dev, config=4)
+    val, state, _ = engine.compute_factors(engine.DevicePanel(bars, mask))
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(44)
+    days = [0, 1, D // 2, D - 250, D - 17, D - 3, D - 2, D - 1]
+    stocks = sorted({0, S - 1} | set(rng.choice(np.arange(1, S - 1), 30, replace=False).tolist()))
+    bad = _sampled_stage1(bars, mask, val, state, days, stocks)
+    bad += _pdf_day(bars, mask, val, state, D - 1)
+    assert not bad, "\n".join(bad[:30])
+
+
+def test_c5_ragged_panel_sampled_and_rolling(dev):
+    import mff_oracle as O
+    from mff import catalog, engine, synth
+    S, D = 5000, 250
+    bars, mask = synth.make_panel_device(S, D, dev, config=5, ragged=True)
+    val, state, _ = engine.compute_factors(engine.DevicePanel(bars, mask))
+    torch.cuda.synchronize()
+    # the ragged recipe really is in the panel
+    st0 = state[catalog.ID["vol_volume1min"]]
+    assert 0.01 < float((st0 == 0).double().mean()) < 0.05  # suspended stock-days
+    rng = np.random.default_rng(55)
+    days = [0, 1, 57, 120, 200, D - 2, D - 1, int(rng.integers(D))]
+    stocks = sorted({0, S - 1} | set(rng.choice(np.arange(1, S - 1), 30, replace=False).tolist()))
+    bad = _sampled_stage1(bars, mask, val, state, days, stocks)
+    bad += _pdf_day(bars, mask, val, state, D - 1)
+    # stage 2, N = 20, over the whole history of 12 stocks
+    names = ["corr_prv", "corr_prvr", "corr_pv", "corr_pvd", "corr_pvl", "corr_pvr", "vol_return1min"]
+    hist = sorted({S - 1} | set(rng.choice(S - 1, 11, replace=False).tolist()))
+    ov, os_ = O.oracle_stage1(_host_sub(bars, mask, list(range(D)), hist), names)
+    rows = [catalog.ID[n] for n in names]
+    ri = torch.as_tensor(rows, device=dev)
+    si = torch.as_tensor(hist, device=dev)
+    v1 = val.index_select(0, ri).contiguous()
+    s1 = state.index_select(0, ri).contiguous()
+    for meth in ("m", "z", "std"):
+        rv, rs = engine.rolling(v1, s1, 20, meth)
+        gv = rv.index_select(2, si).cpu().numpy()
+        gs = rs.index_select(2, si).cpu().numpy()
+        for r, nm in enumerate(names):
+            ev, es = O.oracle_stage2(ov[r], os_[r], 20, meth)
+            bad += compare(gv[r], gs[r], ev, es, f"{nm}/20/{meth}", atol=1e-9)
+    assert not bad, "\n".join(bad[:30])
