@@ -122,3 +122,149 @@ def test_gloo_all_to_all_world2():
     out = dist.run_threads(3, lambda c: c.all_to_all(
         torch.stack([torch.tensor([10.0 * c.rank + r]) for r in range(3)])))
     assert [o.squeeze(1).tolist() for o in out] == [[0.0, 10.0, 20.0], [1.0, 11.0, 21.0], [2.0, 12.0, 22.0]]
+
+
+# --------------------------------------------------------------------------------------
+# The stock-sharded doc_pdf exchange (engine._pdf_ranks_sharded) end to end at world 2:
+# the real exchange code and torch.distributed (gloo) collectives, with numpy stand-ins
+# for the four device phases (sort / count / origin / finalize; their GPU versions are
+# checked in tests/test_gpu_*.py), against the unsharded oracle's frame-wide ranks.
+
+def _ord64(x):
+    import numpy as np
+    b = np.asarray(x, dtype=np.float64).view(np.uint64)
+    neg = (b >> np.uint64(63)) == 1
+    out = np.where(neg, ~b, b | np.uint64(1 << 63))
+    return np.where(np.isnan(x), np.uint64(0xFFFFFFFFFFFFFFFF), out)
+
+
+def _pdf_queries(panel):
+    """[5][D][S] threshold level keys c_last / c per the oracle's rule (CM:1018-1026: levels
+    in ascending rank = ascending key order, first cumulative share > p), NaN = none."""
+    import numpy as np
+    import mff_oracle as O
+    D, S = panel["present"].shape[:2]
+    q = np.full((5, D, S), np.nan)
+    for d in range(D):
+        for s in range(S):
+            pr = panel["present"][d, s]
+            if not pr.any():
+                continue
+            c = panel["close"][d, s][pr].astype(np.float64)
+            v = panel["volume"][d, s][pr].astype(np.float64)
+            with np.errstate(all="ignore"):
+                key = c[-1] / c
+                vd = v / v.sum()
+            lv = {}
+            for k, x in zip(key.tolist(), vd.tolist()):
+                lv[k] = lv.get(k, 0.0) + x
+            for t, p in enumerate((0.6, 0.7, 0.8, 0.9, 0.95)):
+                cum = 0.0
+                for k in sorted(lv):
+                    cum = cum + lv[k]
+                    if O.tot_gt(cum, p) is True:
+                        q[t, d, s] = k
+                        break
+    return q
+
+
+class _NumpyPdf:
+    def __init__(self, sub, val, state, rows):
+        import numpy as np
+        self.val, self.state, self.rows = val, state, rows
+        D = sub["present"].shape[0]
+        self.keys = []
+        for d in range(D):
+            ks = []
+            for s in range(sub["present"].shape[1]):
+                pr = sub["present"][d, s]
+                if pr.any():
+                    c = sub["close"][d, s][pr].astype(np.float64)
+                    ks.append(c[-1] / c)
+            self.keys.append(np.sort(_ord64(np.concatenate(ks))) if ks else np.zeros(0, np.uint64))
+
+    def sort(self, q_all, R, S_all, nd):
+        import numpy as np
+        a = q_all.numpy()[:, :, :nd]  # [R][5][nd][S_all]
+        out = np.sort(_ord64(np.moveaxis(a, 2, 0).reshape(nd, -1)), axis=1)
+        return torch.from_numpy(out.view(np.int64).copy())
+
+    def count(self, q_sorted):
+        import numpy as np
+        qs = q_sorted.numpy().view(np.uint64)
+        out = np.zeros(qs.shape, np.int32)
+        for d in range(qs.shape[0]):
+            k = self.keys[d]
+            lt = np.searchsorted(k, qs[d], side="left")
+            le = np.searchsorted(k, qs[d], side="right")
+            out[d] = 2 * lt + (le - lt)
+        return torch.from_numpy(out)
+
+    def origin(self, q_all, R, S_all, q_sorted, counts):
+        import numpy as np
+        qa = q_all.numpy()
+        qs = q_sorted.numpy().view(np.uint64)
+        cn = counts.numpy()
+        out = np.zeros(qa.shape, np.int32)
+        for dd in range(qa.shape[2]):
+            x = qa[:, :, dd]
+            j = np.searchsorted(qs[dd], _ord64(x), side="left").clip(0, qs.shape[1] - 1)
+            out[:, :, dd] = np.where(np.isnan(x), 0, cn[dd][j])
+        return torch.from_numpy(out)
+
+    def finalize(self, q_local, own):
+        import numpy as np
+        q, c = q_local.numpy(), own.numpy()
+        for t, r in enumerate(self.rows):
+            ok = ~np.isnan(q[t])
+            self.val[r][ok] = (c[t][ok] + 1.0) * 0.5
+            self.state[r][ok] = 2
+
+
+def _pdf_worker(rank, world, port, resq):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "replication-of-minute-frequency-factor_amd"), os.path.join(root, "oracle"),
+              os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import numpy as np
+    from mff import dist, engine, synth
+    comm, _ = dist.init_from_env(backend="gloo")
+    panel = synth.make_panel(13, 5, config=41, ragged=True)  # 5 days over 2 ranks: uneven blocks
+    s0, s1 = dist.shard_bounds(13, world, rank)
+    sub = synth.subpanel(panel, stocks=slice(s0, s1))
+    q = torch.from_numpy(_pdf_queries(sub))
+    val = np.zeros((5, 5, s1 - s0))
+    state = np.zeros((5, 5, s1 - s0), np.uint8)
+    S_all = engine._agreed_max(comm, s1 - s0, torch.device("cpu"))
+    engine._pdf_ranks_sharded(comm, q, S_all, _NumpyPdf(sub, val, state, list(range(5))))
+    comm.barrier()
+    dist_.destroy_process_group()
+    resq.put((rank, (val, state)))
+
+
+def test_gloo_sharded_doc_pdf_exchange_world2():
+    import numpy as np
+    import mff_oracle as O
+    from mff import synth
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_pdf_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    val = np.concatenate([res[0][0], res[1][0]], axis=2)
+    state = np.concatenate([res[0][1], res[1][1]], axis=2)
+    panel = synth.make_panel(13, 5, config=41, ragged=True)
+    names = [f"doc_pdf{p}" for p in (60, 70, 80, 90, 95)]
+    ov, os_ = O.oracle_stage1(panel, names)
+    for t in range(5):
+        ok = os_[t] == O.VALUE
+        assert (state[t][ok] == 2).all(), names[t]
+        assert np.array_equal(val[t][ok], ov[t][ok]), names[t]

@@ -120,3 +120,43 @@ def test_sharded_ranks_match_unsharded_oracle(dev, panel_and_oracle, R):
             bad += compare(v[i], s[i], xv, xs, f"{nm}/xs-{kind}", rtol=1e-6 if kind == "z" else 0.0,
                            atol=1e-9 if kind == "z" else 0.0)
     assert not bad, "\n".join(bad[:20])
+
+
+def test_incremental_update_through_gpu_batches(dev, tmp_path):
+    """MF:62-66, 79-81, 102-110 through the GPU day-file batches: an exposure of the
+    first days is saved (atomic to_parquet), new day files arrive, a second
+    cal_exposure_by_min_data reads the saved exposure, runs ONLY the new files through
+    the stage-1 kernel and concatenates; the result equals the oracle over all days, and
+    the rolling stage over the combined history uses the N-1 days before the first new day."""
+    import mff_oracle as O
+    from MinuteFrequentFactorCICC import MinFreqFactor
+    import MinuteFrequentFactorCalculateMethodsCICC as CM
+    from mff import synth
+    panel = synth.make_panel(24, 9, config=23, ragged=True)
+    folder = tmp_path / "kl"
+    folder.mkdir()
+    (tmp_path / "exp").mkdir()
+    write_day_files(synth.subpanel(panel, days=slice(0, 6)), str(folder))
+    name = "corr_pvr"
+    f = MinFreqFactor(name)
+    f.cal_exposure_by_min_data(CM.cal_corr_pvr, path=str(tmp_path / "exp"), folder_path=str(folder),
+                               batch_days=4)
+    f.to_parquet(str(tmp_path / "exp"))
+    n_old = len(f.factor_exposure)
+    # new files; an old file is rewritten with garbage: it must NOT be recomputed
+    write_day_files(synth.subpanel(panel, days=slice(6, 9)), str(folder))
+    first = sorted(os.listdir(folder))[0]
+    (folder / first).write_bytes(b"not parquet any more")
+    g = MinFreqFactor(name)
+    g.cal_exposure_by_min_data(CM.cal_corr_pvr, path=str(tmp_path / "exp"), folder_path=str(folder),
+                               batch_days=2)
+    assert len(g.factor_exposure) > n_old
+    assert g.factor_exposure["date"].is_monotonic_increasing
+    ov, os_ = O.oracle_stage1(panel, [name])
+    v, s = _dense(g.factor_exposure, name, panel)
+    assert not compare(v, s, ov[0], os_[0], name)
+    for meth in ("m", "z"):
+        out = g.cal_final_exposure(4, meth, mode="days")
+        v, s = _dense(out, f"{name}_4_{meth}", panel)
+        rv, rs = O.oracle_stage2(ov[0], os_[0], 4, meth)
+        assert not compare(v, s, rv, rs, f"{name}_4_{meth}", atol=1e-9)
