@@ -47,6 +47,10 @@ def main():
     nb = nbytes
     nbytes = nb * 8 / 58
     res["stage3_rank_8factors"] = t(lambda: engine.cross_section(val[:8], state[:8], "rank"))
+    for impl in ("b256", "b512", "sort"):
+        os.environ["MFF_XS_RANK_IMPL"] = impl
+        res[f"stage3_rank_8factors_{impl}"] = t(lambda: engine.cross_section(val[:8], state[:8], "rank"))
+    del os.environ["MFF_XS_RANK_IMPL"]
     nbytes = nb
     print(json.dumps(res), flush=True)
 

@@ -11,6 +11,8 @@
 // [R][rows][D][3] (a few MB) and a Chan combine in rank order (exact for constant
 // columns); rank needs the other ranks' values -> all-gather of the columns, then a
 // one-workgroup sort per (row, day) and two binary searches per own stock.
+#include <stdlib.h>
+
 #include "../../include/mff.h"
 #include "mff_internal.h"
 #include "mff_sort.h"
@@ -218,20 +220,24 @@ struct XsLoader {
     const int r = i / S, s = i % S;
     const size_t o = ((size_t)r * rseg + seg) * S + s;
     const double x = v[o];
-    return included(x, st[o]) ? ord64(x) : ~0ull;
+    return included(x, st[o]) ? ord64(x == 0.0 ? 0.0 : x) : ~0ull;  // -0 ranks as +0
   }
 };
 
 __global__ __launch_bounds__(SORT_THREADS) void k_xs_rank(const double* val, const uint8_t* state, int rows,
                                                            int D, int S, const double* val_all,
                                                            const uint8_t* state_all, int R, int S_all,
-                                                           double* out_val, uint8_t* out_state, uint64_t* ws) {
+                                                           double* out_val, uint8_t* out_state, uint64_t* ws,
+                                                           const uint32_t* list) {
   __shared__ uint64_t sk[SORT_CAP];
   const int M = R * S_all;
   const size_t nseg = (size_t)rows * D;
   uint64_t* srt = ws + (size_t)blockIdx.x * 2 * M;
   uint64_t* tmp = srt + M;
-  for (size_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+  // list (optional): [count, seg ...] -- only the segments the bucketed kernel handed over
+  const size_t nwork = list ? (size_t)list[0] : nseg;
+  for (size_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+    const size_t seg = list ? (size_t)list[1 + w] : w;
     XsLoader ld{val_all, state_all, nseg, (int)seg, S_all};
     const uint64_t* sorted;
     if (M <= SORT_CAP) {
@@ -256,11 +262,253 @@ __global__ __launch_bounds__(SORT_THREADS) void k_xs_rank(const double* val, con
         out_state[o] = sx;
         continue;
       }
-      const uint64_t k = ord64(x);
+      const uint64_t k = ord64(x == 0.0 ? 0.0 : x);
       const int lb = lower_bound_u64(sorted, 0, M, k);
       const int ub = upper_bound_u64(sorted, lb, M, k);
       out_val[o] = (double)lb + (double)(ub - lb + 1) * 0.5;
       out_state[o] = MFF_STATE_VALUE;
+    }
+    __syncthreads();
+  }
+}
+
+// Bucketed rank (M = R * S_all <= XR_PER * XR_THREADS values per (row, day)): no sort.  The
+// included values are binned by a monotone bucket function, the buckets scanned into
+// start offsets and the keys scattered bucket by bucket into LDS; the rank of x is then
+//   #values in lower buckets + #smaller keys in its own bucket + (#equal keys + 1) / 2
+// (S6 average rank, exact: every in-bucket comparison is on the full total-order key,
+// with -0 taken as +0 like the value comparison of the oracle).  Two bucket functions
+// are tried in turn, each a histogram pass over the segment:
+//   linear  in the value between the finite min and max (uniform / normal columns);
+//   log     per sign, linear in the IEEE bits above the smallest magnitude (a
+//           log-scale histogram: heavy tails, several decades), zero its own bucket;
+// -inf / +inf take the first / last bucket in both.  A segment whose largest bucket
+// still holds more than XR_MAXB keys (heavy ties) is appended to a list for the
+// sorting kernel (k_xs_rank).
+constexpr int XR_NB = 2048;
+constexpr int XR_PER = 8;
+constexpr int XR_THREADS = 1024;  // default block; XR_THREADS is also the kernel template parameter
+constexpr int XR_MAXB = 48;
+
+__global__ void k_xs_rank_list_init(uint32_t* list) { list[0] = 0u; }
+
+struct XrBucket {
+  int scheme;        // 0 linear, 1 log
+  double xmin, scale;
+  uint64_t nlo, plo;
+  int shn, shp;
+  // bucket of an included value x (x canonical: no -0)
+  __device__ __forceinline__ uint32_t operator()(double x) const {
+    if (x == -__builtin_inf()) return 0u;
+    if (x == __builtin_inf()) return XR_NB - 1;
+    if (scheme == 0) {
+      const double t = (x - xmin) * scale;
+      const int b = (int)t;  // t >= 0 and finite here
+      return 1u + (uint32_t)min(b, XR_NB - 3);
+    }
+    constexpr uint32_t N1 = (XR_NB - 4) / 2;  // buckets per sign
+    if (x == 0.0) return N1 + 1u;
+    const uint64_t m = (uint64_t)__double_as_longlong(fabs(x));
+    if (x < 0.0) return N1 - (uint32_t)((m - nlo) >> shn);  // 1 .. N1, larger |x| lower
+    return N1 + 2u + (uint32_t)((m - plo) >> shp);          // N1+2 .. 2 N1 + 1
+  }
+};
+
+__device__ __forceinline__ int xr_shift(uint64_t span, int bits) {  // (span >> sh) < 2^bits
+  return span == 0ull ? 0 : max(0, 64 - __builtin_clzll(span) - bits);
+}
+
+// LOCAL (one rank: val_all == val, S_all == S): the own elements are the loaded ones, so
+// the output pass works from registers, and the next segment's values are loaded while
+// this one is ranked.  Per element a thread keeps only the canonical value (-0 -> +0),
+// the state byte (the output of an excluded VALUE is NaN: VALUE and not included means
+// NaN), its bucket and its slot in the bucket.
+template <int PER, bool LOCAL, int XR_THREADS>
+__global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREADS) void k_xs_rank_bucket(const double* val, const uint8_t* state, int rows,
+                                                                   int D, int S, const double* val_all,
+                                                                   const uint8_t* state_all, int R, int S_all,
+                                                                   double* out_val, uint8_t* out_state,
+                                                                   uint32_t* list) {
+  __shared__ uint64_t sk[PER * XR_THREADS];
+  __shared__ uint32_t bins[XR_NB];
+  __shared__ unsigned long long mm[6];  // finite min / max (ord64), neg |x| bits min / max, pos bits min / max
+  __shared__ uint32_t wsum[XR_THREADS / 64];
+  __shared__ uint32_t ctl[2];
+  const int M = R * S_all;
+  const size_t nseg = (size_t)rows * D;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int BPT = XR_NB / XR_THREADS;
+  constexpr int NW = (PER + 3) / 4;  // state bytes packed 4 per word
+  double nx[PER];
+  uint32_t ns[NW];
+  const int r0 = tid / S_all, c0 = tid - r0 * S_all;  // (rank, column) of element tid
+  auto load = [&](size_t seg) {
+    int r = r0, cl = c0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) ns[w] = 0u;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + j * XR_THREADS;
+      nx[j] = 0.0;
+      if (i < M && seg < nseg) {
+        const size_t o = LOCAL ? seg * S_all + i : ((size_t)r * nseg + seg) * S_all + cl;
+        nx[j] = val_all[o];
+        ns[j >> 2] |= (uint32_t)state_all[o] << (8 * (j & 3));
+      }
+      if (!LOCAL) {  // element i + XR_THREADS
+        cl += XR_THREADS;
+        while (cl >= S_all) { cl -= S_all; ++r; }
+      }
+    }
+  };
+  auto stats = [&](int q0, int q1, const double (&x)[PER], uint32_t inc) {
+#pragma unroll 1
+    for (int q = q0; q < q1; ++q) {
+      const bool mx = q & 1;
+      uint64_t a = mx ? 0ull : ~0ull;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const double c = x[j];
+        const bool use = ((inc >> j) & 1u) && __builtin_isfinite(c) && (q < 2 || (q < 4 ? c < 0.0 : c > 0.0));
+        const uint64_t k = q < 2 ? ord64(c) : (uint64_t)__double_as_longlong(fabs(c));
+        if (use) a = mx ? max(a, k) : min(a, k);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = (uint64_t)__shfl_xor((long long)a, o, 64);
+        a = mx ? max(a, y) : min(a, y);
+      }
+      if (lane == 0) {
+        if (mx) atomicMax(&mm[q], (unsigned long long)a);
+        else atomicMin(&mm[q], (unsigned long long)a);
+      }
+    }
+  };
+  if (LOCAL) load(blockIdx.x);
+  for (size_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    if (!LOCAL) load(seg);
+    double x[PER];
+    uint32_t inc = 0u, stv = 0u, stn = 0u;  // included; state VALUE; state NULL
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t sb = (ns[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+      const bool in = included(nx[j], (uint8_t)sb);
+      x[j] = in ? (nx[j] == 0.0 ? 0.0 : nx[j]) : 0.0;  // -0 -> +0
+      inc |= (in ? 1u : 0u) << j;
+      stv |= (sb == MFF_STATE_VALUE ? 1u : 0u) << j;
+      stn |= (sb == MFF_STATE_NULL ? 1u : 0u) << j;
+    }
+    if (LOCAL) load(seg + gridDim.x);  // in flight while this segment is ranked
+    if (tid < 6) mm[tid] = (tid & 1) ? 0ull : ~0ull;
+    __syncthreads();
+    stats(0, 2, x, inc);  // finite min / max; the log scheme's stats only if linear fails
+    __syncthreads();
+    XrBucket bk;
+    const bool fin = mm[0] != ~0ull;
+    bk.xmin = fin ? unord64(mm[0]) : 0.0;
+    const double xmax = fin ? unord64(mm[1]) : 0.0;
+    const double range = xmax - bk.xmin;
+    bk.scale = range > 0.0 ? (double)(XR_NB - 2) / range : 0.0;
+    bk.nlo = bk.plo = 0ull;
+    bk.shn = bk.shp = 0;
+    uint32_t bp[PER];  // bucket << 16 | slot in the bucket
+    uint32_t c[BPT], off = 0u, tot = 0u;
+    bool ok = false;
+    for (int scheme = (__builtin_isfinite(range) ? 0 : 1); scheme < 2 && !ok; ++scheme) {
+      bk.scheme = scheme;
+      if (scheme == 1) {
+        stats(2, 6, x, inc);
+        __syncthreads();
+        bk.nlo = mm[2];
+        bk.plo = mm[4];
+        bk.shn = xr_shift(mm[2] == ~0ull ? 0ull : mm[3] - mm[2], 10);  // < 1022 buckets per sign
+        bk.shp = xr_shift(mm[4] == ~0ull ? 0ull : mm[5] - mm[4], 10);
+      }
+      for (int b = tid; b < XR_NB; b += XR_THREADS) bins[b] = 0u;
+      if (tid == 0) ctl[0] = 0u;
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const uint32_t b = bk(x[j]);
+        bp[j] = ((inc >> j) & 1u) ? (b << 16) | atomicAdd(&bins[b], 1u) : 0u;
+      }
+      __syncthreads();
+      uint32_t loc = 0u, mb = 0u;
+#pragma unroll
+      for (int q = 0; q < BPT; ++q) {
+        c[q] = bins[BPT * tid + q];
+        loc += c[q];
+        mb = max(mb, c[q]);
+      }
+      uint32_t incl = loc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mb = max(mb, (uint32_t)__shfl_xor((int)mb, o, 64));
+      if (lane == 63) wsum[wave] = incl;
+      if (lane == 0) atomicMax(&ctl[0], mb);
+      __syncthreads();
+      off = incl - loc;
+      tot = 0u;
+      for (int w = 0; w < XR_THREADS / 64; ++w) {
+        off += w < wave ? wsum[w] : 0u;
+        tot += wsum[w];
+      }
+      ok = ctl[0] <= (uint32_t)XR_MAXB;  // block-uniform
+      __syncthreads();
+    }
+    if (!ok) {  // hand the segment to the sorting kernel
+      if (tid == 0) list[1 + atomicAdd(&list[0], 1u)] = (uint32_t)seg;
+      continue;
+    }
+#pragma unroll
+    for (int q = 0; q < BPT; ++q) {
+      bins[BPT * tid + q] = off;
+      off += c[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if ((inc >> j) & 1u) sk[bins[bp[j] >> 16] + (bp[j] & 0xFFFFu)] = ord64(x[j]);
+    __syncthreads();
+    auto rank_of = [&](double cv, uint32_t b) {
+      const uint64_t kk = ord64(cv);
+      const uint32_t b0 = bins[b], b1 = b + 1 < (uint32_t)XR_NB ? bins[b + 1] : tot;
+      uint32_t less = b0, eq = 0u;
+      for (uint32_t q = b0; q < b1; ++q) {
+        const uint64_t y = sk[q];
+        less += y < kk ? 1u : 0u;
+        eq += y == kk ? 1u : 0u;
+      }
+      return (double)less + (double)(eq + 1u) * 0.5;
+    };
+    if constexpr (LOCAL) {
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const int s = tid + j * XR_THREADS;
+        if (s >= S) break;
+        const size_t o = seg * S + s;
+        const bool in = (inc >> j) & 1u, vl = (stv >> j) & 1u;
+        out_val[o] = in ? rank_of(x[j], bp[j] >> 16) : (vl ? qnan() : 0.0);
+        out_state[o] = vl ? MFF_STATE_VALUE : ((stn >> j) & 1u) ? MFF_STATE_NULL : MFF_STATE_ABSENT;
+      }
+    } else {
+      for (int s = tid; s < S; s += XR_THREADS) {
+        const size_t o = seg * S + s;
+        const double v = val[o];
+        const uint8_t sx = state[o];
+        if (!included(v, sx)) {
+          out_val[o] = (sx == MFF_STATE_VALUE) ? v : 0.0;
+          out_state[o] = sx;
+          continue;
+        }
+        const double cv = v == 0.0 ? 0.0 : v;
+        out_val[o] = rank_of(cv, bk(cv));
+        out_state[o] = MFF_STATE_VALUE;
+      }
     }
     __syncthreads();
   }
@@ -327,7 +575,9 @@ size_t mff_xs_rank_workspace_bytes(int rows, int D, int S_all, int R) {
   const long long nseg = (long long)rows * D;
   const long long g = nseg < XS_RANK_GRID ? nseg : XS_RANK_GRID;
   const long long M = (long long)R * S_all;
-  return M <= SORT_CAP ? 256 : (size_t)(g * 2 * M * 8);
+  const size_t sort = M <= SORT_CAP ? 256 : (size_t)(g * 2 * M * 8);
+  const size_t lst = ((size_t)(nseg + 1) * 4 + 255) & ~(size_t)255;  // bucketed kernel's hand-over list
+  return sort + lst;
 }
 
 int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_loc, const double* val_all,
@@ -339,8 +589,38 @@ int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_
               "mff_xs_rank: NULL buffer");
   const long long nseg = (long long)rows * D;
   const int g = (int)(nseg < XS_RANK_GRID ? nseg : XS_RANK_GRID);
-  hipLaunchKernelGGL(k_xs_rank, dim3(g), dim3(SORT_THREADS), 0, as_stream(stream), val, state, rows, D, S_loc,
-                     val_all, state_all, R, S_all, out_val, out_state, reinterpret_cast<uint64_t*>(workspace));
+  const long long M = (long long)R * S_all;
+  uint64_t* sortws = reinterpret_cast<uint64_t*>(workspace);
+  uint32_t* list = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(workspace) +
+                                               (M <= SORT_CAP ? 256 : (size_t)g * 2 * M * 8));
+  hipStream_t st = as_stream(stream);
+  // MFF_XS_RANK_IMPL=sort: every segment through the sorting kernel (A/B timing)
+  const char* impl = getenv("MFF_XS_RANK_IMPL");
+  if (M <= (long long)XR_PER * XR_THREADS && !(impl && impl[0] == 's')) {
+    MFF_REQUIRE(nseg < (1ll << 32), "mff_xs_rank: too many segments");
+    hipLaunchKernelGGL(k_xs_rank_list_init, dim3(1), dim3(1), 0, st, list);
+    const int gb = (int)(nseg < 4 * XS_RANK_GRID ? nseg : 4 * XS_RANK_GRID);
+    // MFF_XS_RANK_IMPL=b512 / b256: other block sizes (A/B timing; 1024 measured fastest:
+    // 8 factors at c4 1.19 ms vs 1.35 (512) and 1.71 (256))
+    const int thr = (impl && impl[0] == 'b') ? atoi(impl + 1) : XR_THREADS;
+    auto kern = k_xs_rank_bucket<10, true, 512>;
+    if (thr == 1024) kern = R == 1 ? (M <= 5 * 1024 ? k_xs_rank_bucket<5, true, 1024> : k_xs_rank_bucket<8, true, 1024>)
+                                   : (M <= 5 * 1024 ? k_xs_rank_bucket<5, false, 1024> : k_xs_rank_bucket<8, false, 1024>);
+    else if (thr == 256) kern = R == 1 ? (M <= 20 * 256 ? k_xs_rank_bucket<20, true, 256> : k_xs_rank_bucket<32, true, 256>)
+                                       : (M <= 20 * 256 ? k_xs_rank_bucket<20, false, 256> : k_xs_rank_bucket<32, false, 256>);
+    else kern = R == 1 ? (M <= 10 * 512 ? k_xs_rank_bucket<10, true, 512> : k_xs_rank_bucket<16, true, 512>)
+                       : (M <= 10 * 512 ? k_xs_rank_bucket<10, false, 512> : k_xs_rank_bucket<16, false, 512>);
+    hipLaunchKernelGGL(kern, dim3(gb), dim3(thr), 0, st, val, state, rows, D, S_loc, val_all,
+                       state_all, R, S_all, out_val, out_state, list);
+    MFF_LAUNCH_CHECK();
+    // the handed-over segments (the list's count is read on the device)
+    hipLaunchKernelGGL(k_xs_rank, dim3(g), dim3(SORT_THREADS), 0, st, val, state, rows, D, S_loc, val_all,
+                       state_all, R, S_all, out_val, out_state, sortws, (const uint32_t*)list);
+    MFF_LAUNCH_CHECK();
+    return 0;
+  }
+  hipLaunchKernelGGL(k_xs_rank, dim3(g), dim3(SORT_THREADS), 0, st, val, state, rows, D, S_loc,
+                     val_all, state_all, R, S_all, out_val, out_state, sortws, (const uint32_t*)nullptr);
   MFF_LAUNCH_CHECK();
   return 0;
 }

@@ -221,12 +221,24 @@ def test_stage2_live(dev, N, D):
 
 @pytest.mark.parametrize("kind", ["z", "rank"])
 @pytest.mark.parametrize("S", [130, 3000, 5000, 9000])
-def test_stage3_live(dev, kind, S):
-    """z: S <= 8192 runs the one-pass k_xs_zscore_local, 9000 moments + zscore."""
+@pytest.mark.parametrize("ties", [True, False])
+def test_stage3_live(dev, kind, S, ties):
+    """z: S <= 8192 runs the one-pass k_xs_zscore_local, 9000 moments + zscore.  rank:
+    S <= 8192 the bucketed kernel; with ties=True the tie-heavy days (30 % of the values
+    rounded to integers) overflow its buckets and go to the sorting kernel through the
+    hand-over list, ties=False keeps them (continuous values, a few ties, one outlier
+    day spanning 1e-300 .. 1e300); S = 9000 sorts."""
     import mff_oracle as O
     from mff import engine
     val, state = _random_long_panel(6, S, 3)
-    val[2, :] = 7.0  # constant day -> z NaN (0/0)
+    if not ties:
+        rng = np.random.default_rng(S)
+        val = rng.normal(size=val.shape) * rng.choice([1e-3, 1.0, 1e5], size=(1, S))
+        val[rng.random(val.shape) < 0.01] = np.nan
+        val[:, :20] = np.round(val[:, :20] * 4) / 4
+        val[4, :5] = [1e300, -1e300, 1e-300, np.inf, -np.inf]
+        val[5, 10:30] = 2.5
+    val[2, :] = 7.0  # constant day -> z NaN (0/0); one full bucket for the rank
     val[:, :40] = np.round(val[:, :40])  # ties for the rank
     ov, os_ = O.oracle_stage3(val, state, kind)
     rv, rs = engine.cross_section(torch.from_numpy(val[None]).to(dev), torch.from_numpy(state[None]).to(dev),
