@@ -848,24 +848,20 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
           double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
           uint64_t* kd = a.lvl_key ? a.lvl_key + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
           uint8_t* wd = a.lvl_w ? a.lvl_w + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
+          // the list reservation is issued here and its value first used after the
+          // moments and the doc_pdf thresholds, which hide the atomic's round trip
           uint32_t base = 0u;
           if (kd && g == 0) base = atomicAdd(a.lvl_count + d, (uint32_t)L);
-          base = bpermu(gb, base);
-          for (int j = 0; j < nj; ++j) {
-            const int l = l0 + j;
-            if (l < L) {
-              const uint32_t c2 = lv[l], cwb = lc[l];
-              const uint32_t V = c2 - pcum, ee = cwb & 0xFFu;
-              const uint32_t bars = ee - pe;  // pe = -1 before level 0
-              pcum = c2;
-              pe = ee;
-              if (fam & F_LVL) {
+          const uint32_t pe0 = pe;
+          if (fam & F_LVL) {
+            for (int j = 0; j < nj; ++j) {
+              const int l = l0 + j;
+              if (l < L) {
+                const uint32_t c2 = lv[l];
+                const uint32_t V = c2 - pcum;
+                pcum = c2;
                 const double dd = (double)V * inv - x0, d2 = dd * dd;
                 s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
-              }
-              if (kd) {  // doc_pdf level list: key c_last / close (correctly rounded), bars
-                kd[base + l] = dbits(fdiv_f32in(clastf, bitsf(cbase - (cwb >> 8)))) | 0x8000000000000000ull;  // ord64 of a positive
-                wd[base + l] = (uint8_t)bars;
               }
             }
           }
@@ -897,6 +893,20 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
             // Sv = 0: shares NaN, NaN > p (S11) -> the first level
             if (Sv == 0u) e = 0;
             if (g < 5 && e < L) qv = fdiv_f32in(clastf, bitsf(cbase - (lc[e] >> 8)));
+          }
+          if (kd) {  // doc_pdf level list: key c_last / close (correctly rounded), bars at the level
+            base = bpermu(gb, base);
+            uint32_t pe1 = pe0;
+            for (int j = 0; j < nj; ++j) {
+              const int l = l0 + j;
+              if (l < L) {
+                const uint32_t cwb = lc[l];
+                const uint32_t ee = cwb & 0xFFu;
+                kd[base + l] = dbits(fdiv_f32in(clastf, bitsf(cbase - (cwb >> 8)))) | 0x8000000000000000ull;  // ord64 of a positive
+                wd[base + l] = (uint8_t)(ee - pe1);  // pe = -1 before level 0
+                pe1 = ee;
+              }
+            }
           }
           lds_fence();
         }

@@ -32,6 +32,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "../../include/mff.h"
 #include "mff_fmath.h"
 #include "mff_internal.h"
@@ -57,6 +59,9 @@ constexpr uint32_t kSerA = F_SEG | F_MOMR | F_TRD | F_ORD;     // open, close, v
 constexpr uint32_t kSerB = F_MOMV | F_SUMV | F_SUMC | F_CORR;  // close, volume
 constexpr uint32_t kSerH = F_OLS | F_MOMH;                     // high, low
 constexpr uint32_t kSerial = kSerA | kSerB | kSerH;
+#ifndef MFF_SERA_FAST
+#define MFF_SERA_FAST 1
+#endif
 
 // ---- presence bits of one stock-day: 8 words, bit m%32 of word m/32 (compile-time
 // word indices only, so the array stays in registers)
@@ -178,9 +183,11 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
 
   // ---------------------------------------------------------------- accumulators
   double sumv = 0.0;
-  // MOMR
+  // MOMR: the up / down subsets are shifted by their own first member (captured in the
+  // walk), so a constant subset sums to exact zeros (C3) without a min / max per bar
   double s1 = 0, s2 = 0, s3 = 0, s4 = 0, u1 = 0, u2 = 0, w1 = 0, w2 = 0;
-  double umn = __builtin_inf(), umx = -__builtin_inf(), wmn = __builtin_inf(), wmx = -__builtin_inf();
+  double xu = 0.0, xd = 0.0;
+  bool hu = false, hd = false;
   int nu = 0, ndn = 0;
   // ORD: products of close/open over the bars at or beyond the volume thresholds
   double p50 = 1.0, p20 = 1.0, pb50 = 1.0;
@@ -191,8 +198,12 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     th20 = a.ord_th[pl + sd];
     tb50 = a.ord_th[2 * pl + sd];
   }
-  // TRD
-  double vT20 = 0, vT50 = 0, rT20 = 0, rT50 = 0, vH20 = 0, vH50 = 0, a20 = 0, n20 = 0, q20 = 0, a50 = 0;
+  // TRD: running sums of v and v*r over the whole day, snapshot at the window edges
+  // (m = 20, 50: head windows; 189, 219: the tail windows start after them), so a bar
+  // costs one add and one fma instead of a masked add per window; volume sums are
+  // integers < 2^53, exact in f64
+  double tv = 0, trv = 0, S20 = 0, S50 = 0, S189 = 0, S219 = 0, R189 = 0, R219 = 0;
+  double a20 = 0, n20 = 0, q20 = 0, a50 = 0;
   // MOMV
   double t1 = 0, t2 = 0, t3 = 0, t4 = 0;
   // SUMV
@@ -273,29 +284,28 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     p[0] += dx; p[1] += dy; p[2] += dx * dx; p[3] += dy * dy; p[4] += dx * dy;
   };
 
-  auto bar = [&](int m, bool pk, float of, float cf, float vf) {
-    // Returns (MOMR, TRD) without branches: an absent bar gets r = x0r and v = 0, so its
-    // deviation, products and window sums are exact zeros, and every per-bar condition
-    // is a select; the minute windows are wave-uniform selects (only m <= 50, which
-    // needs a reciprocal, stays a uniform branch).  Straight-line code lets the
-    // scheduler overlap the dependent f64 chains of the four bars of a quad.
+  // ALLP: every lane has this bar (the quad's wave-uniform fast path): no presence selects
+  auto bar = [&](int m, bool pk, float of, float cf, float vf, auto allp) {
+    constexpr bool ALLP = decltype(allp)::value;
+    if (ALLP) pk = true;
     if (fam & (F_MOMR | F_TRD | F_ORD)) {
       const double q = fdiv((double)cf, (double)of);  // close / open
-      const double r = pk ? q - 1.0 : x0r;
-      const double v = pk ? (double)vf : 0.0;
+      const double r = q - 1.0;
+      const double v = (ALLP || pk) ? (double)vf : 0.0;
       if (fam & F_MOMR) {
-        const double dd = r - x0r, d2 = dd * dd;
-        s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
+        // an absent bar: deviation 0, neither up nor down
+        const double dd = (ALLP || pk) ? r - x0r : 0.0, d2 = dd * dd;
+        s1 += dd; s2 += d2; s3 = fma(d2, dd, s3); s4 = fma(d2, d2, s4);
         const bool up = pk & (r > 0.0), dn = pk & (r < 0.0);  // r is finite (no NaN case)
         nu += up ? 1 : 0;
         ndn += dn ? 1 : 0;
-        u1 += up ? dd : 0.0; u2 += up ? d2 : 0.0;
-        w1 += dn ? dd : 0.0; w2 += dn ? d2 : 0.0;
-        // min / max of candidates (+-inf when not in the set): one v_min/v_max_f64 each
-        const double ru = up ? r : __builtin_inf(), rd = dn ? r : __builtin_inf();
-        const double ru2 = up ? r : -__builtin_inf(), rd2 = dn ? r : -__builtin_inf();
-        umn = __builtin_fmin(umn, ru); umx = __builtin_fmax(umx, ru2);
-        wmn = __builtin_fmin(wmn, rd); wmx = __builtin_fmax(wmx, rd2);
+        xu = (up & !hu) ? r : xu;
+        xd = (dn & !hd) ? r : xd;
+        hu |= up;
+        hd |= dn;
+        const double eu = up ? r - xu : 0.0, ed = dn ? r - xd : 0.0;
+        u1 += eu; u2 = fma(eu, eu, u2);
+        w1 += ed; w2 = fma(ed, ed, w2);
       }
       if (fam & F_ORD) {  // CM:379-480: top_k(k).min() <= v, v <= bottom_k(50).max()
         p50 *= (pk && vf >= th50) ? q : 1.0;
@@ -303,19 +313,21 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
         pb50 *= (pk && vf <= tb50) ? q : 1.0;
       }
       if (fam & F_TRD) {
-        const double vr = v * r;
-        const bool t20 = m >= 220, t50 = m >= 190;
-        vT20 += t20 ? v : 0.0; rT20 += t20 ? vr : 0.0;
-        vT50 += t50 ? v : 0.0; rT50 += t50 ? vr : 0.0;
+        tv += v;
+        trv = fma(v, pk ? r : 0.0, trv);
+        if (m == 189) { S189 = tv; R189 = trv; }
+        if (m == 219) { S219 = tv; R219 = trv; }
         if (m <= 50) {
           const double iw = vf == 0.0f ? __builtin_inf() : frcp((double)vf);  // inf when v = 0: r/0 semantics
           const double ta = pk ? r * iw : 0.0;
-          vH50 += v; a50 += ta;
+          a50 += ta;
           if (m <= 20) {
-            vH20 += v; a20 += ta;
+            a20 += ta;
             n20 += pk ? (r < 0.0 ? -r : 0.0) * iw : 0.0;
             q20 += pk ? (r > 0.0 ? r : 0.0) * iw : 0.0;
           }
+          if (m == 20) S20 = tv;
+          if (m == 50) S50 = tv;
         }
       }
     }
@@ -382,10 +394,21 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
       olsbar(m0 + 3, (pm >> 3) & 1u, x.h.w, x.l.w, (lm >> 3) & 1u, lh1.y, ll1.y);
     }
     if (fam & (kSerA | kSerB)) {
-      bar(m0 + 0, pm & 1u, x.o.x, x.c.x, x.v.x);
-      bar(m0 + 1, (pm >> 1) & 1u, x.o.y, x.c.y, x.v.y);
-      bar(m0 + 2, (pm >> 2) & 1u, x.o.z, x.c.z, x.v.z);
-      bar(m0 + 3, (pm >> 3) & 1u, x.o.w, x.c.w, x.v.w);
+      // every lane has all four bars (the usual case): the presence selects fold away
+      // (set A only: set B's register budget has no room for the second copy)
+      if (SET == kSerA && MFF_SERA_FAST && __builtin_amdgcn_ballot_w64((pm & 0xFu) != 0xFu) == 0ull) {
+        const std::true_type all;
+        bar(m0 + 0, true, x.o.x, x.c.x, x.v.x, all);
+        bar(m0 + 1, true, x.o.y, x.c.y, x.v.y, all);
+        bar(m0 + 2, true, x.o.z, x.c.z, x.v.z, all);
+        bar(m0 + 3, true, x.o.w, x.c.w, x.v.w, all);
+      } else {
+        const std::false_type some;
+        bar(m0 + 0, pm & 1u, x.o.x, x.c.x, x.v.x, some);
+        bar(m0 + 1, (pm >> 1) & 1u, x.o.y, x.c.y, x.v.y, some);
+        bar(m0 + 2, (pm >> 2) & 1u, x.o.z, x.c.z, x.v.z, some);
+        bar(m0 + 3, (pm >> 3) & 1u, x.o.w, x.c.w, x.v.w, some);
+      }
     }
   };
   uint32_t mw[8];
@@ -551,9 +574,9 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     double sdr;
     const bool has_sdr = std1_raw(m, m.s1 == 0.0 && m.s2 == 0.0, sdr);
     if (has_sdr) val(16, sdr); else nul(16);  // vol_return1min
-    double sup = 0.0, sdn = 0.0;  // fill_null(0)
-    std1_raw(RawMom{u1, u2, 0, 0, nu}, umn == umx, sup);
-    std1_raw(RawMom{w1, w2, 0, 0, ndn}, wmn == wmx, sdn);
+    double sup = 0.0, sdn = 0.0;  // fill_null(0); shifted by a member: constant <=> exact zeros
+    std1_raw(RawMom{u1, u2, 0, 0, nu}, u1 == 0.0 && u2 == 0.0, sup);
+    std1_raw(RawMom{w1, w2, 0, 0, ndn}, w1 == 0.0 && w2 == 0.0, sdn);
     val(17, sup);  // vol_upVol
     val(19, sdn);  // vol_downVol
     if (has_sdr) { val(18, sup / sdr); val(20, sdn / sdr); }
@@ -571,6 +594,8 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     val(13, pb50 - 1.0);  // mmt_bottom20VolumeRet: bottom_k(50) [sic CM:471]
   }
   if (fam & F_TRD) {
+    const double vT20 = tv - S219, vT50 = tv - S189, vH20 = S20, vH50 = S50;
+    const double rT20 = trv - R219, rT50 = trv - R189;
     if (M.any_in(220, 239)) val(50, rT20 / (vT20 + 1.0)); else absent(50);
     if (M.any_in(190, 239)) val(51, rT50 / (vT50 == 0.0 ? 1.0 : vT50)); else absent(51);
     const int nh20 = M.count_in(0, 20), nh50 = M.count_in(0, 50);
