@@ -59,6 +59,10 @@ constexpr uint32_t kSerA = F_SEG | F_MOMR | F_TRD | F_ORD;     // open, close, v
 constexpr uint32_t kSerB = F_MOMV | F_SUMV | F_SUMC | F_CORR;  // close, volume
 constexpr uint32_t kSerH = F_OLS | F_MOMH;                     // high, low
 constexpr uint32_t kSerial = kSerA | kSerB | kSerH;
+constexpr uint32_t kSerAB = kSerA | kSerB;  // one pass over open, close, volume
+#ifndef MFF_FUSE_AB
+#define MFF_FUSE_AB 0
+#endif
 #ifndef MFF_SERA_FAST
 #define MFF_SERA_FAST 1
 #endif
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
 
   // ---------------------------------------------------------------- shifts
   double x0r = 0.0, x0v = 0.0;
-  double x1 = 0, y1 = 0, x2 = 0, y2 = 0, x3 = 0, y3 = 0, x4 = 0, y4 = 0;
+  double x1 = 0, xc = 0, yv = 0;
   if (fam & (F_MOMR | F_TRD)) x0r = fdiv((double)C[fb], (double)O[fb]) - 1.0;  // as in the walk
   if (fam & (F_MOMV | F_SUMV)) x0v = (double)V[fb];
   const float* Hp = a.fld[1] + sd * NBAR;
@@ -173,12 +177,13 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     xh0 = fdiv(y0, x0);
   }
   if (fam & F_CORR) {
-    const double cf1 = (double)C[fb], vf1 = (double)V[fb];
-    const double cf2 = f2 >= 0 ? (double)C[f2] : 0.0, vf2 = f2 >= 0 ? (double)V[f2] : 0.0;
-    x1 = fdivr(cf2 - cf1, cf1, frcp(cf1)); y1 = vf2;  // prv: (pct_change(close), volume), as in the walk
-    x2 = cf1; y2 = vf1;                // pv
-    x3 = cf2; y3 = vf1;                // pvd: (close, volume.shift(1))
-    x4 = cf1; y4 = vf2;                // pvl: (close, volume.shift(-1))
+    // pv / pvd / pvl / prv share the close and volume sums, shifted by the first present
+    // bar; the pct_change of prv is shifted by its first value (as in the walk)
+    const double cf1 = (double)C[fb];
+    const double cf2 = f2 >= 0 ? (double)C[f2] : 0.0;
+    x1 = fdivr(cf2 - cf1, cf1, frcp(cf1));
+    xc = cf1;
+    yv = (double)V[fb];
   }
 
   // ---------------------------------------------------------------- accumulators
@@ -206,16 +211,25 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
   double a20 = 0, n20 = 0, q20 = 0, a50 = 0;
   // MOMV
   double t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-  // SUMV
-  double spre = 0, scls = 0, shead = 0, stail = 0;
+  // SUMV: the minute windows from snapshots of the running volume sum (exact integers)
+  double S30 = 0, S209 = 0, S236 = 0;
   // SUMC
   double amh = 0;
-  // CORR: pv, prv, pvd, pvl, prvr, pvr
-  double P[6][5];
-#pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int j = 0; j < 5; ++j) P[i][j] = 0.0;
+  // CORR.  Rows 0..n-1 = present bars; dc = c - c_row0, dv = v - v_row0.
+  //  pv  (c, v) rows 0..n-1            sums A1 A2 B1 B2 X0
+  //  pvd (c_b, v_b-1) b = 1..n-1       A1 A2, B1 - dv_last, B2 - dv_last^2, X1
+  //  pvl (c_b-1, v_b) b = 1..n-1       A1 - dc_last, A2 - dc_last^2, B1 B2, X2
+  //  prv (pct_b, v_b) b = 1..n-1       E1 E2 (pct shifted by pct_1), B1 B2, EX
+  // (dc = dv = 0 on row 0).  A subset that does not contain row 0 is not shifted by a
+  // member, so its exact constancy (C3: Pearson NaN) comes from the change indices:
+  // kcf / kcl = first / last row whose close differs from the row before (kvf / kvl for
+  // volume), -1 when none.
+  //  prvr (pct_c, pct_v) and pvr (c, pct_v) over the non-zero-volume rows after their
+  //  first: shared pct_v sums Z1 Z2, shifted by the first pair (members).
+  double A1 = 0, A2 = 0, B1 = 0, B2 = 0, X0 = 0, X1 = 0, X2 = 0, E1 = 0, E2 = 0, EX = 0;
+  double Z1 = 0, Z2 = 0, F1 = 0, F2 = 0, FX = 0, G1 = 0, G2 = 0, GX = 0;
+  double dcp = 0, dvp = 0;
+  int kr = 0, kcf = -1, kcl = -1, kvf = -1, kvl = -1;
   double x5 = 0, y5 = 0, x6 = 0;
   int nzc = 0;
   // carries: previous present bar, previous present non-zero-volume bar
@@ -280,9 +294,6 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     }
   };
 
-  auto acc5 = [](double (&p)[5], double dx, double dy) {
-    p[0] += dx; p[1] += dy; p[2] += dx * dx; p[3] += dy * dy; p[4] += dx * dy;
-  };
 
   // ALLP: every lane has this bar (the quad's wave-uniform fast path): no presence selects
   auto bar = [&](int m, bool pk, float of, float cf, float vf, auto allp) {
@@ -332,18 +343,17 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
       }
     }
     if (!(fam & (F_MOMV | F_SUMV | F_SUMC | F_CORR))) return;
+    if (fam & F_SUMV) {  // snapshots of the sum through bars 30, 209, 236 (before bar m's add)
+      if (m == 31) S30 = sumv;
+      if (m == 210) S209 = sumv;
+      if (m == 237) S236 = sumv;
+    }
     if (!pk) return;
     const double c = (double)cf, v = (double)vf;
     if (fam & (F_MOMV | F_SUMV)) sumv += v;
     if (fam & F_MOMV) {
       const double dd = v - x0v, d2 = dd * dd;
-      t1 += dd; t2 += d2; t3 += d2 * dd; t4 += d2 * d2;
-    }
-    if (fam & F_SUMV) {
-      if (m <= 236) spre += v;
-      if (m >= 237) scls += v;
-      if (m <= 30) shead += v;
-      if (m >= 210) stail += v;
+      t1 += dd; t2 += d2; t3 = fma(d2, dd, t3); t4 = fma(d2, d2, t4);
     }
     // one reciprocal per close and per volume serves every quotient of this bar and
     // of the bars that follow it (pct_change, Amihud)
@@ -356,26 +366,35 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
       if (hp && vf > 0.0f) amh += fabs(c - (double)cp) * (rcp_ * rv);  // |dc| / (c_prev * v)
     }
     if (fam & F_CORR) {
-      acc5(P[0], c - x2, v - y2);  // pv
+      const double dc = c - xc, dv = v - yv;
+      A1 += dc; A2 = fma(dc, dc, A2); B1 += dv; B2 = fma(dv, dv, B2); X0 = fma(dc, dv, X0);
       if (hp) {
-        const double pc = fdivr(c - (double)cp, (double)cp, rcp_);
-        acc5(P[1], pc - x1, v - y1);           // prv
-        acc5(P[2], c - x3, (double)vp - y3);   // pvd
-        acc5(P[3], (double)cp - x4, v - y4);   // pvl: (close of the previous bar, this volume)
+        X1 = fma(dc, dvp, X1);  // pvd: (close, previous volume)
+        X2 = fma(dcp, dv, X2);  // pvl: (previous close, volume) = (close, next volume)
+        const double ex = fdivr(c - (double)cp, (double)cp, rcp_) - x1;  // prv
+        E1 += ex; E2 = fma(ex, ex, E2); EX = fma(ex, dv, EX);
+        const bool chc = cf != cp, chv = vf != vp;
+        kcl = chc ? kr : kcl;
+        kcf = (chc && kcf < 0) ? kr : kcf;
+        kvl = chv ? kr : kvl;
+        kvf = (chv && kvf < 0) ? kr : kvf;
       }
+      dcp = dc;
+      dvp = dv;
       if (vf != 0.0f) {  // rows with volume != 0 (CM:855-866, 924-930)
         if (hz) {
           const double pcz = fdivr(c - (double)czp, (double)czp, rcz);
           const double pvz = fdivr(v - (double)vzp, (double)vzp, rvz);
           if (nzc == 1) { x5 = pcz; y5 = pvz; x6 = c; }  // first pair: the shifts
-          const double dy = pvz - y5;
-          acc5(P[4], pcz - x5, dy);  // prvr
-          acc5(P[5], c - x6, dy);    // pvr
+          const double dy = pvz - y5, e5 = pcz - x5, e6 = c - x6;
+          Z1 += dy; Z2 = fma(dy, dy, Z2);
+          F1 += e5; F2 = fma(e5, e5, F2); FX = fma(e5, dy, FX);  // prvr
+          G1 += e6; G2 = fma(e6, e6, G2); GX = fma(e6, dy, GX);  // pvr
         }
         czp = cf; vzp = vf; rcz = rc; rvz = rv; hz = true; ++nzc;
       }
     }
-    cp = cf; vp = vf; rcp_ = rc; hp = true;
+    cp = cf; vp = vf; rcp_ = rc; hp = true; ++kr;
   };
 
   // ---------------------------------------------------------------- the walk
@@ -428,8 +447,8 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     constexpr int NB = LAG ? 2 * NP : NP;  // images: the planes, then their lag copies
     // chunk = CQ quads (4*CQ bars) per stock-day; the lag sets use 8-bar chunks so the
     // staged registers (NB*CQ float4) leave room for a third wave per SIMD
-    constexpr int CQ = (SET == kSerB) ? 2 : 4, BC = 4 * CQ;
-    constexpr int NBUF = (SET == kSerB) ? 2 : 1;  // chunks in flight ahead of the one in use
+    constexpr int CQ = (SET == kSerB || SET == kSerAB) ? 2 : 4, BC = 4 * CQ;
+    constexpr int NBUF = (SET == kSerB || SET == kSerAB) ? 2 : 1;  // chunks in flight ahead of the one in use
     constexpr int LAGC = 48 / BC;                 // lag bar t-50 = chunk c-LAGC, element j-2
     __shared__ __attribute__((aligned(16))) float4 sbufA[4][NB][64 * CQ];
     __shared__ __attribute__((aligned(16))) float4 sbufB[NBUF == 2 ? 4 : 1][NB][64 * CQ];
@@ -621,6 +640,7 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     val(26, sk / ku);
   }
   if (fam & F_SUMV) {
+    const double spre = S236, scls = sumv - S236, shead = S30, stail = sumv - S209;
     if (M.any_in(0, 236)) val(28, spre); else absent(28);
     if (M.any_in(237, 239)) val(29, scls); else absent(29);
     const double vfirst = x0v;
@@ -656,14 +676,19 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     if (std1_raw(m, m.s1 == 0.0 && m.s2 == 0.0, sdv)) val(15, sdv); else nul(15);  // vol_range1min
   }
   if (fam & F_CORR) {
-    auto fin = [&](int f, int np, const double (&p)[5]) { val(f, pearson_raw(np, p[0], p[1], p[2], p[3], p[4])); };
-    fin(35, n, P[0]);      // corr_pv
-    fin(33, n - 1, P[1]);  // corr_prv
-    fin(36, n - 1, P[2]);  // corr_pvd
-    fin(37, n - 1, P[3]);  // corr_pvl
+    const double dcl = dcp, dvl = dvp;  // the last row's shifted close / volume
+    const bool c_tail = kcl <= 1, c_head = kcf < 0 || kcf >= n - 1;  // rows 1..n-1 / 0..n-2 constant
+    const bool v_tail = kvl <= 1, v_head = kvf < 0 || kvf >= n - 1;
+    auto fin = [&](int f, bool cst, int np, double sx, double sy, double sxx, double syy, double sxy) {
+      val(f, cst ? qnan() : pearson_raw(np, sx, sy, sxx, syy, sxy));
+    };
+    fin(35, false, n, A1, B1, A2, B2, X0);                                // corr_pv
+    fin(33, v_tail, n - 1, E1, B1, E2, B2, EX);                           // corr_prv
+    fin(36, c_tail || v_head, n - 1, A1, B1 - dvl, A2, B2 - dvl * dvl, X1);  // corr_pvd
+    fin(37, c_head || v_tail, n - 1, A1 - dcl, B1, A2 - dcl * dcl, B2, X2);  // corr_pvl
     if (nzc > 0) {
-      fin(34, nzc - 1, P[4]);  // corr_prvr
-      fin(38, nzc - 1, P[5]);  // corr_pvr
+      fin(34, false, nzc - 1, F1, Z1, F2, Z2, FX);  // corr_prvr
+      fin(38, false, nzc - 1, G1, Z1, G2, Z2, GX);  // corr_pvr
     } else {
       absent(34); absent(38);
     }
@@ -698,6 +723,13 @@ int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D
     return b;
   };
   const dim3 grid((unsigned)nblk), blk(256);
+  if (MFF_FUSE_AB && (a.fam & kSerAB) == kSerAB) {
+    hipLaunchKernelGGL((k_stage1s<kSerAB, true>), grid, blk, 0, st, patched(kSerAB));
+    if ((a.fam & kSerH) == kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, true>), grid, blk, 0, st, patched(kSerH));
+    else if (a.fam & kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, false>), grid, blk, 0, st, patched(kSerH));
+    MFF_LAUNCH_CHECK();
+    return 0;
+  }
   if ((a.fam & kSerA) == kSerA) hipLaunchKernelGGL((k_stage1s<kSerA, true>), grid, blk, 0, st, patched(kSerA));
   else if (a.fam & kSerA) hipLaunchKernelGGL((k_stage1s<kSerA, false>), grid, blk, 0, st, patched(kSerA));
   if ((a.fam & kSerB) == kSerB) hipLaunchKernelGGL((k_stage1s<kSerB, true>), grid, blk, 0, st, patched(kSerB));
