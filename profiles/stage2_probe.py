@@ -39,9 +39,10 @@ def main():
     for N, meth in [(20, "o"), (20, "m"), (20, "z"), (20, "std"), (5, "z"), (60, "z"), (7, "z"),
                     (120, "z"), (250, "z")]:
         res[f"stage2_N{N}_{meth}"] = t(lambda: engine.rolling(val, state, N, meth))
-    os.environ["MFF_STAGE2_IMPL"] = "slide"
-    for N, meth in [(20, "m"), (20, "z"), (20, "std"), (5, "z"), (60, "z")]:
-        res[f"stage2_slide_N{N}_{meth}"] = t(lambda: engine.rolling(val, state, N, meth))
+    for impl in ("ring", "slide"):
+        os.environ["MFF_STAGE2_IMPL"] = impl
+        for N, meth in [(20, "m"), (20, "z"), (5, "z"), (60, "z")]:
+            res[f"stage2_{impl}_N{N}_{meth}"] = t(lambda: engine.rolling(val, state, N, meth))
     del os.environ["MFF_STAGE2_IMPL"]
     res["stage3_z"] = t(lambda: engine.cross_section(val, state, "z"))
     nb = nbytes

@@ -42,6 +42,10 @@ int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, c
 int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
                   uint32_t fam, double* val, uint8_t* state, const float* ord_th, hipStream_t st);
 
+#ifndef MFF_MERGE_OL
+#define MFF_MERGE_OL 1
+#endif
+
 namespace g16 {
 
 constexpr int NB = 256;  // OLS betas per stock-day (LDS, 8 B each)
@@ -167,6 +171,8 @@ __device__ __forceinline__ void gsort256(T (&a)[K]) {
 constexpr uint32_t G_ORD = F_ORD | F_ORDV;   // volume (thresholds; the products are serial)
 constexpr uint32_t G_LVL = F_LVL | F_PDF;    // close, volume
 constexpr uint32_t kGroups[2] = {G_ORD, G_LVL};
+// both sorted groups in one launch: the volume plane is read once for the two sorts
+constexpr uint32_t G_OL = G_ORD | G_LVL;
 
 template <uint32_t SET>
 // (256, 4): at most 128 VGPRs, four waves per SIMD (the LVL set would take 139 and three)
@@ -1013,14 +1019,15 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
   const long long nblk = (long long)((S + 63) / 64) * D;
   // one 16-lane group launch; it stores its own group's rows (and the queries) only
   auto group_launch = [&](int gi) -> int {
-    const uint32_t set = g16::kGroups[gi];
+    const uint32_t set = gi < 2 ? g16::kGroups[gi] : g16::G_OL;
     if (!(a.fam & set)) return 0;
     g16::GArgs b = a;
     for (int i = 0; i < NF; ++i)
       if (!(kFactorFamily[i] & set)) b.row[i] = -1;
     if (!(set & F_PDF)) b.pdfq = nullptr;
     if (gi == 0) hipLaunchKernelGGL(g16::k_stage1g<g16::G_ORD>, dim3((unsigned)nblk), dim3(256), 0, st, b);
-    else hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b);
+    else if (gi == 1) hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b);
+    else hipLaunchKernelGGL(g16::k_stage1g<g16::G_OL>, dim3((unsigned)nblk), dim3(256), 0, st, b);
     MFF_LAUNCH_CHECK();
     return 0;
   };
@@ -1049,7 +1056,8 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
       return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_PDF, 1024, st,
                         a.lvl_count, a.lvl_key, a.lvl_w);
     }
-    int rc = group_launch(1);
+    // ORD in the same launch when both sorted groups are requested (part 2 then skips it)
+    int rc = group_launch(MFF_MERGE_OL && (a.fam & g16::G_ORD) && (a.fam & (F_LVL | F_PDF)) ? 2 : 1);
     if (rc != 0) return rc;
     if (a.fam & (F_LVL | F_PDF)) {
       // exact general path for the listed stock-days (LVL + PDF only)
@@ -1059,8 +1067,10 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
     }
   }
   if ((part & 2) && !w64) {  // the ORD sort (thresholds) before the serial kernels (products)
-    const int rc = group_launch(0);
-    if (rc != 0) return rc;
+    if (!(MFF_MERGE_OL && (a.fam & g16::G_ORD) && (a.fam & (F_LVL | F_PDF)))) {
+      const int rc = group_launch(0);
+      if (rc != 0) return rc;
+    }
     return launch_serial(fld, valid, S, D, a.row, a.fam, val, state, a.ord_th, st);
   }
   return 0;

@@ -173,6 +173,172 @@ __global__ __launch_bounds__(S2_SLIDE_THREADS) void k_stage2_slide(const double*
   }
 }
 
+// LDS-ring sliding variant (N <= S2_RING_MAXN): the window state of k_stage2_slide, with
+// the window's values in an LDS ring [N][64] (one wave per block, bank = lane: conflict
+// free), so the leaving value is one LDS read instead of a dependent HBM re-read, and the
+// days are loaded S2_U at a time one chunk ahead (as k_stage2_reg).  A null row sits in
+// the ring as a signalling-NaN payload (real NaN values are stored as the quiet NaN).
+constexpr int S2_RING_MAXN = 32;  // measured: ring beats the HBM re-read kernel up to ~N = 32 (N = 7 z 7.0 vs 10.4 ms; N = 120 22 vs 11.4 ms at c4: LDS limits occupancy)
+constexpr uint64_t S2_NULL_BITS = 0x7FF4000000000001ull;
+constexpr int S2_RU = 4;
+
+__global__ __launch_bounds__(64) void k_stage2_ring(const double* val, const uint8_t* state, int D, int S, int N,
+                                                    int method, double* out_val, uint8_t* out_state) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem2[];
+  uint64_t* ring = reinterpret_cast<uint64_t*>(smem2);  // [N][64]
+  const int nsb = (S + 63) / 64;
+  const int row = blockIdx.x / nsb;
+  const int lane = (int)threadIdx.x;
+  const int s = (blockIdx.x % nsb) * 64 + lane;
+  if (s >= S || D <= 0) return;
+  const size_t plane = (size_t)D * S;
+  const double* v = val + row * plane + s;
+  const uint8_t* st = state + row * plane + s;
+  double* ov = out_val + row * plane + s;
+  uint8_t* os = out_state + row * plane + s;
+
+  int cnt = 0, pos = 0;
+  int nnull = 0, nnan = 0, npi = 0, nni = 0, nfin = 0;
+  int k = 0, lastchg = 0;
+  double prev = 0.0, c = 0.0;
+  bool prevok = false;
+  DD S1{0.0, 0.0}, S2{0.0, 0.0};
+  auto slot = [&](int i) -> uint64_t& { return ring[i * 64 + lane]; };
+  auto rebuild = [&]() {  // sums over the whole ring (the current window)
+    S1 = DD{0.0, 0.0};
+    S2 = DD{0.0, 0.0};
+    bool have = false;
+    for (int i = 0; i < N; ++i) {
+      const uint64_t b = slot(i);
+      if (b == S2_NULL_BITS) continue;
+      const double xe = __longlong_as_double((long long)b);
+      if (!__builtin_isfinite(xe)) continue;
+      if (!have) { c = xe; have = true; }
+      const double y = xe - c;
+      S1 = dd_add(S1, y);
+      S2 = dd_add(S2, two_prod(y, y));
+    }
+  };
+  auto day = [&](double x, uint8_t sx, size_t o) {
+    if (sx == MFF_STATE_ABSENT) {
+      ov[o] = 0.0;
+      os[o] = MFF_STATE_ABSENT;
+      return;
+    }
+    const bool isnull = sx == MFF_STATE_NULL;
+    if (isnull) x = 0.0;
+    if (method == MFF_ROLL_O) {
+      ov[o] = x;
+      os[o] = sx;
+      return;
+    }
+    const bool fin = !isnull && __builtin_isfinite(x);
+    if (!(fin && prevok && x == prev)) lastchg = k;
+    prev = x;
+    prevok = fin;
+    bool rb = false;
+    if (cnt == N) {  // the oldest row leaves
+      const uint64_t b = slot(pos);
+      if (b == S2_NULL_BITS) {
+        --nnull;
+      } else {
+        const double xo = __longlong_as_double((long long)b);
+        if (__builtin_isnan(xo)) --nnan;
+        else if (xo == __builtin_inf()) --npi;
+        else if (xo == -__builtin_inf()) --nni;
+        else {
+          --nfin;
+          const double y = xo - c;
+          const double before = S2.hi;
+          S1 = dd_add(S1, -y);
+          S2 = dd_add(S2, dd_neg(two_prod(y, y)));
+          rb = nfin > 0 && before > 0.0 && !(S2.hi > before * 0x1p-30);
+        }
+      }
+    } else {
+      ++cnt;
+    }
+    slot(pos) = isnull ? S2_NULL_BITS : (uint64_t)__double_as_longlong(__builtin_isnan(x) ? qnan() : x);
+    pos = pos + 1 == N ? 0 : pos + 1;
+    if (isnull) ++nnull;
+    else if (__builtin_isnan(x)) ++nnan;
+    else if (x == __builtin_inf()) ++npi;
+    else if (x == -__builtin_inf()) ++nni;
+    else {
+      if (nfin == 0 && !rb) {  // empty of finite values: fresh shift, exact zero sums
+        c = x;
+        S1 = DD{0.0, 0.0};
+        S2 = DD{0.0, 0.0};
+      }
+      ++nfin;
+      if (!rb) {
+        const double y = x - c;
+        S1 = dd_add(S1, y);
+        S2 = dd_add(S2, two_prod(y, y));
+      }
+    }
+    if (rb) rebuild();
+    ++k;
+    if (cnt < N || nnull > 0) {
+      ov[o] = 0.0;
+      os[o] = MFF_STATE_NULL;
+      return;
+    }
+    double mean, sd;
+    if (nnan > 0 || (npi > 0 && nni > 0)) {
+      mean = qnan();
+      sd = qnan();
+    } else if (npi > 0 || nni > 0) {
+      mean = npi > 0 ? __builtin_inf() : -__builtin_inf();
+      sd = qnan();
+    } else if (lastchg <= k - N) {  // rows k-N .. k-1 identical
+      mean = x;
+      sd = 0.0;
+    } else {
+      const double inv_n = 1.0 / (double)N;
+      const double m1 = (S1.hi + S1.lo) * inv_n;
+      mean = c + m1;
+      const DD q = dd_add(S2, dd_neg(dd_sq_div(S1, (double)N)));
+      const double var = q.hi + q.lo;
+      sd = sqrt(var > 0.0 ? var * inv_n : 0.0);
+      if (method == MFF_ROLL_Z) {
+        ov[o] = ((x - c) - m1) / sd;
+        os[o] = MFF_STATE_VALUE;
+        return;
+      }
+    }
+    ov[o] = method == MFF_ROLL_M ? mean : method == MFF_ROLL_STD ? sd : (x - mean) / sd;
+    os[o] = MFF_STATE_VALUE;
+  };
+  // days S2_RU at a time, the next chunk in flight while this one is processed
+  double xb[S2_RU];
+  uint8_t sb[S2_RU];
+#pragma unroll
+  for (int u = 0; u < S2_RU; ++u) {
+    const int d = min(u, D - 1);
+    xb[u] = v[(size_t)d * S];
+    sb[u] = st[(size_t)d * S];
+  }
+  for (int d0 = 0; d0 < D; d0 += S2_RU) {
+    double xc[S2_RU];
+    uint8_t sc[S2_RU];
+#pragma unroll
+    for (int u = 0; u < S2_RU; ++u) {
+      xc[u] = xb[u];
+      sc[u] = sb[u];
+    }
+#pragma unroll
+    for (int u = 0; u < S2_RU; ++u) {
+      const int d = min(d0 + S2_RU + u, D - 1);
+      xb[u] = v[(size_t)d * S];
+      sb[u] = st[(size_t)d * S];
+    }
+#pragma unroll
+    for (int u = 0; u < S2_RU; ++u)
+      if (d0 + u < D) day(xc[u], sc[u], (size_t)(d0 + u) * S);
+  }
+}
+
 // Register-window variant for the common window lengths (N a template constant): the
 // last N present values live in VGPRs as a shift register (w[N-1] = newest, w[0] =
 // oldest, shifted on present days only), so the per-day recompute reads no LDS, and the
@@ -183,13 +349,14 @@ __global__ __launch_bounds__(S2_SLIDE_THREADS) void k_stage2_slide(const double*
 constexpr int S2_U = 4;  // 4 in flight + 4 processed: <= 96 VGPRs at N = 20 (5 waves/SIMD)
 constexpr int S2_THREADS = 256;
 
+// Requires D >= 1 (mff_stage2 checks it before any launch).
 template <int N>
 __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, const uint8_t* state, int D, int S,
                                                          int method, double* out_val, uint8_t* out_state) {
   const int nsb = (S + S2_THREADS - 1) / S2_THREADS;
   const int row = blockIdx.x / nsb;
   const int s = (blockIdx.x % nsb) * S2_THREADS + (int)threadIdx.x;
-  if (s >= S) return;
+  if (s >= S || D <= 0) return;
   const size_t plane = (size_t)D * S;
   const double* v = val + row * plane + s;
   const uint8_t* st = state + row * plane + s;
@@ -417,9 +584,9 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
                        state, D, S, method, out_val, out_state);                                            \
     MFF_LAUNCH_CHECK();                                                                                     \
     return 0;
-  // MFF_STAGE2_IMPL=slide: the sliding kernel for every N (A/B timing)
+  // MFF_STAGE2_IMPL=ring / slide: a sliding kernel for every N (A/B timing)
   const char* impl = getenv("MFF_STAGE2_IMPL");
-  const bool force_slide = impl && impl[0] == 's';
+  const bool force_slide = impl && (impl[0] == 's' || impl[0] == 'r');
   switch (force_slide ? -1 : N) {  // the usual windows: register shift window; other N: sliding sums
     MFF_S2_REG(1)
     MFF_S2_REG(2)
@@ -432,6 +599,13 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
       break;
   }
 #undef MFF_S2_REG
+  if (N <= S2_RING_MAXN && !(impl && impl[1] == 'l')) {  // MFF_STAGE2_IMPL=slide: HBM re-read kernel
+    const long long nr = (long long)rows * ((S + 63) / 64);
+    hipLaunchKernelGGL(k_stage2_ring, dim3((unsigned)nr), dim3(64), (size_t)N * 64 * 8, as_stream(stream), val,
+                       state, D, S, N, method, out_val, out_state);
+    MFF_LAUNCH_CHECK();
+    return 0;
+  }
   const long long nsl = (long long)rows * ((S + S2_SLIDE_THREADS - 1) / S2_SLIDE_THREADS);
   hipLaunchKernelGGL(k_stage2_slide, dim3((unsigned)nsl), dim3(S2_SLIDE_THREADS), 0, as_stream(stream), val, state,
                      D, S, N, method, out_val, out_state);
