@@ -60,6 +60,9 @@ constexpr uint32_t kSerB = F_MOMV | F_SUMV | F_SUMC | F_CORR;  // close, volume
 constexpr uint32_t kSerH = F_OLS | F_MOMH;                     // high, low
 constexpr uint32_t kSerial = kSerA | kSerB | kSerH;
 constexpr uint32_t kSerAB = kSerA | kSerB;  // one pass over open, close, volume
+#ifndef MFF_PAIR_AB
+#define MFF_PAIR_AB 1
+#endif
 #ifndef MFF_FUSE_AB
 #define MFF_FUSE_AB 0
 #endif
@@ -124,18 +127,25 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 // FULL: every family of SET is requested (the usual case), so the family tests fold
 // away at compile time instead of branching per bar
 // set B stages 8-bar chunks (two in flight) and fits 168 VGPRs: three waves per SIMD
-template <uint32_t SET, bool FULL>
-__global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) {
+// PAIR: the wave-pair form (k_stage1s_pair): a 128-thread block = two waves over the SAME
+// 64 stock-days, wave 0 computing set A and wave 1 set B from one shared LDS image of the
+// open / close / volume chunks (each wave fetches half of the rows), so those planes are
+// read from HBM once for both sets.  pbuf: that image, [2 buffers][3 planes][64 * 4].
+constexpr uint32_t kPairPlanes = 1u | 8u | 16u;  // open, close, volume
+template <uint32_t SET, bool FULL, int PAIR>
+__device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   const uint32_t fam = FULL ? SET : (a.fam & SET);
-  // a block is 256 consecutive stock-days of the flattened [D][S] order (val, state, the
-  // planes' rows, the mask and the ORD thresholds are all indexed by sd = d * S + s), so
-  // no lanes idle at the end of a day whatever S is (S = 625 per GPU at 8 GPUs)
+  // a block is 256 (pair form: 64) consecutive stock-days of the flattened [D][S] order
+  // (val, state, the planes' rows, the mask and the ORD thresholds are all indexed by
+  // sd = d * S + s), so no lanes idle at the end of a day whatever S is (S = 625 per GPU
+  // at 8 GPUs)
   const size_t plane = (size_t)a.D * a.S;
-  const size_t sd0 = (size_t)blockIdx.x * 256;
+  const int tix = PAIR ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;
+  const size_t sd0 = (size_t)blockIdx.x * (PAIR ? 64 : 256);
   // every lane walks (with LDS staging a lane also fetches other lanes' rows); lanes past
   // the last stock-day walk a copy of it and store nothing
-  const bool act = sd0 + threadIdx.x < plane;
-  const size_t sd = act ? sd0 + threadIdx.x : plane - 1;
+  const bool act = sd0 + tix < plane;
+  const size_t sd = act ? sd0 + tix : plane - 1;
 
   auto put = [&](int f, double x, uint32_t st) {
     const int r = a.row[f];
@@ -441,20 +451,26 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     // lane-linear), so each lane's ds_read_b128 of its own row is bank-conflict free.
     // OLS also stages chunk c-3 (its bars 2..15 are the bars 50 back of bars 0..13 of
     // chunk c; bars 14, 15 of chunk c-4 are carried in registers).
-    constexpr uint32_t PLM = kPlanes(SET);
+    constexpr uint32_t PLM = PAIR ? kPairPlanes : kPlanes(SET);
     constexpr int NP = __builtin_popcount(PLM);
     constexpr bool LAG = (SET & F_OLS) != 0u;
+    static_assert(!(PAIR && LAG), "the pair form covers sets A and B");
     constexpr int NB = LAG ? 2 * NP : NP;  // images: the planes, then their lag copies
     // chunk = CQ quads (4*CQ bars) per stock-day; the lag sets use 8-bar chunks so the
     // staged registers (NB*CQ float4) leave room for a third wave per SIMD
-    constexpr int CQ = (SET == kSerB || SET == kSerAB) ? 2 : 4, BC = 4 * CQ;
-    constexpr int NBUF = (SET == kSerB || SET == kSerAB) ? 2 : 1;  // chunks in flight ahead of the one in use
+    constexpr int CQ = PAIR ? 4 : (SET == kSerB || SET == kSerAB) ? 2 : 4, BC = 4 * CQ;
+    // chunks in flight ahead of the one in use (the pair form double-buffers: its DMA for
+    // chunk c+1 is issued after chunk c is read, into the other buffer)
+    constexpr int NBUF = PAIR ? 1 : (SET == kSerB || SET == kSerAB) ? 2 : 1;
     constexpr int LAGC = 48 / BC;                 // lag bar t-50 = chunk c-LAGC, element j-2
-    __shared__ __attribute__((aligned(16))) float4 sbufA[4][NB][64 * CQ];
+    __shared__ __attribute__((aligned(16))) float4 sbufA[PAIR ? 1 : 4][NB][64 * CQ];
     __shared__ __attribute__((aligned(16))) float4 sbufB[NBUF == 2 ? 4 : 1][NB][64 * CQ];
     const int lane = (int)(threadIdx.x & 63u), wave = (int)(threadIdx.x >> 6);
-    float4(*sbA)[64 * CQ] = sbufA[wave];
-    float4(*sbB)[64 * CQ] = NBUF == 2 ? sbufB[NBUF == 2 ? wave : 0] : sbufA[wave];
+    typedef float4 Img[64 * CQ];
+    Img* const pb0 = reinterpret_cast<Img*>(pbuf);
+    Img* const pb1 = PAIR ? pb0 + NB : nullptr;
+    float4(*sbA)[64 * CQ] = PAIR ? pb0 : sbufA[PAIR ? 0 : wave];
+    float4(*sbB)[64 * CQ] = NBUF == 2 ? sbufB[NBUF == 2 ? wave : 0] : sbA;
     // source-quad swizzle: a 16-lane ds_read_b128 phase touches distinct banks
     auto swz = [](int r) { return CQ == 4 ? (r >> 2) & 3 : (r >> 3) & 1; };
     const float* pbase[NP];
@@ -464,12 +480,13 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
       for (int p = 0; p < 5; ++p)
         if ((PLM >> p) & 1u) pbase[pi++] = a.fld[p];
     }
-    const size_t rowbase = sd0 + 64 * wave;
+    const size_t rowbase = sd0 + (PAIR ? 0 : 64 * wave);
     auto dma = [&](float4(*sb)[64 * CQ], int c, int img0) {
 #pragma unroll
       for (int pi = 0; pi < NP; ++pi)
 #pragma unroll
         for (int i = 0; i < CQ; ++i) {
+          if (PAIR && (i < CQ / 2) != (wave == 0)) continue;  // each wave of the pair: half the rows
           const int r = (64 / CQ) * i + lane / CQ;
           const int k = (lane % CQ) ^ swz(r);
           const size_t row = min(rowbase + r, plane - 1);
@@ -501,7 +518,20 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
     uint32_t pw1 = 0u, pw2 = 0u;  // mask words w-1, w-2
     auto step = [&](float4(*sb)[64 * CQ], int c, int h, uint32_t bits, uint32_t lbits) {
       float4 X[NB][CQ];
-      if constexpr (NBUF == 2 && NB == 2 && CQ == 2) {
+      if constexpr (PAIR) {
+        // chunk c is in buffer c & 1: this wave's half has landed (vmcnt 0), the
+        // partner's half after the barrier; read it, then fetch chunk c+1 into the other
+        // buffer (both waves finished reading it at chunk c-1, before this barrier)
+        sb = (c & 1) ? pb1 : pb0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+#pragma unroll
+        for (int ii = 0; ii < NB; ++ii)
+#pragma unroll
+          for (int k = 0; k < CQ; ++k) X[ii][k] = sb[ii][CQ * lane + (k ^ sw)];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (c + 1 < NBAR / BC) dma((c & 1) ? pb0 : pb1, c + 1, 0);
+      } else if constexpr (NBUF == 2 && NB == 2 && CQ == 2) {
         // two chunks in flight: the compiler would wait for every LDS-DMA (vmcnt(0))
         // before a ds_read, so the reads are issued here after waiting only for chunk
         // c (chunk c+1's NB*CQ DMA instructions, issued last, may stay outstanding;
@@ -527,7 +557,7 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
         // the reads have returned before the DMA refills the buffers
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
-      if (c + NBUF < NBAR / BC) {
+      if (!PAIR && c + NBUF < NBAR / BC) {
         dma(sb, c + NBUF, 0);
         if (LAG && c + 1 >= LAGC) dma(sb, c + 1 - LAGC, NP);
       }
@@ -695,6 +725,21 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
   }
 }
 
+template <uint32_t SET, bool FULL>
+__global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) {
+  s1s_body<SET, FULL, 0>(a, nullptr);
+}
+
+// The wave pair (see s1s_body): set A on wave 0, set B on wave 1 of the same 64
+// stock-days, one LDS image of the open / close / volume chunks (2 buffers x 3 planes x
+// 64 rows x 16 bars = 24 KB).  The branch is wave-uniform; both walks pass the same
+// number of barriers (one per 16-bar chunk).
+__global__ __launch_bounds__(128, 2) void k_stage1s_pair(SArgs a) {
+  __shared__ __attribute__((aligned(16))) float4 pbuf[2 * 3 * 64 * 4];
+  if (threadIdx.x < 64) s1s_body<kSerA, true, 1>(a, pbuf);
+  else s1s_body<kSerB, true, 1>(a, pbuf);
+}
+
 }  // namespace s1s
 
 // launch the serial kernel for the families of `fam` it covers (mff_stage1g.hip)
@@ -723,6 +768,14 @@ int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D
     return b;
   };
   const dim3 grid((unsigned)nblk), blk(256);
+  if (MFF_PAIR_AB && (a.fam & kSerAB) == kSerAB) {  // sets A and B in one wave-pair launch
+    hipLaunchKernelGGL(k_stage1s_pair, dim3((unsigned)(((long long)S * D + 63) / 64)), dim3(128), 0, st,
+                       patched(kSerAB));
+    if ((a.fam & kSerH) == kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, true>), grid, blk, 0, st, patched(kSerH));
+    else if (a.fam & kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, false>), grid, blk, 0, st, patched(kSerH));
+    MFF_LAUNCH_CHECK();
+    return 0;
+  }
   if (MFF_FUSE_AB && (a.fam & kSerAB) == kSerAB) {
     hipLaunchKernelGGL((k_stage1s<kSerAB, true>), grid, blk, 0, st, patched(kSerAB));
     if ((a.fam & kSerH) == kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, true>), grid, blk, 0, st, patched(kSerH));
