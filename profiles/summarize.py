@@ -1,5 +1,6 @@
 """Turn a profiles/run_profiles.sh output directory into the committed summaries:
-profiles/pmc_stage1.json (HBM bytes per stage-1 pass = the sum over its launches, read by
+profiles/pmc_stage1.json (HBM bytes per stage-1 pass = the sum over its launches incl. the
+doc_pdf sort / count, read by
 bench.py's roofline "traffic"; per-kernel values alongside) and profiles/<round>/rocprof/
 *.csv copies.
 
@@ -27,7 +28,7 @@ def counters(path, per_kernel):
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row["Kernel_Name"].split("(")[0].replace("void ", "").split("::")[-1]
-            if name.startswith("k_stage1"):
+            if name.startswith("k_stage1") or name.startswith("k_pdf"):
                 v = float(row["Counter_Value"])
                 out[row["Counter_Name"]] = out.get(row["Counter_Name"], 0.0) + v
                 k = per_kernel.setdefault(name, {})
@@ -48,7 +49,8 @@ def main():
         if d.startswith("pmc_") and os.path.exists(p):
             c.update(counters(p, per))
     fetch_kb, write_kb = c.get("FETCH_SIZE"), c.get("WRITE_SIZE")
-    res = {"kernel": "stage-1 pass (all k_stage1* launches of one step)",
+    res = {"kernel": "stage-1 pass (all k_stage1* launches of one step + the doc_pdf sort / count "
+                     "on the side stream, the launches bench.py's roofline window covers)",
            "stocks": a.stocks, "days": a.days, "round": a.tag,
            "fetch_size_kib": fetch_kb, "write_size_kib": write_kb,
            "hbm_bytes_per_launch": None if fetch_kb is None or write_kb is None
@@ -58,7 +60,7 @@ def main():
                               **v} for k, v in per.items()}}
     cal = 0.0
     for k, v in per.items():
-        f = 1.0 / 0.822 if k.startswith("k_stage1s") else 2.0
+        f = 1.0 / 0.822 if k.startswith("k_stage1s") else 2.0  # k_stage1s incl. k_stage1s_pair
         cal += (f * v.get("FETCH_SIZE", 0.0) + v.get("WRITE_SIZE", 0.0)) * 1024
     res["hbm_bytes_calibrated"] = int(cal)
     with open(os.path.join(HERE, "pmc_stage1.json"), "w") as f:
