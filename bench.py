@@ -10,10 +10,10 @@ and its cross-rank exchange) over the whole panel, inputs already resident in HB
 The panel (S stocks x D days) is sharded by stock over the ranks: total work is fixed,
 so "scaling" is "strong".  value = S*D*K / max-over-ranks(wall time of the K steps).
 
-roofline: the stage-1 pass (one mff_stage1 call = five launches: k_stage1s for the
-streaming / OLS families x3, k_stage1g for the sorted families x2, plus the small exact
-list kernel; and the doc_pdf sort / count on the side stream, whose tail the window
-includes), algorithmic bytes per pass = 5,354 B/stock-day (4,832 B OHLCV+mask in, 58 x
+roofline: the stage-1 pass (one mff_stage1 call = four launches: k_stage1g for the sorted
+families, the k_stage1s_pair wave pair for the streaming families of open / close /
+volume, k_stage1s for OLS / MOMH, the small exact-list kernel; and the doc_pdf sort /
+count on the side stream, whose tail the window includes), algorithmic bytes per pass = 5,354 B/stock-day (4,832 B OHLCV+mask in, 58 x
 9 B out) x local stock-days, over the pass's average duration from HIP
 events on its launch stream; peak 8.0 TB/s (MI355X_MICROARCH.md).  bound stays "hbm":
 the north star prices the pass against HBM bandwidth.  traffic: HBM bytes per pass from
@@ -342,9 +342,10 @@ def main():
                 "traffic": traffic,
                 "traffic_calibrated": traffic_cal,
                 "valu": valu,
-                "kernel": "stage-1 pass: k_stage1s<SEG|MOMR|TRD>, <MOMV|SUMV|SUMC|CORR>, <OLS|MOMH>, "
-                          "k_stage1g<ORD|ORDV>, <LVL|PDF> (+ k_stage1 exact list) + doc_pdf "
-                          "sort/count (side stream, inside the window)",
+                "kernel": "stage-1 pass: k_stage1g<ORD|ORDV|LVL|PDF> (sorted families), "
+                          "k_stage1s_pair (wave pair: <SEG|MOMR|TRD|ORD> + <MOMV|SUMV|SUMC|CORR>), "
+                          "k_stage1s<OLS|MOMH>, k_stage1 exact list, + doc_pdf k_pdf_sort / "
+                          "k_pdf_count on the side stream (inside the window)",
                 "bytes_per_launch": bytes_launch,
                 "avg_kernel_ms": round(k_ms, 3),
             },
