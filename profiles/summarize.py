@@ -65,7 +65,7 @@ def main():
     res["hbm_bytes_calibrated"] = int(cal)
     with open(os.path.join(HERE, "pmc_stage1.json"), "w") as f:
         json.dump(res, f, indent=1)
-    dst = os.path.join(HERE, a.tag, "rocprof")
+    dst = os.path.join(HERE, a.tag.split("-")[0], "rocprof")
     os.makedirs(dst, exist_ok=True)
     stats = os.path.join(a.src, "trace", "trace_kernel_stats.csv")
     if os.path.exists(stats):
