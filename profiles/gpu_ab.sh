@@ -1,6 +1,7 @@
 # A/B timing on one GPU box: bench with libmff_a.so (HEAD) and libmff_b.so (working
 # tree), alternating A B A B, each under rocprofv3 kernel stats (profiles/ab_build.sh).
-# VARIANTS="a b c ..." times more in-tree builds mff/libmff_<v>.so the same way.
+# VARIANTS="a b c ..." times more in-tree builds mff/libmff_<v>.so the same way;
+# ENV_<v>="NAME=value ..." sets extra environment for variant <v> (e.g. ENV_b="MFF_PDF_OVERLAP=0").
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 PKG=replication-of-minute-frequency-factor_amd
@@ -12,7 +13,9 @@ RUNS=""
 for rep in 1 2; do for v in $VARIANTS; do RUNS="$RUNS $v$rep"; done; done
 for run in $RUNS; do
   v=${run:0:1}
-  MFF_LIBRARY=$R/$PKG/mff/libmff_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/$run -o trace --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-extras --steps 3 --warmup 1 ${BENCH_ARGS:-} > $OUT/$run.log 2>&1 || { echo "RUN $run FAILED"; tail -20 $OUT/$run.log; exit 1; }
+  eval "XENV=\${ENV_$v:-}"
+  ( [ -n "$XENV" ] && export $XENV
+  MFF_LIBRARY=$R/$PKG/mff/libmff_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/$run -o trace --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-extras --steps 3 --warmup 1 ${BENCH_ARGS:-} > $OUT/$run.log 2>&1 ) || { echo "RUN $run FAILED"; tail -20 $OUT/$run.log; exit 1; }
   find $OUT/$run -name "*kernel_trace.csv" -delete
 done
 VARIANTS="$VARIANTS" python3 - <<'PY'

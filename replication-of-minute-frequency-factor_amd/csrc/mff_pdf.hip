@@ -34,6 +34,7 @@ constexpr int PDF_MAXM = 1 << 24;  // queries per day (all ranks): 2 n_less + n_
 constexpr int PDF_ZQ = 9160;     // sorted queries per count workgroup (LDS: 16 B each)
 constexpr int PDF_PAD = 64;      // ~0 sentinels after the slice's distinct values
 constexpr int PDF_NBK = 8192;    // bucket table over the workgroup's distinct query values
+constexpr int PDF_CT = 1024;     // threads per count / finalize workgroup (<= 1024: wsum[16])
 
 struct QLoader {
   const double* q;  // [R][5][D][S_loc]
@@ -241,7 +242,7 @@ struct PdfArgs {
 };
 
 template <bool FUSED>
-__global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
+__global__ __launch_bounds__(PDF_CT) void k_pdf_count(PdfArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t below_s;
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(1024) void k_pdf_count(PdfArgs a) {
 }
 
 // multi-rank finalize: counts summed over ranks -> per (day, slice) LDS lookup of own queries
-__global__ __launch_bounds__(1024) void k_pdf_finalize(PdfArgs a) {
+__global__ __launch_bounds__(PDF_CT) void k_pdf_finalize(PdfArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ int occ_s;
   __shared__ uint32_t wsum[16];
@@ -474,14 +475,14 @@ static int pdf_launch(PdfArgs& a, const uint64_t* q_sorted, int M, hipStream_t s
   if (mode == 2) {
     const long long nblk = (long long)a.Z * a.nd;
     MFF_REQUIRE(nblk < (1ll << 31), "mff_pdf_finalize: too many days in one call");
-    hipLaunchKernelGGL(k_pdf_finalize, dim3((unsigned)nblk), dim3(1024), lds, st, a);
+    hipLaunchKernelGGL(k_pdf_finalize, dim3((unsigned)nblk), dim3(PDF_CT), lds, st, a);
   } else {
     const long long nblk = ((long long)a.Z * a.nd + 7) / 8 * 8;
     MFF_REQUIRE(nblk < (1ll << 31), "mff_pdf_count: too many days in one call");
     if (mode == 1)
-      hipLaunchKernelGGL(k_pdf_count<true>, dim3((unsigned)nblk), dim3(1024), lds, st, a);
+      hipLaunchKernelGGL(k_pdf_count<true>, dim3((unsigned)nblk), dim3(PDF_CT), lds, st, a);
     else
-      hipLaunchKernelGGL(k_pdf_count<false>, dim3((unsigned)nblk), dim3(1024), lds, st, a);
+      hipLaunchKernelGGL(k_pdf_count<false>, dim3((unsigned)nblk), dim3(PDF_CT), lds, st, a);
   }
   MFF_LAUNCH_CHECK();
   return 0;

@@ -974,13 +974,16 @@ extern "C" size_t mff_pdf_levels_bytes(int S, int D) {
 
 // part bit 1: the LVL/PDF group (levels + queries) and the exact list kernel — everything
 // the doc_pdf rank needs; part bit 2: the ORD group and the serial families (which read
-// the ORD thresholds).  mff_stage1 = both, in that order.
+// the ORD thresholds).  mff_stage1 = both, in that order.  Bit 4: the high / low serial
+// kernel (OLS, MOMH) alone — it reads nothing another launch writes, so it may run on its
+// own stream from the start; bit 8 (with bit 2): part 2 without it.
 static int stage1_parts(const float* open, const float* high, const float* low, const float* close,
                         const float* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
                         int nf, double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
                         void* workspace, void* stream, int part) {
   clear_error();
-  MFF_REQUIRE(part >= 1 && part <= 3, "mff_stage1_part: part=%d must be 1, 2 or 3", part);
+  MFF_REQUIRE(part >= 1 && part <= 15 && (!(part & 8) || (part & 2)) && !((part & 4) && (part & 3)),
+              "mff_stage1_part: part=%d must be 1, 2, 3, 4, 10 or 11", part);
   MFF_REQUIRE(S > 0 && D > 0, "mff_stage1: S=%d D=%d must be positive", S, D);
   MFF_REQUIRE((long long)S * D < (1ll << 31), "mff_stage1: S*D must be < 2^31");
   MFF_REQUIRE(nf > 0 && nf <= NF, "mff_stage1: nf=%d out of range", nf);
@@ -1066,12 +1069,17 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
       if (rc != 0) return rc;
     }
   }
+  constexpr uint32_t kHL = F_OLS | F_MOMH;  // the high / low serial kernel's families
+  if (part & 4) {
+    if (w64) return 0;  // the w64 path (part 1) computed every family
+    return launch_serial(fld, valid, S, D, a.row, a.fam & kHL, val, state, a.ord_th, st);
+  }
   if ((part & 2) && !w64) {  // the ORD sort (thresholds) before the serial kernels (products)
     if (!(MFF_MERGE_OL && (a.fam & g16::G_ORD) && (a.fam & (F_LVL | F_PDF)))) {
       const int rc = group_launch(0);
       if (rc != 0) return rc;
     }
-    return launch_serial(fld, valid, S, D, a.row, a.fam, val, state, a.ord_th, st);
+    return launch_serial(fld, valid, S, D, a.row, (part & 8) ? a.fam & ~kHL : a.fam, val, state, a.ord_th, st);
   }
   return 0;
 }

@@ -111,13 +111,21 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
     if need_pdf and PDF_OVERLAP:
         # part 1 (sorted families: doc_pdf levels + queries), then the doc_pdf rank on a
         # side stream while part 2 (the serial families) runs on the launch stream
+        hl = None
+        if HL_STREAM:  # the high / low serial kernel from the start, on its own stream
+            hl = _side_stream(dev, 1)
+            hl.wait_stream(main)
+            args_hl = args[:-1] + [hl.cuda_stream]
+            _lib.check(lib.mff_stage1_part(*args_hl, 4), "mff_stage1_part(4)")
         _lib.check(lib.mff_stage1_part(*args, 1), "mff_stage1_part(1)")
         side = _side_stream(dev)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
-        _lib.check(lib.mff_stage1_part(*args, 2), "mff_stage1_part(2)")
+        _lib.check(lib.mff_stage1_part(*args, 10 if hl is not None else 2), "mff_stage1_part(2)")
         main.wait_stream(side)
+        if hl is not None:
+            main.wait_stream(hl)
         if events is not None:  # after the doc_pdf tail on the side stream
             events[1].record(main)
         return val, state, ids
@@ -131,11 +139,18 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
 
 # MFF_PDF_OVERLAP=0: doc_pdf after the whole stage-1 pass on one stream (A/B timing)
 PDF_OVERLAP = os.environ.get("MFF_PDF_OVERLAP", "1") != "0"
+# The high / low serial kernel (OLS, MOMH) reads only the high / low planes and writes
+# only its own rows, so it runs on a third stream from the start of the pass: its blocks
+# (180 VGPRs, 2 waves per SIMD) fill the VGPRs the sorted-group kernel (128, 4 waves)
+# leaves and the gaps of the doc_pdf phases (+2 % pass throughput, profiles/r02/).
+# MFF_HL_STREAM=0: launch order of round 1 (A/B timing).
+HL_STREAM = os.environ.get("MFF_HL_STREAM", "1") != "0"
+
 _SIDE = {}
 
 
-def _side_stream(dev) -> torch.cuda.Stream:
-    key = (dev.index, threading.get_ident())
+def _side_stream(dev, which: int = 0) -> torch.cuda.Stream:
+    key = (dev.index, threading.get_ident(), which)
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(dev)
     return _SIDE[key]
