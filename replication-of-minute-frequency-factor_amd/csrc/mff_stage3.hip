@@ -273,56 +273,113 @@ __global__ __launch_bounds__(SORT_THREADS) void k_xs_rank(const double* val, con
 }
 
 // Bucketed rank (M = R * S_all <= XR_PER * XR_THREADS values per (row, day)): no sort.  The
-// included values are binned by a monotone bucket function, the buckets scanned into
-// start offsets and the keys scattered bucket by bucket into LDS; the rank of x is then
+// included values are binned by a monotone two-level bucket function, the buckets scanned
+// into start offsets and the keys scattered bucket by bucket into LDS; the rank of x is
 //   #values in lower buckets + #smaller keys in its own bucket + (#equal keys + 1) / 2
 // (S6 average rank, exact: every in-bucket comparison is on the full total-order key,
-// with -0 taken as +0 like the value comparison of the oracle).  Two bucket functions
-// are tried in turn, each a histogram pass over the segment:
-//   linear  in the value between the finite min and max (uniform / normal columns);
-//   log     per sign, linear in the IEEE bits above the smallest magnitude (a
-//           log-scale histogram: heavy tails, several decades), zero its own bucket;
-// -inf / +inf take the first / last bucket in both.  A segment whose largest bucket
-// still holds more than XR_MAXB keys (heavy ties) is appended to a list for the
-// sorting kernel (k_xs_rank).
-constexpr int XR_NB = 2048;
+// with -0 taken as +0 like the value comparison of the oracle).
+//  * level 1: XB1 buckets, linear in the value between the finite min and max (scheme 0)
+//    or, when that leaves a bucket too full, per sign linear in the IEEE bits above the
+//    smallest magnitude (scheme 1: a log-scale histogram, zero its own bucket); -inf / +inf
+//    take the first / last bucket;
+//  * level 2: level-1 bucket b (c_b values) is cut into n_b = 1 + c_b * XB1 / M equal
+//    sub-ranges (sum n_b <= XB2), so a dense cluster gets proportionally finer buckets
+//    (histogram equalisation: ~M / XB1 values per bucket whatever the distribution);
+//  * ties: the key a bucket's slot 0 received is its reference; the keys equal to it are
+//    only counted, the others are packed behind them, so a bucket of one tied value (0.0,
+//    1.0, a fill value: many factors hold hundreds of exact ties per day) costs O(1) and a
+//    bucket's scan covers its non-reference keys only.
+// A segment with a bucket of more than XR_MAXO non-reference keys under both schemes is
+// appended to a list for the sorting kernel (k_xs_rank).
+constexpr int XB1 = 1024;
+constexpr int XB2 = 2048;
 constexpr int XR_PER = 8;
 constexpr int XR_THREADS = 1024;  // default block; XR_THREADS is also the kernel template parameter
-constexpr int XR_MAXB = 48;
+constexpr int XR_MAXO = 48;
 
 __global__ void k_xs_rank_list_init(uint32_t* list) { list[0] = 0u; }
 
+// packed u16 counters / offsets, two per LDS word (every count here is <= 8192)
+__device__ __forceinline__ uint32_t get16(const uint32_t* w, uint32_t i) { return (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; }
+__device__ __forceinline__ uint32_t inc16(uint32_t* w, uint32_t i) {
+  return (atomicAdd(&w[i >> 1], 1u << (16 * (i & 1))) >> (16 * (i & 1))) & 0xFFFFu;
+}
+
 struct XrBucket {
-  int scheme;        // 0 linear, 1 log
-  double xmin, scale;
+  int scheme;          // 0 linear, 1 log
+  double xmin_h, scale;
   uint64_t nlo, plo;
   int shn, shp;
-  // bucket of an included value x (x canonical: no -0)
-  __device__ __forceinline__ uint32_t operator()(double x) const {
+  const uint32_t* tab;  // LDS [XB1]: level-2 base | n << 16
+  // level-1 bucket of an included value x (x canonical: no -0) and its position in the
+  // bucket f in [0, 1] (monotone in x within the bucket)
+  __device__ __forceinline__ uint32_t l1(double x, double& f) const {
+    f = 0.0;
     if (x == -__builtin_inf()) return 0u;
-    if (x == __builtin_inf()) return XR_NB - 1;
+    if (x == __builtin_inf()) return XB1 - 1;
     if (scheme == 0) {
-      const double t = (x - xmin) * scale;
-      const int b = (int)t;  // t >= 0 and finite here
-      return 1u + (uint32_t)min(b, XR_NB - 3);
+      // halved operands: max - min cannot overflow; t >= 0 for x >= min
+      const double t = (x * 0.5 - xmin_h) * scale;
+      const double fl = floor(t);
+      const int b = min((int)fl, XB1 - 3);
+      f = t - (double)b;  // in [0, 1), or up to 2 in the clamped top bucket
+      return 1u + (uint32_t)b;
     }
-    constexpr uint32_t N1 = (XR_NB - 4) / 2;  // buckets per sign
+    constexpr uint32_t N1 = (XB1 - 4) / 2;  // buckets per sign
     if (x == 0.0) return N1 + 1u;
     const uint64_t m = (uint64_t)__double_as_longlong(fabs(x));
-    if (x < 0.0) return N1 - (uint32_t)((m - nlo) >> shn);  // 1 .. N1, larger |x| lower
-    return N1 + 2u + (uint32_t)((m - plo) >> shp);          // N1+2 .. 2 N1 + 1
+    if (x < 0.0) {
+      const uint64_t q = m - nlo;
+      f = (double)((~q) & ((1ull << shn) - 1ull)) * ldexp(1.0, -shn);  // larger |x|: lower
+      return N1 - (uint32_t)(q >> shn);                                           // 1 .. N1
+    }
+    const uint64_t q = m - plo;
+    f = (double)(q & ((1ull << shp) - 1ull)) * ldexp(1.0, -shp);
+    return N1 + 2u + (uint32_t)(q >> shp);  // N1+2 .. 2 N1 + 1
+  }
+  __device__ __forceinline__ uint32_t operator()(double x) const {
+    double f;
+    const uint32_t b = l1(x, f);
+    const uint32_t t = tab[b], n = t >> 16;
+    return (t & 0xFFFFu) + min(n - 1u, (uint32_t)(f * (double)n));
   }
 };
 
-__device__ __forceinline__ int xr_shift(uint64_t span, int bits) {  // (span >> sh) < 2^bits
-  return span == 0ull ? 0 : max(0, 64 - __builtin_clzll(span) - bits);
+// shift with (span >> sh) < N (the log scheme's buckets per sign)
+__device__ __forceinline__ int xr_shift(uint64_t span, uint32_t N) {
+  int sh = span == 0ull ? 0 : max(0, 64 - __builtin_clzll(span) - (31 - __builtin_clz(N)));
+  while ((span >> sh) >= (uint64_t)N) ++sh;
+  return sh;
+}
+
+// block-wide exclusive scan of one u32 per thread; *total = block sum.  Ends synced.
+template <int NT>
+__device__ __forceinline__ uint32_t xr_scan(uint32_t x, uint32_t* wsum, uint32_t* total) {
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+  uint32_t incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t off = incl - x, tot = 0u;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    off += w < wave ? wsum[w] : 0u;
+    tot += wsum[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return off;
 }
 
 // LOCAL (one rank: val_all == val, S_all == S): the own elements are the loaded ones, so
 // the output pass works from registers, and the next segment's values are loaded while
 // this one is ranked.  Per element a thread keeps only the canonical value (-0 -> +0),
 // the state byte (the output of an excluded VALUE is NaN: VALUE and not included means
-// NaN), its bucket and its slot in the bucket.
+// NaN), its level-2 bucket and its slot in the bucket.
 template <int PER, bool LOCAL, int XR_THREADS>
 __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREADS) void k_xs_rank_bucket(const double* val, const uint8_t* state, int rows,
                                                                    int D, int S, const double* val_all,
@@ -330,14 +387,20 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
                                                                    double* out_val, uint8_t* out_state,
                                                                    uint32_t* list) {
   __shared__ uint64_t sk[PER * XR_THREADS];
-  __shared__ uint32_t bins[XR_NB];
+  __shared__ uint32_t tab[XB1];        // level-1 -> level-2 base | n << 16
+  __shared__ uint32_t h1[XB1 / 2];     // level-1 counts (u16 x 2)
+  __shared__ uint32_t ctr[XB2 / 2];    // pack counters (u16 x 2)
+  __shared__ uint32_t bins[XB2 / 2];   // level-2 counts, then starts (u16 x 2)
+  __shared__ uint32_t eqc[XB2 / 2];    // keys equal to the bucket's reference (u16 x 2)
   __shared__ unsigned long long mm[6];  // finite min / max (ord64), neg |x| bits min / max, pos bits min / max
   __shared__ uint32_t wsum[XR_THREADS / 64];
   __shared__ uint32_t ctl[2];
+  static_assert(XB2 / 2 % XR_THREADS == 0 || XR_THREADS % (XB2 / 2) == 0, "bucket words per thread");
+  constexpr int W1 = (XB1 / 2 + XR_THREADS - 1) / XR_THREADS;  // level-1 words per thread
+  constexpr int W2 = (XB2 / 2 + XR_THREADS - 1) / XR_THREADS;  // level-2 words per thread
   const int M = R * S_all;
   const size_t nseg = (size_t)rows * D;
-  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int BPT = XR_NB / XR_THREADS;
+  const int tid = (int)threadIdx.x, lane = tid & 63;
   constexpr int NW = (PER + 3) / 4;  // state bytes packed 4 per word
   double nx[PER];
   uint32_t ns[NW];
@@ -405,80 +468,159 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
     __syncthreads();
     XrBucket bk;
     const bool fin = mm[0] != ~0ull;
-    bk.xmin = fin ? unord64(mm[0]) : 0.0;
+    const double xmin = fin ? unord64(mm[0]) : 0.0;
     const double xmax = fin ? unord64(mm[1]) : 0.0;
-    const double range = xmax - bk.xmin;
-    bk.scale = range > 0.0 ? (double)(XR_NB - 2) / range : 0.0;
+    bk.xmin_h = xmin * 0.5;
+    const double range_h = xmax * 0.5 - bk.xmin_h;
+    bk.scale = range_h > 0.0 ? (double)(XB1 - 2) / range_h : 0.0;
     bk.nlo = bk.plo = 0ull;
     bk.shn = bk.shp = 0;
-    uint32_t bp[PER];  // bucket << 16 | slot in the bucket
-    uint32_t c[BPT], off = 0u, tot = 0u;
+    bk.tab = tab;
+    uint32_t bp[PER];  // level-2 bucket << 16 | slot in the bucket
+    uint32_t isref = 0u;
+    uint32_t tot = 0u;
     bool ok = false;
-    for (int scheme = (__builtin_isfinite(range) ? 0 : 1); scheme < 2 && !ok; ++scheme) {
+    // a range of a few denormals overflows the linear scale: log scheme only
+    for (int scheme = __builtin_isfinite(bk.scale) ? 0 : 1; scheme < 2 && !ok; ++scheme) {
       bk.scheme = scheme;
       if (scheme == 1) {
         stats(2, 6, x, inc);
         __syncthreads();
         bk.nlo = mm[2];
         bk.plo = mm[4];
-        bk.shn = xr_shift(mm[2] == ~0ull ? 0ull : mm[3] - mm[2], 10);  // < 1022 buckets per sign
-        bk.shp = xr_shift(mm[4] == ~0ull ? 0ull : mm[5] - mm[4], 10);
+        constexpr uint32_t N1 = (XB1 - 4) / 2;  // buckets per sign
+        bk.shn = xr_shift(mm[2] == ~0ull ? 0ull : mm[3] - mm[2], N1);
+        bk.shp = xr_shift(mm[4] == ~0ull ? 0ull : mm[5] - mm[4], N1);
       }
-      for (int b = tid; b < XR_NB; b += XR_THREADS) bins[b] = 0u;
+      // level 1: histogram -> sub-bucket counts -> level-2 bases
+      for (int w = tid; w < XB1 / 2; w += XR_THREADS) h1[w] = 0u;
+      for (int w = tid; w < XB2 / 2; w += XR_THREADS) { bins[w] = 0u; eqc[w] = 0u; }
       if (tid == 0) ctl[0] = 0u;
       __syncthreads();
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
-        const uint32_t b = bk(x[j]);
-        bp[j] = ((inc >> j) & 1u) ? (b << 16) | atomicAdd(&bins[b], 1u) : 0u;
+        if ((inc >> j) & 1u) {
+          double f;
+          inc16(h1, bk.l1(x[j], f));
+        }
       }
       __syncthreads();
-      uint32_t loc = 0u, mb = 0u;
+      {
+        uint32_t nb[2 * W1], loc = 0u;
 #pragma unroll
-      for (int q = 0; q < BPT; ++q) {
-        c[q] = bins[BPT * tid + q];
-        loc += c[q];
-        mb = max(mb, c[q]);
+        for (int q = 0; q < W1; ++q) {
+          const int w = tid * W1 + q;
+          const uint32_t cw = w < XB1 / 2 ? h1[w] : 0u;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t c = (cw >> (16 * h)) & 0xFFFFu;
+            // 1 + c * XB1 / M sub-ranges: sum <= XB1 + XB1 = XB2
+            nb[2 * q + h] = c ? 1u + (uint32_t)((c * (uint32_t)XB1) / (uint32_t)M) : 0u;
+            loc += nb[2 * q + h];
+          }
+        }
+        uint32_t all;
+        uint32_t off = xr_scan<XR_THREADS>(loc, wsum, &all);
+#pragma unroll
+        for (int q = 0; q < W1; ++q)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int b = 2 * (tid * W1 + q) + h;
+            if (b < XB1) tab[b] = off | (nb[2 * q + h] << 16);
+            off += nb[2 * q + h];
+          }
       }
-      uint32_t incl = loc;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
-        if (lane >= o) incl += y;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) mb = max(mb, (uint32_t)__shfl_xor((int)mb, o, 64));
-      if (lane == 63) wsum[wave] = incl;
-      if (lane == 0) atomicMax(&ctl[0], mb);
       __syncthreads();
-      off = incl - loc;
-      tot = 0u;
-      for (int w = 0; w < XR_THREADS / 64; ++w) {
-        off += w < wave ? wsum[w] : 0u;
-        tot += wsum[w];
+      // level 2: histogram (slots) -> starts
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if ((inc >> j) & 1u) {
+          const uint32_t b = bk(x[j]);
+          bp[j] = (b << 16) | inc16(bins, b);
+        } else {
+          bp[j] = 0u;
+        }
       }
-      ok = ctl[0] <= (uint32_t)XR_MAXB;  // block-uniform
+      __syncthreads();
+      {
+        uint32_t cw[W2], loc = 0u;
+#pragma unroll
+        for (int q = 0; q < W2; ++q) {
+          const int w = tid * W2 + q;
+          cw[q] = w < XB2 / 2 ? bins[w] : 0u;
+          loc += (cw[q] & 0xFFFFu) + (cw[q] >> 16);
+        }
+        uint32_t off = xr_scan<XR_THREADS>(loc, wsum, &tot);
+#pragma unroll
+        for (int q = 0; q < W2; ++q) {
+          const int w = tid * W2 + q;
+          const uint32_t c0 = cw[q] & 0xFFFFu;
+          if (w < XB2 / 2) bins[w] = off | ((off + c0) << 16);
+          off += c0 + (cw[q] >> 16);
+        }
+      }
+      __syncthreads();
+      // scatter; the key at a bucket's slot 0 is its reference
+#pragma unroll
+      for (int j = 0; j < PER; ++j)
+        if ((inc >> j) & 1u) sk[get16(bins, bp[j] >> 16) + (bp[j] & 0xFFFFu)] = ord64(x[j]);
+      __syncthreads();
+      isref = 0u;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if ((inc >> j) & 1u) {
+          const uint32_t b = bp[j] >> 16;
+          if (sk[get16(bins, b)] == ord64(x[j])) {
+            isref |= 1u << j;
+            inc16(eqc, b);
+          }
+        }
+      }
+      __syncthreads();
+      // the fullest bucket's non-reference keys
+      uint32_t mo = 0u;
+#pragma unroll
+      for (int q = 0; q < W2; ++q) {
+        const int w = tid * W2 + q;
+        if (w < XB2 / 2) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const uint32_t b = 2 * (uint32_t)w + h;
+            const uint32_t b1 = b + 1 < (uint32_t)XB2 ? get16(bins, b + 1) : tot;
+            mo = max(mo, b1 - get16(bins, b) - get16(eqc, b));
+          }
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) mo = max(mo, (uint32_t)__shfl_xor((int)mo, o, 64));
+      if (lane == 0) atomicMax(&ctl[0], mo);
+      __syncthreads();
+      ok = ctl[0] <= (uint32_t)XR_MAXO;  // block-uniform
       __syncthreads();
     }
     if (!ok) {  // hand the segment to the sorting kernel
       if (tid == 0) list[1 + atomicAdd(&list[0], 1u)] = (uint32_t)seg;
       continue;
     }
-#pragma unroll
-    for (int q = 0; q < BPT; ++q) {
-      bins[BPT * tid + q] = off;
-      off += c[q];
-    }
+    // pack each bucket's non-reference keys behind its reference-equal run (the
+    // reference stays at slot 0: the packed keys start at slot eqc >= 1)
+    for (int w = tid; w < XB2 / 2; w += XR_THREADS) ctr[w] = 0u;
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < PER; ++j)
-      if ((inc >> j) & 1u) sk[bins[bp[j] >> 16] + (bp[j] & 0xFFFFu)] = ord64(x[j]);
+    for (int j = 0; j < PER; ++j) {
+      if (((inc & ~isref) >> j) & 1u) {
+        const uint32_t b = bp[j] >> 16;
+        sk[get16(bins, b) + get16(eqc, b) + inc16(ctr, b)] = ord64(x[j]);
+      }
+    }
     __syncthreads();
     auto rank_of = [&](double cv, uint32_t b) {
       const uint64_t kk = ord64(cv);
-      const uint32_t b0 = bins[b], b1 = b + 1 < (uint32_t)XR_NB ? bins[b + 1] : tot;
-      uint32_t less = b0, eq = 0u;
-      for (uint32_t q = b0; q < b1; ++q) {
+      const uint32_t b0 = get16(bins, b), e = get16(eqc, b);
+      const uint32_t b1 = b + 1 < (uint32_t)XB2 ? get16(bins, b + 1) : tot;
+      const uint64_t ref = sk[b0];
+      uint32_t less = b0 + (ref < kk ? e : 0u), eq = ref == kk ? e : 0u;
+      for (uint32_t q = b0 + e; q < b1; ++q) {
         const uint64_t y = sk[q];
         less += y < kk ? 1u : 0u;
         eq += y == kk ? 1u : 0u;
@@ -600,16 +742,9 @@ int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_
     MFF_REQUIRE(nseg < (1ll << 32), "mff_xs_rank: too many segments");
     hipLaunchKernelGGL(k_xs_rank_list_init, dim3(1), dim3(1), 0, st, list);
     const int gb = (int)(nseg < 4 * XS_RANK_GRID ? nseg : 4 * XS_RANK_GRID);
-    // MFF_XS_RANK_IMPL=b512 / b256: other block sizes (A/B timing; 1024 measured fastest:
-    // 8 factors at c4 1.19 ms vs 1.35 (512) and 1.71 (256))
-    const int thr = (impl && impl[0] == 'b') ? atoi(impl + 1) : XR_THREADS;
-    auto kern = k_xs_rank_bucket<10, true, 512>;
-    if (thr == 1024) kern = R == 1 ? (M <= 5 * 1024 ? k_xs_rank_bucket<5, true, 1024> : k_xs_rank_bucket<8, true, 1024>)
-                                   : (M <= 5 * 1024 ? k_xs_rank_bucket<5, false, 1024> : k_xs_rank_bucket<8, false, 1024>);
-    else if (thr == 256) kern = R == 1 ? (M <= 20 * 256 ? k_xs_rank_bucket<20, true, 256> : k_xs_rank_bucket<32, true, 256>)
-                                       : (M <= 20 * 256 ? k_xs_rank_bucket<20, false, 256> : k_xs_rank_bucket<32, false, 256>);
-    else kern = R == 1 ? (M <= 10 * 512 ? k_xs_rank_bucket<10, true, 512> : k_xs_rank_bucket<16, true, 512>)
-                       : (M <= 10 * 512 ? k_xs_rank_bucket<10, false, 512> : k_xs_rank_bucket<16, false, 512>);
+    constexpr int thr = XR_THREADS;
+    auto kern = R == 1 ? (M <= 5 * thr ? k_xs_rank_bucket<5, true, thr> : k_xs_rank_bucket<8, true, thr>)
+                       : (M <= 5 * thr ? k_xs_rank_bucket<5, false, thr> : k_xs_rank_bucket<8, false, thr>);
     hipLaunchKernelGGL(kern, dim3(gb), dim3(thr), 0, st, val, state, rows, D, S_loc, val_all,
                        state_all, R, S_all, out_val, out_state, list);
     MFF_LAUNCH_CHECK();

@@ -249,6 +249,40 @@ def test_stage3_live(dev, kind, S, ties):
     assert not bad, "\n".join(bad)
 
 
+@pytest.mark.parametrize("S", [5000, 8000])
+def test_stage3_rank_distributions(dev, S):
+    """The bucketed rank on the distributions that defeat a one-level histogram: one
+    dominant exact tie (1.0) among near values, two tie groups one ulp apart, a dense
+    cluster with far outliers (lognormal sigma 6), a range of a few denormals, only
+    infinities and zeros of both signs, integer-valued days (heavy ties everywhere), a
+    day of one value; S = 8000 runs the 8-per-thread instantiation."""
+    import mff_oracle as O
+    from mff import engine
+    rng = np.random.default_rng(S + 1)
+    D = 8
+    val = np.empty((D, S))
+    val[0] = np.where(rng.random(S) < 0.5, 1.0, 1.0 + rng.integers(-30, 30, S) * 1e-3)
+    val[1] = np.where(rng.random(S) < 0.4, 0.5, np.nextafter(0.5, 1.0))
+    m = rng.random(S) < 0.2
+    val[1, m] = 0.5 + rng.normal(size=int(m.sum())) * 1e-9
+    val[2] = rng.lognormal(0.0, 6.0, S) * rng.choice([-1.0, 1.0], S)
+    val[3] = rng.integers(0, 9, S) * 5e-324
+    val[4] = rng.choice([np.inf, -np.inf, 0.0, -0.0, 1.0], S)
+    val[5] = rng.integers(-3, 4, S).astype(float)
+    val[6] = 3.25
+    val[7] = np.where(rng.random(S) < 0.7, 0.0, rng.normal(size=S) * 1e-12)
+    val[rng.random(val.shape) < 0.02] = np.nan
+    state = np.full(val.shape, 2, np.uint8)
+    state[rng.random(val.shape) < 0.03] = 1
+    state[rng.random(val.shape) < 0.03] = 0
+    ov, os_ = O.oracle_stage3(val, state, "rank")
+    rv, rs = engine.cross_section(torch.from_numpy(val[None]).to(dev), torch.from_numpy(state[None]).to(dev),
+                                  "rank")
+    torch.cuda.synchronize()
+    bad = compare(rv[0].cpu().numpy(), rs[0].cpu().numpy(), ov, os_, "xs/rank", atol=0.0, rtol=0.0)
+    assert not bad, "\n".join(bad)
+
+
 def test_stage3_golden(dev):
     from golden.make_golden import STAGE23_FACTORS
     from mff import engine, catalog
