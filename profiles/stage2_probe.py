@@ -36,23 +36,26 @@ def main():
         ms = a.elapsed_time(b) / reps
         return round(ms, 3), round(nbytes / (ms * 1e-3) / 1e9, 1)
 
-    for N, meth in [(20, "o"), (20, "m"), (20, "z"), (20, "std"), (5, "z"), (60, "z"), (7, "z"),
-                    (120, "z"), (250, "z")]:
+    cases = [(20, "o"), (20, "m"), (20, "z"), (20, "std"), (5, "z"), (60, "z"), (7, "z"), (120, "z"), (250, "z")]
+    if "quick" in sys.argv[1:]:  # the A/B subset
+        cases = [(20, "o"), (20, "z"), (5, "z"), (60, "z")]
+    for N, meth in cases:
         res[f"stage2_N{N}_{meth}"] = t(lambda: engine.rolling(val, state, N, meth))
-    for impl in ("ring", "slide"):
-        os.environ["MFF_STAGE2_IMPL"] = impl
-        for N, meth in [(20, "m"), (20, "z"), (5, "z"), (60, "z")]:
-            res[f"stage2_{impl}_N{N}_{meth}"] = t(lambda: engine.rolling(val, state, N, meth))
-    del os.environ["MFF_STAGE2_IMPL"]
-    res["stage3_z"] = t(lambda: engine.cross_section(val, state, "z"))
-    nb = nbytes
-    nbytes = nb * 8 / 58
-    res["stage3_rank_8factors"] = t(lambda: engine.cross_section(val[:8], state[:8], "rank"))
-    for impl in ("b256", "b512", "sort"):
-        os.environ["MFF_XS_RANK_IMPL"] = impl
-        res[f"stage3_rank_8factors_{impl}"] = t(lambda: engine.cross_section(val[:8], state[:8], "rank"))
-    del os.environ["MFF_XS_RANK_IMPL"]
-    nbytes = nb
+    if "quick" not in sys.argv[1:]:
+        for impl in ("ring", "slide"):
+            os.environ["MFF_STAGE2_IMPL"] = impl
+            for N, meth in [(20, "m"), (20, "z"), (5, "z"), (60, "z")]:
+                res[f"stage2_{impl}_N{N}_{meth}"] = t(lambda: engine.rolling(val, state, N, meth))
+        del os.environ["MFF_STAGE2_IMPL"]
+        res["stage3_z"] = t(lambda: engine.cross_section(val, state, "z"))
+        nb = nbytes
+        nbytes = nb * 8 / 58
+        res["stage3_rank_8factors"] = t(lambda: engine.cross_section(val[:8], state[:8], "rank"))
+        res["stage3_rank_8factors_sort"] = None
+        os.environ["MFF_XS_RANK_IMPL"] = "sort"
+        res["stage3_rank_8factors_sort"] = t(lambda: engine.cross_section(val[:8], state[:8], "rank"))
+        del os.environ["MFF_XS_RANK_IMPL"]
+        nbytes = nb
     print(json.dumps(res), flush=True)
 
 
