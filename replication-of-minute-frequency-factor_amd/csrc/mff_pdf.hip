@@ -20,6 +20,10 @@
 //   3. finalize — each own query looks its position up in its slice (LDS) and writes the
 //                rank.  With one rank, 2 and 3 run as one kernel (mff_pdf_rank_local):
 //                the slice's counters never leave LDS.
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "../../include/mff.h"
 #include "mff_internal.h"
 #include "mff_sort.h"
@@ -31,10 +35,18 @@ namespace mff {
 size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w);  // mff_stage1g.hip
 
 constexpr int PDF_MAXM = 1 << 24;  // queries per day (all ranks): 2 n_less + n_eq stays in u32
-constexpr int PDF_ZQ = 9160;     // sorted queries per count workgroup (LDS: 16 B each)
+constexpr int PDF_ZQ = 9160;     // sorted queries per workgroup, u64 counters (LDS: 16 B each)
+constexpr int PDF_ZQ32 = 12500;  // sorted queries per count workgroup, packed u32 counters (12 B)
 constexpr int PDF_PAD = 64;      // ~0 sentinels after the slice's distinct values
-constexpr int PDF_NBK = 8192;    // bucket table over the workgroup's distinct query values
+constexpr int PDF_NBK = 4096;    // bucket table over the workgroup's distinct query values
 constexpr int PDF_CT = 1024;     // threads per count / finalize workgroup (<= 1024: wsum[16])
+// packed counter: n_less part in the low PDF_LB bits, n_eq part above.  Exact while a
+// slice's total weight stays below 2^PDF_LB (240 bars x S_loc < 2^21: S_loc <= 8738) and
+// no single value collects 2^(32 - PDF_LB) equal keys -- the latter is detected (the
+// fields no longer sum to the slice's weight) and the slice recounted with u64 counters.
+// The one value every stock-day holds is 1.0 (c_last / c_last: the last close's level),
+// so its equal keys are counted apart, in a full u32.
+constexpr int PDF_LB = 21;
 
 struct QLoader {
   const double* q;  // [R][5][D][S_loc]
@@ -122,34 +134,46 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, 
 // stock-days share e.g. the key 1.0 -- would otherwise deepen every search), build the
 // bucket table and the search depth.  Block-wide; ends synced.
 //   L[0] = Q[P0-1], L[1..nv] = distinct slice values > L[0], L[nv+1 .. nv+PDF_PAD] = ~0
+// C32 (the packed-counter slice): C is a u32 array too small for the compaction's
+// staging, so the distinct values are written straight into L from a second read of the
+// slice in global memory (L2-hot), and the counters zeroed as u32.
+template <typename CT>
 __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, int P0, int P1,
-                                                    uint64_t* L, uint64_t* C, uint16_t* T,
+                                                    uint64_t* L, CT* C, uint16_t* T,
                                                     uint32_t* wsum, int* occ_s) {
+  constexpr bool C32 = sizeof(CT) == 4;
   const int nq = P1 - P0;
-  for (int i = threadIdx.x; i < nq; i += blockDim.x) L[1 + i] = Q[P0 + i];
+  if (!C32)
+    for (int i = threadIdx.x; i < nq; i += blockDim.x) L[1 + i] = Q[P0 + i];
+  const uint64_t L0 = P0 > 0 ? Q[P0 - 1] : 0ull;
   if (threadIdx.x == 0) {
-    L[0] = P0 > 0 ? Q[P0 - 1] : 0ull;
+    L[0] = L0;
     *occ_s = 0;
   }
   __syncthreads();
-  // compaction: a thread's contiguous chunk -> distinct values into C, then back to L
+  // compaction: a thread's contiguous chunk -> distinct values (into C, then back to L;
+  // C32: straight into L after the offsets are known)
   const int per = (nq + (int)blockDim.x - 1) / (int)blockDim.x;
   const int i0 = min(nq, (int)threadIdx.x * per), i1 = min(nq, i0 + per);
-  const uint64_t L0 = L[0];
+  auto at = [&](int i) { return C32 ? Q[P0 + i] : L[1 + i]; };  // slice element i (i >= -1)
   uint32_t cnt = 0u;
   for (int i = i0; i < i1; ++i) {
-    const uint64_t x = L[1 + i];
-    cnt += (x != ~0ull && x > L0 && x != L[i]) ? 1u : 0u;
+    const uint64_t x = at(i), xp = i > 0 ? at(i - 1) : L0;
+    cnt += (x != ~0ull && x > L0 && x != xp) ? 1u : 0u;
   }
   uint32_t nu;
   uint32_t off = block_excl_scan(cnt, wsum, &nu);
   for (int i = i0; i < i1; ++i) {
-    const uint64_t x = L[1 + i];
-    if (x != ~0ull && x > L0 && x != L[i]) C[off++] = x;
+    const uint64_t x = at(i), xp = i > 0 ? at(i - 1) : L0;
+    if (x != ~0ull && x > L0 && x != xp) {
+      if (C32) L[1 + off++] = x;
+      else reinterpret_cast<uint64_t*>(C)[off++] = x;
+    }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < (int)nu; i += blockDim.x) L[1 + i] = C[i];
-  for (int i = threadIdx.x; i < nq; i += blockDim.x) C[i] = 0ull;
+  if (!C32)
+    for (int i = threadIdx.x; i < (int)nu; i += blockDim.x) L[1 + i] = reinterpret_cast<uint64_t*>(C)[i];
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) C[i] = (CT)0;
   if (threadIdx.x < PDF_PAD) L[1 + nu + threadIdx.x] = ~0ull;
   __syncthreads();
   PdfSlice sl;
@@ -239,33 +263,32 @@ struct PdfArgs {
   uint8_t* state;
   int rows[5];
   int S, D, d0, nd, M, Z, Mz;
+  int packed;  // count: u32 packed counters (PDF_LB), u64 recount on overflow
 };
 
-template <bool FUSED>
-__global__ __launch_bounds__(PDF_CT) void k_pdf_count(PdfArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t below_s;
-  __shared__ int occ_s;
-  // XCD-aware block order: hardware dispatches block b to XCD b % 8; the Z slices of a
-  // day get consecutive logical ids on one XCD (they share the day's close plane in L2)
-  const int per_xcd = gridDim.x >> 3;  // host pads the grid to a multiple of 8
-  const int lid = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-  const int dd = lid / a.Z, z = lid % a.Z;
-  if (dd >= a.nd) return;
-  const int d = a.d0 + dd;
+// One (day, slice [P0, P1)) count.  C32: packed u32 counters (n_less part low, n_eq part
+// high); returns false -- before writing anything -- when an n_eq field overflowed, so the
+// caller recounts the slice with u64 counters.
+template <bool FUSED, bool C32>
+__device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd, int P0, int P1, int mz,
+                                                unsigned char* smem, uint32_t* wsum, uint32_t* below_s,
+                                                uint32_t* inw_s, uint32_t* one_s, int* occ_s) {
+  constexpr uint64_t K1 = 0xBFF0000000000000ull;  // ord64(1.0)
+  typedef typename std::conditional<C32, uint32_t, uint64_t>::type CT;
   const int S = a.S;
   const uint64_t* Q = a.q_sorted + (size_t)dd * a.M;
-  const int P0 = z * a.Mz, P1 = min(a.M, P0 + a.Mz);
   const int nq = P1 - P0;
+  uint64_t* L = reinterpret_cast<uint64_t*>(smem);  // [mz + 1 + PDF_PAD]
+  CT* C = reinterpret_cast<CT*>(L + mz + 1 + PDF_PAD);  // [mz]
+  uint16_t* T = reinterpret_cast<uint16_t*>(C + mz);
+  if (threadIdx.x == 0) {
+    *below_s = 0u;
+    *inw_s = 0u;
+    *one_s = 0u;
+  }
+  const PdfSlice sl = pdf_slice_setup(Q, a.M, P0, P1, L, C, T, wsum, occ_s);
 
-  uint64_t* L = reinterpret_cast<uint64_t*>(smem);  // [Mz + 1 + PDF_PAD]
-  uint64_t* C = L + a.Mz + 1 + PDF_PAD;             // [Mz]
-  uint16_t* T = reinterpret_cast<uint16_t*>(C + a.Mz);
-  if (threadIdx.x == 0) below_s = 0u;
-  const PdfSlice sl = pdf_slice_setup(Q, a.M, P0, P1, L, C, T, wsum, &occ_s);
-
-  uint32_t below = 0u;
+  uint32_t below = 0u, inw = 0u;
   if (sl.nv > 0) {
     // The day's level list is flat (stage 1 appends every stock-day's levels: key =
     // c_last / c as ord64, weight = bars at the level), so a thread simply takes every
@@ -303,6 +326,7 @@ __global__ __launch_bounds__(PDF_CT) void k_pdf_count(PdfArgs a) {
         const bool bl = key[u] <= sl.L0;  // (padding entries have weight 0)
         in[u] = !bl && key[u] <= sl.qmax;
         below += bl ? w[u] : 0u;
+        inw += in[u] ? w[u] : 0u;
         const bool gtmin = key[u] > sl.qmin;
         const int bk = (in[u] && gtmin) ? (int)((key[u] - sl.qmin) >> sl.sh) : 0;
         j[u] = (in[u] && gtmin) ? (int)sl.T[bk] - 1 : -1;
@@ -335,32 +359,117 @@ __global__ __launch_bounds__(PDF_CT) void k_pdf_count(PdfArgs a) {
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const uint64_t x = L1[j[u] + 1];
-        if (in[u]) atomicAdd((unsigned long long*)&C[j[u] + 1], x == key[u] ? ((uint64_t)w[u] << 32) : (uint64_t)w[u]);
+        if (in[u]) {
+          if (C32 && x == key[u] && key[u] == K1) atomicAdd(one_s, w[u]);
+          else if (C32) atomicAdd(reinterpret_cast<uint32_t*>(&C[j[u] + 1]), x == key[u] ? (w[u] << PDF_LB) : w[u]);
+          else atomicAdd(reinterpret_cast<unsigned long long*>(&C[j[u] + 1]),
+                         x == key[u] ? ((uint64_t)w[u] << 32) : (uint64_t)w[u]);
+        }
       }
     }
     below = (uint32_t)__reduce_add_sync(~0ull, (int)below);
-    if (lane_id() == 0) atomicAdd(&below_s, below);
+    inw = (uint32_t)__reduce_add_sync(~0ull, (int)inw);
+    if (lane_id() == 0) {
+      atomicAdd(below_s, below);
+      atomicAdd(inw_s, inw);
+    }
   }
   __syncthreads();
-  pdf_slice_scan(C, sl.nv, below_s, wsum);
+  if (C32) {
+    // packed fields -> 2 n_less + n_eq per distinct value; the fields must sum to the
+    // slice's in-range weight (else an n_eq field wrapped: recount with u64 counters)
+    uint32_t* C2 = reinterpret_cast<uint32_t*>(C);
+    const int per = (sl.nv + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int i0 = min(sl.nv, (int)threadIdx.x * per), i1 = min(sl.nv, i0 + per);
+    const uint32_t one = *one_s;
+    auto eq_at = [&](int i) { return (C2[i] >> PDF_LB) + (L[1 + i] == K1 ? one : 0u); };
+    uint32_t tot = 0u;
+    for (int i = i0; i < i1; ++i) tot += (C2[i] & ((1u << PDF_LB) - 1u)) + eq_at(i);
+    uint32_t all;
+    uint32_t run = *below_s + block_excl_scan(tot, wsum, &all);
+    if (all != *inw_s) return false;  // block-uniform; nothing written yet
+    for (int i = i0; i < i1; ++i) {
+      const uint32_t lt = C2[i] & ((1u << PDF_LB) - 1u), eq = eq_at(i);
+      C2[i] = 2u * (run + lt) + eq;
+      run += lt + eq;
+    }
+    __syncthreads();
+  } else {
+    pdf_slice_scan(reinterpret_cast<uint64_t*>(C), sl.nv, *below_s, wsum);
+  }
+  // per distinct value: 2 n_less + n_eq (C32) or n_less | n_eq << 32
+  auto twice_rank = [&](int j) -> uint32_t {
+    if (C32) return reinterpret_cast<const uint32_t*>(C)[j];
+    const uint64_t cn = reinterpret_cast<const uint64_t*>(C)[j];
+    return 2u * (uint32_t)cn + (uint32_t)(cn >> 32);
+  };
   if (FUSED) {
-    pdf_slice_resolve(sl, C, a.q_local, S, a.D, d, a.rows, a.val, a.state);
+    // own queries [5][D][S] of day d that fall in this slice -> rank (S6 average)
+    if (sl.nv > 0) {
+      const size_t plane = (size_t)a.D * S;
+      for (int i = threadIdx.x; i < 5 * S; i += blockDim.x) {
+        const int t = i / S, s = i - t * S;
+        if (a.rows[t] < 0) continue;
+        const double q = a.q_local[(size_t)t * plane + (size_t)d * S + s];
+        if (__builtin_isnan(q)) continue;  // no level passed (null) or absent stock-day
+        const uint64_t key = ord64(q);
+        if (key <= sl.L0 || key > sl.qmax) continue;  // another slice owns its first copy
+        int lo, hi;
+        sl.range(key, lo, hi);
+        const uint32_t c2 = twice_rank(lower_bound_u64(sl.L + 1, lo, hi, key));
+        const size_t o = (size_t)a.rows[t] * plane + (size_t)d * S + s;
+        a.val[o] = ((double)c2 + 1.0) * 0.5;
+        a.state[o] = MFF_STATE_VALUE;
+      }
+    }
   } else {
     // per sorted position: the counts of its distinct value (positions holding Q[P0-1]
-    // or NaN are never looked up)
-    // one word per position, 2 n_less + n_eq: the average rank n_less + (n_eq + 1) / 2
-    // = (2 n_less + n_eq + 1) / 2 is linear in it, so the ranks' words simply add up
+    // or NaN are never looked up); one word per position, 2 n_less + n_eq: the average
+    // rank n_less + (n_eq + 1) / 2 = (2 n_less + n_eq + 1) / 2 is linear in it, so the
+    // ranks' words simply add up
     uint32_t* out = a.counts + (size_t)dd * a.M + P0;
     for (int i = threadIdx.x; i < nq; i += blockDim.x) {
       const uint64_t x = Q[P0 + i];
-      uint64_t cn = 0ull;
+      uint32_t c2 = 0u;
       if (x > sl.L0 && x <= sl.qmax) {
         int lo, hi;
         sl.range(x, lo, hi);
-        cn = C[lower_bound_u64(L + 1, lo, hi, x)];
+        c2 = twice_rank(lower_bound_u64(L + 1, lo, hi, x));
       }
-      out[i] = 2u * (uint32_t)cn + (uint32_t)(cn >> 32);
+      out[i] = c2;
     }
+  }
+  __syncthreads();  // the LDS is reused by the next slice count of this workgroup
+  return true;
+}
+
+// One workgroup per (day, slice of <= Mz sorted queries).  a.packed: u32 counters (the
+// slice twice as long as with u64 ones: every slice re-reads the day's level list, the
+// kernel's dominant traffic), a slice whose n_eq field overflowed recounted as two halves
+// with u64 counters.
+template <bool FUSED>
+__global__ __launch_bounds__(PDF_CT) void k_pdf_count(PdfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t below_s, inw_s, one_s;
+  __shared__ int occ_s;
+  // XCD-aware block order: hardware dispatches block b to XCD b % 8; the Z slices of a
+  // day get consecutive logical ids on one XCD (they share the day's level list in L2)
+  const int per_xcd = gridDim.x >> 3;  // host pads the grid to a multiple of 8
+  const int lid = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+  const int dd = lid / a.Z, z = lid % a.Z;
+  if (dd >= a.nd) return;
+  const int d = a.d0 + dd;
+  const int P0 = z * a.Mz, P1 = min(a.M, P0 + a.Mz);
+  if (a.packed) {
+    if (!pdf_count_slice<FUSED, true>(a, d, dd, P0, P1, a.Mz, smem, wsum, &below_s, &inw_s, &one_s, &occ_s)) {
+      __syncthreads();
+      const int mid = P0 + (P1 - P0 + 1) / 2;
+      pdf_count_slice<FUSED, false>(a, d, dd, P0, mid, mid - P0, smem, wsum, &below_s, &inw_s, &one_s, &occ_s);
+      pdf_count_slice<FUSED, false>(a, d, dd, mid, P1, P1 - mid, smem, wsum, &below_s, &inw_s, &one_s, &occ_s);
+    }
+  } else {
+    pdf_count_slice<FUSED, false>(a, d, dd, P0, P1, a.Mz, smem, wsum, &below_s, &inw_s, &one_s, &occ_s);
   }
 }
 
@@ -461,15 +570,19 @@ int mff_pdf_sort(const double* q_all, int R, int S_loc, int D, int d0, int nd, u
   return 0;
 }
 
-static void pdf_slices(int M, int& Z, int& Mz, size_t& lds) {
-  Z = (M + PDF_ZQ - 1) / PDF_ZQ;
+static void pdf_slices(int M, int& Z, int& Mz, size_t& lds, bool packed) {
+  Z = (M + (packed ? PDF_ZQ32 : PDF_ZQ) - 1) / (packed ? PDF_ZQ32 : PDF_ZQ);
   Mz = (M + Z - 1) / Z;
-  lds = (size_t)(Mz + 1 + PDF_PAD) * 8 + (size_t)Mz * 8 + (size_t)(PDF_NBK + 1) * 2;
+  // packed: L u64 + C u32 (the u64 recount's half slices fit the same bytes)
+  lds = (size_t)(Mz + 1 + PDF_PAD) * 8 + (size_t)Mz * (packed ? 4 : 8) + (size_t)(PDF_NBK + 1) * 2;
 }
 
 static int pdf_launch(PdfArgs& a, const uint64_t* q_sorted, int M, hipStream_t st, int mode) {
   size_t lds;
-  pdf_slices(M, a.Z, a.Mz, lds);
+  // packed counters for the count phases while a slice's weight (<= 240 bars per stock of
+  // this rank) fits the n_less field
+  a.packed = mode != 2 && (long long)NBAR * a.S < (1ll << PDF_LB) && getenv("MFF_PDF_U64") == nullptr;
+  pdf_slices(M, a.Z, a.Mz, lds, a.packed);
   a.q_sorted = q_sorted;
   a.M = M;
   if (mode == 2) {

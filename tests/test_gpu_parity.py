@@ -129,12 +129,31 @@ def test_doc_pdf_merge_path(dev):
 
 
 def test_doc_pdf_four_slices(dev):
-    """M = 5*S = 25,000 queries per day: four LDS query slices in mff_pdf_count, with the
-    bench's stock count (ranks exact, tolerance 0)."""
+    """M = 5*S = 25,000 queries per day (the bench's stock count): two packed-counter LDS
+    query slices in mff_pdf_count (three with MFF_PDF_U64; ranks exact, tolerance 0)."""
     import mff_oracle as O
     from mff import synth
     panel = synth.make_panel(5000, 1, config=13)
     names = ["doc_pdf70", "doc_pdf80", "doc_pdf90"]
+    ov, os_ = O.oracle_stage1(panel, names)
+    gv, gs, _ = _run_stage1(panel, dev, names)
+    bad = []
+    for r, nm in enumerate(names):
+        bad += compare(gv[r], gs[r], ov[r], os_[r], nm, atol=0.0, rtol=0.0)
+    assert not bad, "\n".join(bad)
+
+
+def test_doc_pdf_shared_values_recount(dev):
+    """Day 0: 3,000 identical stocks, so every level key and every query value is shared
+    by all of them (n_eq >= 3,000 per value): the packed u32 counters' n_eq field
+    overflows, the slice detects it (fields no longer sum to its weight) and recounts as
+    two halves with u64 counters; day 1 is ordinary (packed path)."""
+    import mff_oracle as O
+    from mff import synth
+    panel = synth.make_panel(3000, 2, config=16)
+    for k in ("open", "high", "low", "close", "volume", "present"):
+        panel[k][0] = panel[k][0][0:1]
+    names = ["doc_pdf60", "doc_pdf70", "doc_pdf80", "doc_pdf90", "doc_pdf95"]
     ov, os_ = O.oracle_stage1(panel, names)
     gv, gs, _ = _run_stage1(panel, dev, names)
     bad = []
