@@ -309,6 +309,19 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
     const int step = (int)blockDim.x * UNR;
     const int steps = sl.steps;
     const bool shallow = steps <= 6;
+    // software-pipelined: the next UNR entries are loaded before this UNR's searches
+    uint64_t nkey[UNR];
+    uint32_t nw[UNR];
+    auto fetch = [&](int i0) {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int i = i0 + u * (int)blockDim.x;
+        const bool v = i < n;
+        nkey[u] = v ? K[i] : 0ull;
+        nw[u] = v ? (uint32_t)Wt[i] : 0u;
+      }
+    };
+    fetch((int)threadIdx.x);
     for (int i0 = (int)threadIdx.x; i0 < n; i0 += step) {
       uint64_t key[UNR];
       uint32_t w[UNR];
@@ -316,11 +329,10 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
       bool in[UNR];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const int i = i0 + u * (int)blockDim.x;
-        const bool v = i < n;
-        key[u] = v ? K[i] : 0ull;
-        w[u] = v ? (uint32_t)Wt[i] : 0u;
+        key[u] = nkey[u];
+        w[u] = nw[u];
       }
+      fetch(i0 + step);
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const bool bl = key[u] <= sl.L0;  // (padding entries have weight 0)
