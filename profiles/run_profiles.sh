@@ -27,5 +27,6 @@ for pmc in "FETCH_SIZE" "WRITE_SIZE" \
   timeout -s KILL 240 rocprofv3 --pmc $pmc --kernel-include-regex "k_stage1|k_pdf" -d "$OUT/pmc_$name" -o pmc \
     --output-format csv -- python3 "${BENCH[@]}" --steps 1 --warmup 0 > "$OUT/pmc_$name.log" 2>&1
 done
+python3 "$R/profiles/pass_span.py" "$OUT/trace" "$OUT/pass_spans.csv" > "$OUT/pass_spans.log" 2>&1 || true
 find "$OUT" -name "*kernel_trace.csv" -delete
 echo "profiles done: $OUT"
