@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "mff_fmath.h"
 #include "mff_wave.h"
 
 namespace mff {
@@ -24,10 +25,13 @@ __device__ __forceinline__ bool std1_raw(const RawMom& m, bool exact0, double& o
   out = sqrt(v);
   return true;
 }
-// central m2, m3, m4 (biased); exact zeros when s1..s4 are all zero
+// central m2, m3, m4 (biased); exact zeros when s1..s4 are all zero.  The sums are shifted
+// by a member, so m2 = a2 - mu^2 cancels at most a factor ~2n (the set's variance is at
+// least range^2 / 2n, a2 at most range^2): its sign is decided, whatever the rounding of
+// the four quotients, which are therefore products with one reciprocal of n.
 __device__ __forceinline__ void central(const RawMom& m, double& m2, double& m3, double& m4) {
-  const double n = (double)m.n;
-  const double mu = m.s1 / n, a2 = m.s2 / n, a3 = m.s3 / n, a4 = m.s4 / n;
+  const double inv = 1.0 / (double)m.n;
+  const double mu = m.s1 * inv, a2 = m.s2 * inv, a3 = m.s3 * inv, a4 = m.s4 * inv;
   m2 = a2 - mu * mu;
   m3 = a3 - 3.0 * mu * a2 + 2.0 * mu * mu * mu;
   m4 = a4 - 4.0 * mu * a3 + 6.0 * mu * mu * a2 - 3.0 * mu * mu * mu * mu;
@@ -40,16 +44,25 @@ __device__ __forceinline__ void skew_kurt(const RawMom& m, double& sk, double& k
     sk = ku = qnan();
     return;
   }
-  sk = (m.n == 2) ? 0.0 : m3 / (m2 * sqrt(m2));
-  ku = m4 / (m2 * m2) - 3.0;
+  // m2 > 0 here: m3 / m2^1.5 and m4 / m2^2 from one reciprocal and one rsqrt (mff_fmath.h:
+  // tolerance-only statistics, a few ulp)
+  double sq, rsq;
+  fsqrt2(m2, sq, rsq);
+  const double r2 = frcp(m2);
+  sk = (m.n == 2) ? 0.0 : m3 * r2 * rsq;
+  ku = m4 * r2 * r2 - 3.0;
 }
 // S3 Pearson from shifted sums over n pairs (shift = a member pair)
 __device__ __forceinline__ double pearson_raw(int n, double sx, double sy, double sxx, double syy, double sxy) {
   if (n < 2) return qnan();
-  const double dn = (double)n;
-  const double vx = sxx - sx * sx / dn, vy = syy - sy * sy / dn;
-  if (!(vx != 0.0) || !(vy != 0.0)) return (__builtin_isnan(vx) || __builtin_isnan(vy)) ? qnan() : qnan();
-  return (sxy - sx * sy / dn) / sqrt(vx * vy);
+  // shifted by a member pair: the variances' signs are decided (as in central), so the
+  // quotients by n are products with one reciprocal and the root a refined rsqrt
+  const double inv = 1.0 / (double)n;
+  const double vx = sxx - sx * (sx * inv), vy = syy - sy * (sy * inv);
+  if (!(vx != 0.0) || !(vy != 0.0)) return qnan();
+  double sq, rsq;
+  fsqrt2(vx * vy, sq, rsq);
+  return (sxy - sx * (sy * inv)) * rsq;
 }
 
 }  // namespace mff
