@@ -63,9 +63,6 @@ constexpr uint32_t kSerAB = kSerA | kSerB;  // one pass over open, close, volume
 #ifndef MFF_PAIR_AB
 #define MFF_PAIR_AB 1
 #endif
-#ifndef MFF_FUSE_AB
-#define MFF_FUSE_AB 0
-#endif
 #ifndef MFF_SERA_FAST
 #define MFF_SERA_FAST 1
 #endif
@@ -771,13 +768,6 @@ int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D
   if (MFF_PAIR_AB && (a.fam & kSerAB) == kSerAB) {  // sets A and B in one wave-pair launch
     hipLaunchKernelGGL(k_stage1s_pair, dim3((unsigned)(((long long)S * D + 63) / 64)), dim3(128), 0, st,
                        patched(kSerAB));
-    if ((a.fam & kSerH) == kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, true>), grid, blk, 0, st, patched(kSerH));
-    else if (a.fam & kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, false>), grid, blk, 0, st, patched(kSerH));
-    MFF_LAUNCH_CHECK();
-    return 0;
-  }
-  if (MFF_FUSE_AB && (a.fam & kSerAB) == kSerAB) {
-    hipLaunchKernelGGL((k_stage1s<kSerAB, true>), grid, blk, 0, st, patched(kSerAB));
     if ((a.fam & kSerH) == kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, true>), grid, blk, 0, st, patched(kSerH));
     else if (a.fam & kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, false>), grid, blk, 0, st, patched(kSerH));
     MFF_LAUNCH_CHECK();
