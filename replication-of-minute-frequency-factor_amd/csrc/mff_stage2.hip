@@ -6,12 +6,14 @@
 // skipped, not counted; a window holding a null has < N samples -> null.
 //
 // Layout: lane = stock, loop over days reading val[row][d][s..] (coalesced across the
-// lanes).  Two kernels:
-//  * k_stage2_reg<N> (N in {1, 2, 3, 5, 10, 20, 60}): the last N present values in VGPRs,
-//    each window recomputed from scratch by two passes (x0-shifted mean, squared
-//    deviations);
-//  * k_stage2_slide (any N >= 1): double-double sliding sums with exact constant-window
-//    detection and in-window null / NaN / inf counts.
+// lanes).  Kernels:
+//  * k_stage2_reg<N> (every N <= 64, a template instance each): the last N present values
+//    in VGPRs, each window recomputed from scratch in one pass over the values shifted by
+//    the oldest (window_stats);
+//  * k_stage2_slide (any N >= 1, used for N > 64): double-double sliding sums with exact
+//    constant-window detection and in-window null / NaN / inf counts;
+//  * k_stage2_ring (N <= 32, only with MFF_STAGE2_IMPL=ring: A/B and tests): the slide
+//    state with the window in an LDS ring.
 // Both give: NaN/inf affect only the windows holding them, and a constant window has std
 // exactly 0 (C6: z = 0/0 = NaN).
 #include <stdlib.h>
@@ -585,19 +587,20 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
   // MFF_STAGE2_IMPL=ring / slide: a sliding kernel for every N (A/B timing)
   const char* impl = getenv("MFF_STAGE2_IMPL");
   const bool force_slide = impl && (impl[0] == 's' || impl[0] == 'r');
-  switch (force_slide ? -1 : N) {  // the usual windows: register shift window; other N: sliding sums
-    MFF_S2_REG(1)
-    MFF_S2_REG(2)
-    MFF_S2_REG(3)
-    MFF_S2_REG(5)
-    MFF_S2_REG(10)
-    MFF_S2_REG(20)
-    MFF_S2_REG(60)
+#define MFF_S2_REG4(a) MFF_S2_REG(a) MFF_S2_REG(a + 1) MFF_S2_REG(a + 2) MFF_S2_REG(a + 3)
+#define MFF_S2_REG16(a) MFF_S2_REG4(a) MFF_S2_REG4(a + 4) MFF_S2_REG4(a + 8) MFF_S2_REG4(a + 12)
+  switch (force_slide ? -1 : N) {  // N <= 64: register shift window; longer windows: sliding sums
+    MFF_S2_REG16(1)
+    MFF_S2_REG16(17)
+    MFF_S2_REG16(33)
+    MFF_S2_REG16(49)
     default:
       break;
   }
+#undef MFF_S2_REG16
+#undef MFF_S2_REG4
 #undef MFF_S2_REG
-  if (N <= S2_RING_MAXN && !(impl && impl[1] == 'l')) {  // MFF_STAGE2_IMPL=slide: HBM re-read kernel
+  if (N <= S2_RING_MAXN && impl && impl[0] == 'r') {  // MFF_STAGE2_IMPL=ring: LDS-ring kernel
     const long long nr = (long long)rows * ((S + 63) / 64);
     hipLaunchKernelGGL(k_stage2_ring, dim3((unsigned)nr), dim3(64), (size_t)N * 64 * 8, as_stream(stream), val,
                        state, D, S, N, method, out_val, out_state);

@@ -214,10 +214,10 @@ def _random_long_panel(D, S, seed):
                                   (64, 150), (65, 150), (120, 300), (250, 400),
                                   (20, 1), (20, 3), (5, 4), (3, 8), (7, 8)])
 def test_stage2_live(dev, N, D):
-    """N in {1, 2, 3, 5, 10, 20, 60}: register shift window (k_stage2_reg); any other N
-    (7, 64, 65, 120, 250): the sliding double-double kernel (k_stage2_slide).  D covers
-    D < 4 (no whole register chunk), D % 4 == 0 (last chunk flushed after the loop) and
-    D < N; two factor rows exercise the per-row plane offsets."""
+    """N <= 64: register shift window (k_stage2_reg<N>); 65, 120, 250: the sliding
+    double-double kernel (k_stage2_slide).  D covers D < 4 (no whole register chunk),
+    D % 4 == 0 (last chunk flushed after the loop) and D < N; two factor rows exercise
+    the per-row plane offsets."""
     import mff_oracle as O
     from mff import engine
     val, state = _random_long_panel(D, 130, N)
@@ -235,6 +235,25 @@ def test_stage2_live(dev, N, D):
         for r in range(2):
             ov, os_ = O.oracle_stage2(v[r], st[r], N, meth)
             bad += compare(rv[r], rs[r], ov, os_, f"N{N}/D{D}/row{r}/{meth}", atol=1e-9)
+    assert not bad, "\n".join(bad[:20])
+
+
+@pytest.mark.parametrize("impl,N", [("ring", 7), ("ring", 20), ("slide", 7), ("slide", 20), ("slide", 64)])
+def test_stage2_sliding_kernels_forced(dev, impl, N, monkeypatch):
+    """The sliding kernels for windows the register kernel also covers (MFF_STAGE2_IMPL:
+    the LDS-ring form for N <= 32, the HBM re-read double-double form for any N)."""
+    import mff_oracle as O
+    from mff import engine
+    monkeypatch.setenv("MFF_STAGE2_IMPL", impl)
+    D = 150
+    val, state = _random_long_panel(D, 130, N + 7)
+    val[20, 6] = 1e15
+    bad = []
+    for meth in ("m", "z", "std"):
+        rv, rs = engine.rolling(torch.from_numpy(val[None]).to(dev), torch.from_numpy(state[None]).to(dev), N, meth)
+        torch.cuda.synchronize()
+        ov, os_ = O.oracle_stage2(val, state, N, meth)
+        bad += compare(rv[0].cpu().numpy(), rs[0].cpu().numpy(), ov, os_, f"{impl}/N{N}/{meth}", atol=1e-9)
     assert not bad, "\n".join(bad[:20])
 
 
