@@ -10,12 +10,15 @@ and its cross-rank exchange) over the whole panel, inputs already resident in HB
 The panel (S stocks x D days) is sharded by stock over the ranks: total work is fixed,
 so "scaling" is "strong".  value = S*D*K / max-over-ranks(wall time of the K steps).
 
-roofline: the stage-1 pass (one mff_stage1 call = four launches: k_stage1g for the sorted
-families, the k_stage1s_pair wave pair for the streaming families of open / close /
-volume, k_stage1s for OLS / MOMH, the small exact-list kernel; and the doc_pdf sort /
-count on the side stream, whose tail the window includes), algorithmic bytes per pass = 5,354 B/stock-day (4,832 B OHLCV+mask in, 58 x
-9 B out) x local stock-days, over the pass's average duration from HIP
-events on its launch stream; peak 8.0 TB/s (MI355X_MICROARCH.md).  bound stays "hbm":
+roofline: the stage-1 pass (engine.compute_factors: k_stage1s for OLS / MOMH on its own
+stream from the start; k_stage1g for the sorted families and the small exact-list kernel,
+then the k_stage1s_pair wave pair for the streaming families of open / close / volume on
+the launch stream; the doc_pdf sort / count on a side stream; the launch stream waits for
+both, so the window covers every launch), algorithmic bytes per pass = 5,354
+B/stock-day (4,832 B OHLCV+mask in, 58 x 9 B out) x local stock-days, over
+the pass's average duration from HIP events on its launch stream; peak 8.0 TB/s
+(MI355X_MICROARCH.md).  The launches overlap, so rocprof's per-kernel averages do not add
+up to the window; profiles/pass_span.py turns the kernel trace into per-pass spans.  bound stays "hbm":
 the north star prices the pass against HBM bandwidth.  traffic: HBM bytes per pass from
 the committed rocprofv3 PMC passes (profiles/pmc_stage1.json: FETCH_SIZE x 2 per the
 gfx950 correction + WRITE_SIZE, summed over the launches), or null; traffic_calibrated:
@@ -342,10 +345,11 @@ def main():
                 "traffic": traffic,
                 "traffic_calibrated": traffic_cal,
                 "valu": valu,
-                "kernel": "stage-1 pass: k_stage1g<ORD|ORDV|LVL|PDF> (sorted families), "
-                          "k_stage1s_pair (wave pair: <SEG|MOMR|TRD|ORD> + <MOMV|SUMV|SUMC|CORR>), "
-                          "k_stage1s<OLS|MOMH>, k_stage1 exact list, + doc_pdf k_pdf_sort / "
-                          "k_pdf_count on the side stream (inside the window)",
+                "kernel": "stage-1 pass over three streams: k_stage1s<OLS|MOMH> (own stream), "
+                          "k_stage1g<ORD|ORDV|LVL|PDF> + k_stage1 exact list, then k_stage1s_pair "
+                          "(wave pair: <SEG|MOMR|TRD|ORD> + <MOMV|SUMV|SUMC|CORR>) on the launch "
+                          "stream, doc_pdf k_pdf_sort / k_pdf_count (side stream); window = the "
+                          "whole pass",
                 "bytes_per_launch": bytes_launch,
                 "avg_kernel_ms": round(k_ms, 3),
             },
