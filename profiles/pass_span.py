@@ -55,6 +55,8 @@ def main():
                           for k in names])
     for i, p in enumerate(passes):
         print(f"pass {i}: span {(p['end'] - p['start']) / 1e6:.3f} ms, {len(p['kernels'])} launches")
+        for k, (st, en) in sorted(p["kernels"].items(), key=lambda kv: kv[1][0]):
+            print(f"    {k:32s} {(st - p['start']) / 1e6:8.3f} -> {(en - p['start']) / 1e6:8.3f} ms")
 
 
 if __name__ == "__main__":
