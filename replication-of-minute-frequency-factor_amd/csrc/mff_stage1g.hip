@@ -177,7 +177,9 @@ constexpr uint32_t G_OL = G_ORD | G_LVL;
 template <uint32_t SET>
 // (256, 4): at most 128 VGPRs, four waves per SIMD (the LVL set would take 139 and three)
 __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
-  __shared__ __attribute__((aligned(16))) uint64_t scratch[16][NB];  // 2 KB per group
+  // 2 KB per group plus 64 B of padding: the four groups of a wave start 16 banks apart,
+  // so a store of 16 consecutive words per group covers the 64 banks once
+  __shared__ __attribute__((aligned(16))) uint64_t scratch[16][NB + 8];
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
   const int grp = lane >> 4;
@@ -781,13 +783,16 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
 #pragma unroll
           for (int k = 0; k < K; ++k) { cw[k] = 0u; vv[k] = 0u; }
         } else {
-          uint32_t* sv = reinterpret_cast<uint32_t*>(scr);  // 256 volumes of this group
+          // 256 volumes of this group, bar 16g + k at slot 16k + g (the key's low byte):
+          // each store instruction writes 16 consecutive words per group (conflict free)
+          uint32_t* sv = reinterpret_cast<uint32_t*>(scr);
           uint32_t key[K];
 #pragma unroll
           for (int k = 0; k < K; ++k) {
             const bool pk = (pb >> k) & 1u;
-            sv[e0 + k] = ((pb & vokm) >> k) & 1u ? (uint32_t)v[k] : 0u;
-            key[k] = pk ? ((cmx - fbits(c[k])) << 8) | (uint32_t)(e0 + k) : 0xffffffffu;
+            const uint32_t slot = (uint32_t)(16 * k + g);
+            sv[slot] = ((pb & vokm) >> k) & 1u ? (uint32_t)v[k] : 0u;
+            key[k] = pk ? ((cmx - fbits(c[k])) << 8) | slot : 0xffffffffu;
           }
           gsort256u(key);
           lds_fence();
@@ -814,6 +819,12 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
         const uint32_t lastm = (n - 1 >= e0 && n - 1 < e0 + K) ? 1u << (n - 1 - e0) : 0u;
         const uint32_t endm = (diffm | lastm) & validm;
         const int L = gcount(endm);
+        uint64_t* kd = a.lvl_key ? a.lvl_key + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
+        uint8_t* wd = a.lvl_w ? a.lvl_w + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
+        // the list reservation is issued here and its value first used after the
+        // compaction, the moments and the doc_pdf thresholds (the atomic's round trip)
+        uint32_t base = 0u;
+        if (!wide && kd && g == 0) base = atomicAdd(a.lvl_count + d, (uint32_t)L);
         if (!wide) {
           // Compact the levels (run ends, descending close) into LDS by level index:
           //   lv[l] = cumulative volume through level l (exact u32: sum(v) <= 240 * 2^24),
@@ -835,8 +846,6 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
             }
           }
           lds_fence();
-          const int nj = (L + 15) >> 4;  // levels per lane (uniform inside the group)
-          const int l0 = nj * g;
           const uint32_t Sv = (uint32_t)sumv;
           const double inv = 1.0 / sumv;
           // level 0 (the highest close) is the member shift of the share moments
@@ -845,26 +854,14 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
           // 20*cum > k*Sv, i.e. cum > floor(k*Sv/20) (integers); an exact tie
           // 20*cum == k*Sv at a level (only when 20 | k*Sv) is left to the exact path.
           // floor(k*Sv/20) = k*(Sv/20) + (k*(Sv%20))/20 in u32.
-          // the lane's first level continues from the previous lane's last one
-          uint32_t pcum = 0u;  // cumulative volume before level l0
-          if (l0 > 0 && l0 <= L) pcum = lv[l0 - 1];
           double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
-          uint64_t* kd = a.lvl_key ? a.lvl_key + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
-          uint8_t* wd = a.lvl_w ? a.lvl_w + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
-          // the list reservation is issued here and its value first used after the
-          // moments and the doc_pdf thresholds, which hide the atomic's round trip
-          uint32_t base = 0u;
-          if (kd && g == 0) base = atomicAdd(a.lvl_count + d, (uint32_t)L);
           if (fam & F_LVL) {
-            for (int j = 0; j < nj; ++j) {
-              const int l = l0 + j;
-              if (l < L) {
-                const uint32_t c2 = lv[l];
-                const uint32_t V = c2 - pcum;
-                pcum = c2;
-                const double dd = (double)V * inv - x0, d2 = dd * dd;
-                s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
-              }
+            // levels interleaved over the lanes (level l from lane l % 16): each read
+            // instruction touches 16 consecutive words per group
+            for (int l = g; l < L; l += 16) {
+              const uint32_t V = lv[l] - (l > 0 ? lv[l - 1] : 0u);
+              const double dd = (double)V * inv - x0, d2 = dd * dd;
+              s1 += dd; s2 += d2; s3 += d2 * dd; s4 += d2 * d2;
             }
           }
           if (fast && (fam & F_LVL)) {

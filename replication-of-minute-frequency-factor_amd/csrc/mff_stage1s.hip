@@ -66,6 +66,9 @@ constexpr uint32_t kSerAB = kSerA | kSerB;  // one pass over open, close, volume
 #ifndef MFF_SERA_FAST
 #define MFF_SERA_FAST 1
 #endif
+#ifndef MFF_PAIR_QREAD
+#define MFF_PAIR_QREAD 0
+#endif
 
 // ---- presence bits of one stock-day: 8 words, bit m%32 of word m/32 (compile-time
 // word indices only, so the array stays in registers)
@@ -515,7 +518,31 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     uint32_t pw1 = 0u, pw2 = 0u;  // mask words w-1, w-2
     auto step = [&](float4(*sb)[64 * CQ], int c, int h, uint32_t bits, uint32_t lbits) {
       float4 X[NB][CQ];
-      if constexpr (PAIR) {
+      if constexpr (PAIR && MFF_PAIR_QREAD) {
+        // as below, but the DMA of chunk c+1 goes out first and the chunk is read one quad
+        // ahead of its use (two quads of registers staged instead of four)
+        sb = (c & 1) ? pb1 : pb0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (c + 1 < NBAR / BC) dma((c & 1) ? pb0 : pb1, c + 1, 0);
+        float4 Y[2][NB];
+#pragma unroll
+        for (int ii = 0; ii < NB; ++ii) Y[0][ii] = sb[ii][CQ * lane + (0 ^ sw)];
+#pragma unroll
+        for (int k = 0; k < CQ; ++k) {
+          if (k + 1 < CQ) {
+#pragma unroll
+            for (int ii = 0; ii < NB; ++ii) Y[(k + 1) & 1][ii] = sb[ii][CQ * lane + ((k + 1) ^ sw)];
+          }
+          float4 Z[NB][CQ];
+#pragma unroll
+          for (int ii = 0; ii < NB; ++ii) Z[ii][0] = Y[k & 1][ii];
+          __builtin_amdgcn_sched_barrier(0);
+          quad(BC * c + 4 * k, bits >> (BC * h + 4 * k), 0u, toq(Z, 0, 0), one4, one4, one4, one4);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+      } else if constexpr (PAIR) {
         // chunk c is in buffer c & 1: this wave's half has landed (vmcnt 0), the
         // partner's half after the barrier; read it, then fetch chunk c+1 into the other
         // buffer (both waves finished reading it at chunk c-1, before this barrier)

@@ -146,13 +146,18 @@ PDF_OVERLAP = os.environ.get("MFF_PDF_OVERLAP", "1") != "0"
 # MFF_HL_STREAM=0: launch order of round 1 (A/B timing).
 HL_STREAM = os.environ.get("MFF_HL_STREAM", "1") != "0"
 
+# Stream priorities of the side streams (torch / HIP: lower = higher priority; 0 is the
+# default): MFF_PDF_PRIO for the doc_pdf rank phases, MFF_HL_PRIO for the high / low kernel.
+PDF_PRIO = int(os.environ.get("MFF_PDF_PRIO", "0"))
+HL_PRIO = int(os.environ.get("MFF_HL_PRIO", "0"))
+
 _SIDE = {}
 
 
 def _side_stream(dev, which: int = 0) -> torch.cuda.Stream:
     key = (dev.index, threading.get_ident(), which)
     if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(dev)
+        _SIDE[key] = torch.cuda.Stream(dev, priority=HL_PRIO if which == 1 else PDF_PRIO)
     return _SIDE[key]
 
 
