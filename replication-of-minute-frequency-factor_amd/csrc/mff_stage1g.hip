@@ -409,7 +409,9 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
       }
       if (fam & needC) {
         load(3, c, 1.0f);
-        sanitize(c, 1.0f);
+        // LVL / PDF read closes of present bars only (masked keys, the last present
+        // close), so their absent slots need no canonical value
+        if (fam & needC & ~(F_LVL | F_PDF)) sanitize(c, 1.0f);
       }
       if (fam & needO) {
         load(0, o, 1.0f);
@@ -759,7 +761,9 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           const bool pk = (pb >> k) & 1u;
-          const bool vok = (v[k] == rintf(v[k])) & (v[k] >= 0.0f) & (v[k] <= 16777216.0f);
+          // integral and in [+0, 2^24] (v is sanitized: no -0; NaN / inf / negatives
+          // have bit patterns above the one of 2^24)
+          const bool vok = (v[k] == rintf(v[k])) & (fbits(v[k]) <= 0x4b800000u);
           vokm |= (vok ? 1u : 0u) << k;
           cmx = max(cmx, pk ? fbits(c[k]) : 0u);
           cmn = min(cmn, pk ? fbits(c[k]) : 0xffffffffu);
@@ -791,7 +795,9 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
           for (int k = 0; k < K; ++k) {
             const bool pk = (pb >> k) & 1u;
             const uint32_t slot = (uint32_t)(16 * k + g);
-            sv[slot] = ((pb & vokm) >> k) & 1u ? (uint32_t)v[k] : 0u;
+            // absent bars hold 0 (sanitized); a non-integral volume's truncation only
+            // reaches stock-days the exact kernel finishes (the list keys use closes)
+            sv[slot] = (uint32_t)v[k];
             key[k] = pk ? ((cmx - fbits(c[k])) << 8) | slot : 0xffffffffu;
           }
           gsort256u(key);
@@ -799,7 +805,7 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
 #pragma unroll
           for (int k = 0; k < K; ++k) {
             cw[k] = key[k] >> 8;
-            vv[k] = (e0 + k < n) ? sv[key[k] & 0xffu] : 0u;
+            vv[k] = sv[key[k] & 0xffu];  // elements past n: key ~0 -> slot 255 (bar 255: none, 0)
           }
           lds_fence();
         }
