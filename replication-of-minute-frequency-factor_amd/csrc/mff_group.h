@@ -203,6 +203,11 @@ __device__ __forceinline__ bool gpres(uint32_t pb, int m) {
   return (bpermu(gbase() + (m >> 4), pb) >> (m & 15)) & 1u;
 }
 
+// all-ones when bar k of the lane is present / absent (one v_bfe_i32: a mask for
+// v_and / v_or instead of a compare and a select)
+__device__ __forceinline__ uint32_t present_bits(uint32_t pb, int k) { return (uint32_t)((int32_t)(pb << (31 - k)) >> 31); }
+__device__ __forceinline__ uint32_t absent_bits(uint32_t pb, int k) { return ~present_bits(pb, k); }
+
 // ---- bar-range masks of this lane (16-bit, bit k = bar 16*gi+k in [lo, hi])
 __device__ __forceinline__ uint32_t rmask(int lo, int hi) {
   const int b0 = 16 * gi();

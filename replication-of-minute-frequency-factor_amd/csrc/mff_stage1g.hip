@@ -232,7 +232,12 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
       const uint32_t needV = F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD;
       auto sanitize = [&](float (&x)[K], float dflt) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) x[k] = ((pb >> k) & 1u) ? x[k] + 0.0f : dflt;
+        for (int k = 0; k < K; ++k) {
+          if (dflt == 0.0f)  // x + 0 (no -0) where present, the bits of +0 elsewhere
+            x[k] = bitsf(fbits(x[k] + 0.0f) & present_bits(pb, k));
+          else
+            x[k] = ((pb >> k) & 1u) ? x[k] + 0.0f : dflt;
+        }
       };
       // phase A planes: high, low (OLS, MOMH); later phases load the others
       if (fam & needHL) {
@@ -425,27 +430,32 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
 
         uint32_t key[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) key[k] = ((pb >> k) & 1u) ? fbits(v[k]) : 0xffffffffu;
+        for (int k = 0; k < K; ++k) key[k] = fbits(v[k]) | absent_bits(pb, k);  // v sanitized
         gsort256u(key);
-        auto kth = [&](int e) { return bitsf(bpermu(gb + (e >> 4), pick(key, e & 15))); };
-        th50 = kth(n >= 50 ? n - 50 : 0);  // top_k(50).min()   CM:391-396
-        th20 = kth(n >= 20 ? n - 20 : 0);  // top_k(20).min()
-        tb50 = kth(n >= 50 ? 49 : n - 1);  // bottom_k(50).max() CM:417-422
-        if ((fam & F_ORD) && a.ord_th && g < 3 && act) {
+        // the sorted keys go through the group's LDS scratch (element e = 16 g + k at slot
+        // 16 k + g: conflict-free stores), and each lane reads the one element it needs:
+        // lanes 0..9 the top ten (n-1-g), lanes 10..12 the three order statistics
+        uint32_t* so = reinterpret_cast<uint32_t*>(scr);
+#pragma unroll
+        for (int k = 0; k < K; ++k) so[16 * k + g] = key[k];
+        lds_fence();
+        const int e = g < 10 ? n - 1 - g
+                    : g == 10 ? (n >= 50 ? n - 50 : 0)    // top_k(50).min()   CM:391-396
+                    : g == 11 ? (n >= 20 ? n - 20 : 0)    // top_k(20).min()
+                    : (n >= 50 ? 49 : n - 1);             // bottom_k(50).max() CM:417-422
+        const float xe = (e >= 0 && g < 13) ? bitsf(so[((e & 15) << 4) | (e >> 4)]) : 0.0f;
+        lds_fence();  // the LVL section reuses the scratch
+        th50 = bpermf(gb + 10, xe);
+        th20 = bpermf(gb + 11, xe);
+        tb50 = bpermf(gb + 12, xe);
+        if ((fam & F_ORD) && a.ord_th && g >= 10 && g < 13 && act) {
           const size_t pl = (size_t)a.D * a.S;
-          a.ord_th[(size_t)g * pl + sd] = g == 0 ? th50 : g == 1 ? th20 : tb50;
+          a.ord_th[(size_t)(g - 10) * pl + sd] = xe;
         }
         if (fam & F_ORDV) {
-          double t10 = 0.0, t5 = 0.0;
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            const int e = 16 * g + k;
-            const double x = (double)bitsf(key[k]);
-            if (e < n && e >= n - 10) t10 += x;
-            if (e < n && e >= n - 5) t5 += x;
-          }
-          t10 = gsum(t10);
-          t5 = gsum(t5);
+          // the top ten / five elements (fewer when n < 10: e < 0 reads nothing)
+          const double t10 = gsum(g < 10 ? (double)xe : 0.0);
+          const double t5 = gsum(g < 5 ? (double)xe : 0.0);
           R.val(47, t10 / sumv);  // doc_vol10_ratio
           R.val(48, t5 / sumv);   // doc_vol5_ratio
           R.val(49, t5 / sumv);   // doc_vol50_ratio: top_k(5) [sic CM:1196]
@@ -760,13 +770,12 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
         uint32_t cmx = 0u, cmn = 0xffffffffu;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          const bool pk = (pb >> k) & 1u;
           // integral and in [+0, 2^24] (v is sanitized: no -0; NaN / inf / negatives
           // have bit patterns above the one of 2^24)
           const bool vok = (v[k] == rintf(v[k])) & (fbits(v[k]) <= 0x4b800000u);
           vokm |= (vok ? 1u : 0u) << k;
-          cmx = max(cmx, pk ? fbits(c[k]) : 0u);
-          cmn = min(cmn, pk ? fbits(c[k]) : 0xffffffffu);
+          cmx = max(cmx, fbits(c[k]) & present_bits(pb, k));
+          cmn = min(cmn, fbits(c[k]) | absent_bits(pb, k));
         }
         const bool ok = (pb & ~vokm) == 0u;
         cmx = gmax_u(cmx);
@@ -793,12 +802,11 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
           uint32_t key[K];
 #pragma unroll
           for (int k = 0; k < K; ++k) {
-            const bool pk = (pb >> k) & 1u;
             const uint32_t slot = (uint32_t)(16 * k + g);
             // absent bars hold 0 (sanitized); a non-integral volume's truncation only
             // reaches stock-days the exact kernel finishes (the list keys use closes)
             sv[slot] = (uint32_t)v[k];
-            key[k] = pk ? ((cmx - fbits(c[k])) << 8) | slot : 0xffffffffu;
+            key[k] = ((cmx - fbits(c[k])) << 8) | slot | absent_bits(pb, k);
           }
           gsort256u(key);
           lds_fence();

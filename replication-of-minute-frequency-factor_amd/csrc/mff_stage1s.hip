@@ -66,6 +66,10 @@ constexpr uint32_t kSerAB = kSerA | kSerB;  // one pass over open, close, volume
 #ifndef MFF_SERA_FAST
 #define MFF_SERA_FAST 1
 #endif
+// set B's all-present quad path: in the pair form set B shares set A's register budget
+#ifndef MFF_SERB_FAST
+#define MFF_SERB_FAST 1
+#endif
 #ifndef MFF_PAIR_QREAD
 #define MFF_PAIR_QREAD 0
 #endif
@@ -424,8 +428,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     }
     if (fam & (kSerA | kSerB)) {
       // every lane has all four bars (the usual case): the presence selects fold away
-      // (set A only: set B's register budget has no room for the second copy)
-      if (SET == kSerA && MFF_SERA_FAST && __builtin_amdgcn_ballot_w64((pm & 0xFu) != 0xFu) == 0ull) {
+      // (set A, and set B in the pair form, where it has set A's register budget; set B's
+      // own kernel has no room for the second copy)
+      if (((SET == kSerA && MFF_SERA_FAST) || (SET == kSerB && PAIR && MFF_SERB_FAST)) &&
+          __builtin_amdgcn_ballot_w64((pm & 0xFu) != 0xFu) == 0ull) {
         const std::true_type all;
         bar(m0 + 0, true, x.o.x, x.c.x, x.v.x, all);
         bar(m0 + 1, true, x.o.y, x.c.y, x.v.y, all);

@@ -111,19 +111,33 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
     if need_pdf and PDF_OVERLAP:
         # part 1 (sorted families: doc_pdf levels + queries), then the doc_pdf rank on a
         # side stream while part 2 (the serial families) runs on the launch stream
-        hl = None
-        if HL_STREAM:  # the high / low serial kernel from the start, on its own stream
-            hl = _side_stream(dev, 1)
+        hl = _side_stream(dev, 1) if HL_STREAM else None
+
+        def launch_hl():  # the high / low serial kernel on its own stream
             hl.wait_stream(main)
-            args_hl = args[:-1] + [hl.cuda_stream]
-            _lib.check(lib.mff_stage1_part(*args_hl, 4), "mff_stage1_part(4)")
+            _lib.check(lib.mff_stage1_part(*(args[:-1] + [hl.cuda_stream]), 4), "mff_stage1_part(4)")
+
+        if hl is not None and HL_AT == "start":
+            launch_hl()
         _lib.check(lib.mff_stage1_part(*args, 1), "mff_stage1_part(1)")
-        side = _side_stream(dev)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
+        if hl is not None and HL_AT == "part1":
+            launch_hl()
+        if PDF_FIRST:
+            # the doc_pdf phases (whole-CU workgroups) on the launch stream before part 2:
+            # behind the wave-pair kernel they only get CUs its blocks have drained
             pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
-        _lib.check(lib.mff_stage1_part(*args, 10 if hl is not None else 2), "mff_stage1_part(2)")
-        main.wait_stream(side)
+            if hl is not None and HL_AT == "pdf":
+                launch_hl()
+            _lib.check(lib.mff_stage1_part(*args, 10 if hl is not None else 2), "mff_stage1_part(2)")
+        else:
+            side = _side_stream(dev)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
+            _lib.check(lib.mff_stage1_part(*args, 10 if hl is not None else 2), "mff_stage1_part(2)")
+            main.wait_stream(side)
+        if hl is not None and HL_AT == "pdf" and not PDF_FIRST:
+            launch_hl()
         if hl is not None:
             main.wait_stream(hl)
         if events is not None:  # after the doc_pdf tail on the side stream
@@ -139,12 +153,17 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
 
 # MFF_PDF_OVERLAP=0: doc_pdf after the whole stage-1 pass on one stream (A/B timing)
 PDF_OVERLAP = os.environ.get("MFF_PDF_OVERLAP", "1") != "0"
+# MFF_PDF_FIRST=1: the doc_pdf phases on the launch stream between part 1 and part 2
+PDF_FIRST = os.environ.get("MFF_PDF_FIRST", "0") != "0"
 # The high / low serial kernel (OLS, MOMH) reads only the high / low planes and writes
 # only its own rows, so it runs on a third stream from the start of the pass: its blocks
 # (180 VGPRs, 2 waves per SIMD) fill the VGPRs the sorted-group kernel (128, 4 waves)
 # leaves and the gaps of the doc_pdf phases (+2 % pass throughput, profiles/r02/).
 # MFF_HL_STREAM=0: launch order of round 1 (A/B timing).
 HL_STREAM = os.environ.get("MFF_HL_STREAM", "1") != "0"
+# MFF_HL_AT: when that stream's launch is issued: "start" (default), "part1" (after the
+# sorted-group launch), "pdf" (after the doc_pdf phases)
+HL_AT = os.environ.get("MFF_HL_AT", "start")
 
 # Stream priorities of the side streams (torch / HIP: lower = higher priority; 0 is the
 # default): MFF_PDF_PRIO for the doc_pdf rank phases, MFF_HL_PRIO for the high / low kernel.
