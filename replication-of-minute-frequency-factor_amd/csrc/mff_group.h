@@ -205,6 +205,8 @@ __device__ __forceinline__ bool gpres(uint32_t pb, int m) {
 
 // all-ones when bar k of the lane is present / absent (one v_bfe_i32: a mask for
 // v_and / v_or instead of a compare and a select)
+// (the shift form compiles to and + cmp + cndmask; __builtin_amdgcn_sbfe gives the bfe but
+// the longer live ranges spilled the group kernel: measured slower)
 __device__ __forceinline__ uint32_t present_bits(uint32_t pb, int k) { return (uint32_t)((int32_t)(pb << (31 - k)) >> 31); }
 __device__ __forceinline__ uint32_t absent_bits(uint32_t pb, int k) { return ~present_bits(pb, k); }
 

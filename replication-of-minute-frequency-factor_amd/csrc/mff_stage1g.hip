@@ -42,6 +42,14 @@ int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, c
 int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
                   uint32_t fam, double* val, uint8_t* state, const float* ord_th, hipStream_t st);
 
+// 16 stock-days of one day per block iteration; MFF_GITER iterations per block
+#ifndef MFF_GITER
+#define MFF_GITER 4
+#endif
+// waves per SIMD the group kernel is built for (its LDS allows 5 at 31.7 KB per block)
+#ifndef MFF_GWAVES
+#define MFF_GWAVES 4
+#endif
 #ifndef MFF_MERGE_OL
 #define MFF_MERGE_OL 1
 #endif
@@ -176,10 +184,13 @@ constexpr uint32_t G_OL = G_ORD | G_LVL;
 
 template <uint32_t SET>
 // (256, 4): at most 128 VGPRs, four waves per SIMD (the LVL set would take 139 and three)
-__global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
+__global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
   // 2 KB per group plus 64 B of padding: the four groups of a wave start 16 banks apart,
   // so a store of 16 consecutive words per group covers the 64 banks once
-  __shared__ __attribute__((aligned(16))) uint64_t scratch[16][NB + 8];
+  // per group: the sorted families need 2 x 240 words (level cumulative volumes and
+  // close words; the 256-word key / volume images fit inside), the OLS betas 256 doubles
+  constexpr int SW = (SET & F_OLS) ? 2 * NB : 2 * NBAR;  // words
+  __shared__ __attribute__((aligned(16))) uint64_t scratch[16][SW / 2 + 8];
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
   const int grp = lane >> 4;
@@ -188,12 +199,12 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
   uint64_t* scr = scratch[wave * 4 + grp];
   double* scr_d = reinterpret_cast<double*>(scr);
   const uint32_t fam = a.fam & SET;
-  const int ntile = (a.S + 63) / 64;
+  const int ntile = (a.S + 16 * MFF_GITER - 1) / (16 * MFF_GITER);
   const int d = blockIdx.x / ntile;
-  const int s0 = (blockIdx.x % ntile) * 64;
+  const int s0 = (blockIdx.x % ntile) * (16 * MFF_GITER);
   const size_t plane = (size_t)a.D * a.S;
 
-  for (int it = 0; it < 4; ++it) {
+  for (int it = 0; it < MFF_GITER; ++it) {
     const int s = s0 + it * 16 + wave * 4 + grp;
     const bool act = s < a.S;
     const size_t sd = (size_t)d * a.S + (act ? s : 0);
@@ -847,7 +858,7 @@ __global__ __launch_bounds__(256, 4) void k_stage1g(GArgs a) {
           // per level below runs over ceil(L/16) slots per lane (a lane's levels
           // contiguous) instead of the 16 sorted bars.
           uint32_t* lv = reinterpret_cast<uint32_t*>(scr);
-          uint32_t* lc = lv + 256;
+          uint32_t* lc = lv + NBAR;  // L <= 240 levels
           uint32_t cum = gscan_excl_u(tv);
           int li = (int)gscan_excl_u((uint32_t)__builtin_popcount(endm));
 #pragma unroll
@@ -1030,7 +1041,7 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
   a.ord_th = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256 + (size_t)S * D * sizeof(int));
   const char* impl = getenv("MFF_STAGE1_IMPL");
   const bool w64 = impl && strcmp(impl, "w64") == 0;
-  const long long nblk = (long long)((S + 63) / 64) * D;
+  const long long nblk = (long long)((S + 16 * MFF_GITER - 1) / (16 * MFF_GITER)) * D;
   // one 16-lane group launch; it stores its own group's rows (and the queries) only
   auto group_launch = [&](int gi) -> int {
     const uint32_t set = gi < 2 ? g16::kGroups[gi] : g16::G_OL;

@@ -427,11 +427,13 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       olsbar(m0 + 3, (pm >> 3) & 1u, x.h.w, x.l.w, (lm >> 3) & 1u, lh1.y, ll1.y);
     }
     if (fam & (kSerA | kSerB)) {
-      // every lane has all four bars (the usual case): the presence selects fold away
+      // every lane has all four bars (the usual case): the presence selects fold away.
+      // Suspended lanes (n == 0) do not veto it: they walk don't-care values and store
+      // ABSENT whatever they accumulated
       // (set A, and set B in the pair form, where it has set A's register budget; set B's
       // own kernel has no room for the second copy)
       if (((SET == kSerA && MFF_SERA_FAST) || (SET == kSerB && PAIR && MFF_SERB_FAST)) &&
-          __builtin_amdgcn_ballot_w64((pm & 0xFu) != 0xFu) == 0ull) {
+          __builtin_amdgcn_ballot_w64((pm & 0xFu) != 0xFu && n > 0) == 0ull) {
         const std::true_type all;
         bar(m0 + 0, true, x.o.x, x.c.x, x.v.x, all);
         bar(m0 + 1, true, x.o.y, x.c.y, x.v.y, all);
