@@ -136,6 +136,8 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 // open / close / volume chunks (each wave fetches half of the rows), so those planes are
 // read from HBM once for both sets.  pbuf: that image, [2 buffers][3 planes][64 * 4].
 constexpr uint32_t kPairPlanes = 1u | 8u | 16u;  // open, close, volume
+// sqrt(cov) / (vx vy) from the x50 sums: x 50^1.5
+constexpr double kOlsSq = 353.55339059327376220;
 template <uint32_t SET, bool FULL, int PAIR>
 __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   const uint32_t fam = FULL ? SET : (a.fam & SET);
@@ -283,21 +285,23 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     if (m >= 49 && cR - cQ == 50) {  // window m-49..m, all 50 bars present (CM:129)
       const double Sx = Rx - Qx, Sy = Ry - Qy, Sxx = Rxx - Qxx, Syy = Ryy - Qyy, Sxy = Rxy - Qxy;
       const bool cx = lcx <= m - 49, cy = lcy <= m - 49;  // constant low / high
-      const double vx = cx ? 0.0 : (Sxx - Sx * Sx * 0.02) * 0.02;
-      const double vy = cy ? 0.0 : (Syy - Sy * Sy * 0.02) * 0.02;
-      const double cv = (cx || cy) ? 0.0 : (Sxy - Sx * Sy * 0.02) * 0.02;
+      // 50 x the population (co)variances: the factor 1/50 cancels in beta, cov^2/(vx vy)
+      // and cov/sqrt(vx vy), and is applied once at the end to sum sqrt(cov)/(vx vy);
+      // a constant side has exactly zero variance (C3): its flag, not the value, decides
+      const double Vx = fma(-Sx * 0.02, Sx, Sxx), Vy = fma(-Sy * 0.02, Sy, Syy);
+      const double Cv = fma(-Sx * 0.02, Sy, Sxy);
       // beta = cov / var_x, or mean_y / mean_x when var_x == 0 (CM:131-134)
-      const bool vz = vx != 0.0;
-      const double beta = fdiv(vz ? cv : y0 + Sy * 0.02, vz ? vx : x0 + Sx * 0.02);
-      const double prod = vx * vy;
-      if (prod != 0.0) {
+      const bool vz = !cx && Vx != 0.0;
+      const double beta = fdiv(vz ? (cy ? 0.0 : Cv) : y0 + Sy * 0.02, vz ? Vx : x0 + Sx * 0.02);
+      const double prod = Vx * Vy;
+      if (!cx && !cy && prod != 0.0) {
         const double ip = frcp(prod);
         double sp, rp, sc, rc;
         fsqrt2(prod, sp, rp);  // prod < 0: NaN, as sqrt(prod)
-        fsqrt2(cv, sc, rc);    // cv < 0: NaN, as cov**0.5
-        sq += (cv == 0.0 ? 0.0 : sc) * ip;  // cov**0.5 / (vx*vy)   CM:137
-        scs += cv * cv * ip;                // cov**2 / (vx*vy)     CM:212
-        scr += cv * rp;                     // cov / (vx*vy)**0.5   CM:261
+        fsqrt2(Cv, sc, rc);    // cov < 0: NaN, as cov**0.5
+        sq += (Cv == 0.0 ? 0.0 : sc) * ip;  // cov**0.5 / (vx*vy) / (50^1.5)   CM:137
+        scs += Cv * Cv * ip;                // cov**2 / (vx*vy)     CM:212
+        scr += Cv * rp;                     // cov / (vx*vy)**0.5   CM:261
         ++Wq;
       }
       if (W == 0) b0 = beta;  // betas shifted by the first one (a member)
@@ -720,7 +724,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       double bstd = 0.0;
       if (has_std) bstd = sqrt((bd2 - bd1 * bd1 / (double)W) / (double)(W - 1));
       if (has_std && tot_ne(bstd, 0.0) && Wq > 0)
-        val(5, (sq / (double)Wq) * (bl - bmean) / bstd);  // mmt_ols_qrs CM:156-171
+        val(5, (sq * kOlsSq / (double)Wq) * (bl - bmean) / bstd);  // mmt_ols_qrs CM:156-171
       else
         val(5, 0.0);
       val(6, Wq > 0 ? scs / (double)Wq : 0.0);  // mmt_ols_corr_square_mean

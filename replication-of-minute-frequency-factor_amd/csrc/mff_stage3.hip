@@ -293,8 +293,12 @@ __global__ __launch_bounds__(SORT_THREADS) void k_xs_rank(const double* val, con
 // appended to a list for the sorting kernel (k_xs_rank).
 constexpr int XB1 = 1024;
 constexpr int XB2 = 2048;
-constexpr int XR_PER = 8;
-constexpr int XR_THREADS = 1024;  // default block; XR_THREADS is also the kernel template parameter
+#ifndef MFF_XR_THREADS
+#define MFF_XR_THREADS 1024
+#endif
+constexpr int XR_THREADS = MFF_XR_THREADS;  // default block; XR_THREADS is also the kernel template parameter
+constexpr int XR_PER = 8192 / XR_THREADS;   // values per thread at most (M <= 8192)
+constexpr int XR_PER_LO = (5 * 1024) / XR_THREADS;  // the smaller instantiation (S <= 5120 at R = 1)
 constexpr int XR_MAXO = 48;
 
 __global__ void k_xs_rank_list_init(uint32_t* list) { list[0] = 0u; }
@@ -303,6 +307,33 @@ __global__ void k_xs_rank_list_init(uint32_t* list) { list[0] = 0u; }
 __device__ __forceinline__ uint32_t get16(const uint32_t* w, uint32_t i) { return (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; }
 __device__ __forceinline__ uint32_t inc16(uint32_t* w, uint32_t i) {
   return (atomicAdd(&w[i >> 1], 1u << (16 * (i & 1))) >> (16 * (i & 1))) & 0xFFFFu;
+}
+// inc16 with the wave's hot bucket aggregated: the active lanes holding the first active
+// lane's counter index take one atomic (the count) and slots base + their rank among
+// themselves; the others take one atomic each.  Tie-heavy days put most of a wave's
+// values into one bucket, whose LDS word would otherwise take 64 serialized atomics per
+// wave-instruction.  Slots inside a bucket are interchangeable (any key may be slot 0).
+// Measured slower at c4 (all 58 rows 11.0 -> 11.9 ms): off by default.
+#ifndef MFF_XR_AGG
+#define MFF_XR_AGG 0
+#endif
+__device__ __forceinline__ uint32_t inc16_agg(uint32_t* w, uint32_t i) {
+  if (!MFF_XR_AGG) return inc16(w, i);
+  const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+  const uint64_t same = __ballot(i == i0);
+  uint32_t r;
+  if (i == i0) {
+    const uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
+    uint32_t base = 0u;
+    if (before == 0u) {
+      const uint32_t sh = 16u * (i0 & 1u);
+      base = (atomicAdd(&w[i0 >> 1], (uint32_t)__popcll(same) << sh) >> sh) & 0xFFFFu;
+    }
+    r = (uint32_t)__builtin_amdgcn_readfirstlane((int)base) + before;
+  } else {
+    r = inc16(w, i);
+  }
+  return r;
 }
 
 struct XrBucket {
@@ -501,7 +532,7 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
       for (int j = 0; j < PER; ++j) {
         if ((inc >> j) & 1u) {
           double f;
-          inc16(h1, bk.l1(x[j], f));
+          inc16_agg(h1, bk.l1(x[j], f));
         }
       }
       __syncthreads();
@@ -536,7 +567,7 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
       for (int j = 0; j < PER; ++j) {
         if ((inc >> j) & 1u) {
           const uint32_t b = bk(x[j]);
-          bp[j] = (b << 16) | inc16(bins, b);
+          bp[j] = (b << 16) | inc16_agg(bins, b);
         } else {
           bp[j] = 0u;
         }
@@ -572,7 +603,7 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
           const uint32_t b = bp[j] >> 16;
           if (sk[get16(bins, b)] == ord64(x[j])) {
             isref |= 1u << j;
-            inc16(eqc, b);
+            inc16_agg(eqc, b);
           }
         }
       }
@@ -610,7 +641,7 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
     for (int j = 0; j < PER; ++j) {
       if (((inc & ~isref) >> j) & 1u) {
         const uint32_t b = bp[j] >> 16;
-        sk[get16(bins, b) + get16(eqc, b) + inc16(ctr, b)] = ord64(x[j]);
+        sk[get16(bins, b) + get16(eqc, b) + inc16_agg(ctr, b)] = ord64(x[j]);
       }
     }
     __syncthreads();
@@ -743,8 +774,8 @@ int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_
     hipLaunchKernelGGL(k_xs_rank_list_init, dim3(1), dim3(1), 0, st, list);
     const int gb = (int)(nseg < 4 * XS_RANK_GRID ? nseg : 4 * XS_RANK_GRID);
     constexpr int thr = XR_THREADS;
-    auto kern = R == 1 ? (M <= 5 * thr ? k_xs_rank_bucket<5, true, thr> : k_xs_rank_bucket<8, true, thr>)
-                       : (M <= 5 * thr ? k_xs_rank_bucket<5, false, thr> : k_xs_rank_bucket<8, false, thr>);
+    auto kern = R == 1 ? (M <= XR_PER_LO * thr ? k_xs_rank_bucket<XR_PER_LO, true, thr> : k_xs_rank_bucket<XR_PER, true, thr>)
+                       : (M <= XR_PER_LO * thr ? k_xs_rank_bucket<XR_PER_LO, false, thr> : k_xs_rank_bucket<XR_PER, false, thr>);
     hipLaunchKernelGGL(kern, dim3(gb), dim3(thr), 0, st, val, state, rows, D, S_loc, val_all,
                        state_all, R, S_all, out_val, out_state, list);
     MFF_LAUNCH_CHECK();
