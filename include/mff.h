@@ -106,7 +106,10 @@ size_t mff_stage1_workspace_bytes(int S, int D);
  * doc_pdf levels and queries, exact list), part 2 = ORD + the serial families.  Once part 1 is
  * done the mff_pdf_* phases may run on another stream, concurrently with part 2.
  * part 3 = mff_stage1.  part 4 = the high / low serial families (OLS, MOMH) alone, which
- * depend on no other launch (any stream, any time); part 10 / 11 = part 2 / 3 without them. */
+ * depend on no other launch (any stream, any time); part 10 / 11 = part 2 / 3 without them.
+ * part 17 = part 1 without the exact list kernel, part 32 = that kernel alone (after part
+ * 17, before the mff_pdf_* phases and before the LVL/PDF rows are read; part 2 need not
+ * wait for it). */
 int mff_stage1_part(const float* open, const float* high, const float* low,
                     const float* close, const float* volume, const uint32_t* valid,
                     int S, int D, const int32_t* factor_ids /* host */, int nf,

@@ -998,14 +998,18 @@ extern "C" size_t mff_pdf_levels_bytes(int S, int D) {
 // the doc_pdf rank needs; part bit 2: the ORD group and the serial families (which read
 // the ORD thresholds).  mff_stage1 = both, in that order.  Bit 4: the high / low serial
 // kernel (OLS, MOMH) alone — it reads nothing another launch writes, so it may run on its
-// own stream from the start; bit 8 (with bit 2): part 2 without it.
+// own stream from the start; bit 8 (with bit 2): part 2 without it.  Part 17 = part 1
+// without the exact list kernel, part 32 = that kernel alone (it only adds LVL/PDF
+// values and doc_pdf levels of the listed stock-days, so the serial families need not
+// wait for it).
 static int stage1_parts(const float* open, const float* high, const float* low, const float* close,
                         const float* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
                         int nf, double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
                         void* workspace, void* stream, int part) {
   clear_error();
-  MFF_REQUIRE(part >= 1 && part <= 15 && (!(part & 8) || (part & 2)) && !((part & 4) && (part & 3)),
-              "mff_stage1_part: part=%d must be 1, 2, 3, 4, 10 or 11", part);
+  MFF_REQUIRE(part == 1 || part == 2 || part == 3 || part == 4 || part == 10 || part == 11 || part == 17 ||
+                  part == 32,
+              "mff_stage1_part: part=%d must be 1, 2, 3, 4, 10, 11, 17 or 32", part);
   MFF_REQUIRE(S > 0 && D > 0, "mff_stage1: S=%d D=%d must be positive", S, D);
   MFF_REQUIRE((long long)S * D < (1ll << 31), "mff_stage1: S*D must be < 2^31");
   MFF_REQUIRE(nf > 0 && nf <= NF, "mff_stage1: nf=%d out of range", nf);
@@ -1056,16 +1060,21 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
     MFF_LAUNCH_CHECK();
     return 0;
   };
+  if (a.fam & F_PDF) {
+    size_t ok, ow;
+    pdf_levels_split(S, D, &ok, &ow);
+    char* base = reinterpret_cast<char*>(pdf_levels);
+    a.lvl_count = reinterpret_cast<uint32_t*>(base);
+    a.lvl_key = reinterpret_cast<uint64_t*>(base + ok);
+    a.lvl_w = reinterpret_cast<uint8_t*>(base + ow);
+  }
+  if (part == 32) {  // the exact list kernel alone (after part 17, e.g. on another stream)
+    if (w64 || !(a.fam & (F_LVL | F_PDF))) return 0;
+    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_LVL | F_PDF, 1024,
+                      st, a.lvl_count, a.lvl_key, a.lvl_w);
+  }
   if (part & 1) {  // LVL/PDF group + exact list: everything the doc_pdf phases read
-    if (a.fam & F_PDF) {
-      size_t ok, ow;
-      pdf_levels_split(S, D, &ok, &ow);
-      char* base = reinterpret_cast<char*>(pdf_levels);
-      a.lvl_count = reinterpret_cast<uint32_t*>(base);
-      a.lvl_key = reinterpret_cast<uint64_t*>(base + ok);
-      a.lvl_w = reinterpret_cast<uint8_t*>(base + ow);
-      MFF_HIP(hipMemsetAsync(a.lvl_count, 0, (size_t)D * 4, st));
-    }
+    if (a.fam & F_PDF) MFF_HIP(hipMemsetAsync(a.lvl_count, 0, (size_t)D * 4, st));
     MFF_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
     if (w64) {  // the wave-per-stock-day kernel for everything
       const int rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, nullptr, nullptr, ~0u, 0, st);
@@ -1084,8 +1093,9 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
     // ORD in the same launch when both sorted groups are requested (part 2 then skips it)
     int rc = group_launch(MFF_MERGE_OL && (a.fam & g16::G_ORD) && (a.fam & (F_LVL | F_PDF)) ? 2 : 1);
     if (rc != 0) return rc;
-    if (a.fam & (F_LVL | F_PDF)) {
-      // exact general path for the listed stock-days (LVL + PDF only)
+    if ((a.fam & (F_LVL | F_PDF)) && !(part & 16)) {
+      // exact general path for the listed stock-days (LVL + PDF only); part 17 leaves it
+      // to a later part-32 call
       rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt,
                       F_LVL | F_PDF, 1024, st, a.lvl_count, a.lvl_key, a.lvl_w);
       if (rc != 0) return rc;

@@ -70,6 +70,9 @@ constexpr uint32_t kSerAB = kSerA | kSerB;  // one pass over open, close, volume
 #ifndef MFF_SERB_FAST
 #define MFF_SERB_FAST 1
 #endif
+#ifndef MFF_CAPTURE_BRANCH
+#define MFF_CAPTURE_BRANCH 0
+#endif
 #ifndef MFF_PAIR_QREAD
 #define MFF_PAIR_QREAD 0
 #endif
@@ -328,8 +331,13 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         const bool up = pk & (r > 0.0), dn = pk & (r < 0.0);  // r is finite (no NaN case)
         nu += up ? 1 : 0;
         ndn += dn ? 1 : 0;
-        xu = (up & !hu) ? r : xu;
-        xd = (dn & !hd) ? r : xd;
+        // first up / down member of each lane: a wave-uniform branch, taken only while
+        // some lane still meets its first one (the first few bars), not a select per bar
+        const bool cu = up & !hu, cd = dn & !hd;
+        if (MFF_CAPTURE_BRANCH ? __builtin_amdgcn_ballot_w64(cu | cd) != 0ull : true) {
+          xu = cu ? r : xu;
+          xd = cd ? r : xd;
+        }
         hu |= up;
         hd |= dn;
         const double eu = up ? r - xu : 0.0, ed = dn ? r - xd : 0.0;
@@ -403,7 +411,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         if (hz) {
           const double pcz = fdivr(c - (double)czp, (double)czp, rcz);
           const double pvz = fdivr(v - (double)vzp, (double)vzp, rvz);
-          if (nzc == 1) { x5 = pcz; y5 = pvz; x6 = c; }  // first pair: the shifts
+          // first pair: the shifts (a wave-uniform branch, as for set A's captures)
+          if (MFF_CAPTURE_BRANCH ? __builtin_amdgcn_ballot_w64(nzc == 1) != 0ull : true) {
+            if (nzc == 1) { x5 = pcz; y5 = pvz; x6 = c; }
+          }
           const double dy = pvz - y5, e5 = pcz - x5, e6 = c - x6;
           Z1 += dy; Z2 = fma(dy, dy, Z2);
           F1 += e5; F2 = fma(e5, e5, F2); FX = fma(e5, dy, FX);  // prvr

@@ -119,7 +119,7 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
 
         if hl is not None and HL_AT == "start":
             launch_hl()
-        _lib.check(lib.mff_stage1_part(*args, 1), "mff_stage1_part(1)")
+        _lib.check(lib.mff_stage1_part(*args, 17 if EXACT_SIDE and not PDF_FIRST else 1), "mff_stage1_part(1)")
         if hl is not None and HL_AT == "part1":
             launch_hl()
         if PDF_FIRST:
@@ -132,8 +132,14 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
         else:
             side = _side_stream(dev)
             side.wait_stream(main)
+            if EXACT_SIDE:  # the exact list kernel ahead of the doc_pdf phases, off the launch stream
+                _lib.check(lib.mff_stage1_part(*(args[:-1] + [side.cuda_stream]), 32), "mff_stage1_part(32)")
+            sorted_ev = torch.cuda.Event() if SORT_FIRST and comm is None else None
             with torch.cuda.stream(side):
-                pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
+                pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch,
+                          after_sort=(lambda: sorted_ev.record(side)) if sorted_ev is not None else None)
+            if sorted_ev is not None:  # part 2 after the doc_pdf sort (whole-CU workgroups)
+                main.wait_event(sorted_ev)
             _lib.check(lib.mff_stage1_part(*args, 10 if hl is not None else 2), "mff_stage1_part(2)")
             main.wait_stream(side)
         if hl is not None and HL_AT == "pdf" and not PDF_FIRST:
@@ -153,6 +159,12 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
 
 # MFF_PDF_OVERLAP=0: doc_pdf after the whole stage-1 pass on one stream (A/B timing)
 PDF_OVERLAP = os.environ.get("MFF_PDF_OVERLAP", "1") != "0"
+# MFF_EXACT_SIDE=1 (default): the exact list kernel (LVL/PDF of the listed stock-days) runs on
+# the doc_pdf side stream, so part 2 starts right after the sorted-group kernel
+EXACT_SIDE = os.environ.get("MFF_EXACT_SIDE", "1") != "0"
+# MFF_SORT_FIRST=1: part 2 waits for the doc_pdf sort (which otherwise gets CUs only as the
+# wave-pair kernel's blocks drain)
+SORT_FIRST = os.environ.get("MFF_SORT_FIRST", "0") != "0"
 # MFF_PDF_FIRST=1: the doc_pdf phases on the launch stream between part 1 and part 2
 PDF_FIRST = os.environ.get("MFF_PDF_FIRST", "0") != "0"
 # The high / low serial kernel (OLS, MOMH) reads only the high / low planes and writes
@@ -182,8 +194,9 @@ def _side_stream(dev, which: int = 0) -> torch.cuda.Stream:
 
 def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows: List[int], val, state,
               comm=None,
-              day_batch: Optional[int] = None, workspace_budget: int = 2 << 30):
-    """doc_pdf frame-wide ranks (CM:1015-1017) for all days, in day batches."""
+              day_batch: Optional[int] = None, workspace_budget: int = 2 << 30, after_sort=None):
+    """doc_pdf frame-wide ranks (CM:1015-1017) for all days, in day batches.  ``after_sort``:
+    optional callable, invoked once the first day batch's sort is enqueued (single rank)."""
     lib = _lib.load()
     D, S = panel.D, panel.S
     dev = panel.device
@@ -203,6 +216,8 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
         q_sorted = torch.empty((nd, M), dtype=torch.int64, device=dev)
         _lib.check(lib.mff_pdf_sort(_lib.ptr(pdfq), R, S_all, D, d0, nd, _lib.ptr(q_sorted),
                                     _lib.ptr(ws), st), "mff_pdf_sort")
+        if after_sort is not None and d0 == 0:
+            after_sort()
         # single rank: count + finalize fused, no exchange
         _lib.check(lib.mff_pdf_rank_local(_lib.ptr(levels), _lib.ptr(pdfq), S, D, d0, nd,
                                           _lib.ptr(q_sorted), M,
