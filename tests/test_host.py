@@ -58,6 +58,12 @@ def test_library_catalogue_and_errors_without_gpu():
     with pytest.raises(_lib.MffError):
         _lib.check(rc, "mff_stage2")
     assert lib.mff_pdf_workspace_bytes(300, 1, 10) > 0
+    # mff_stage1_part: the part codes of include/mff.h, checked before any device work
+    ids = _lib.int_array([0])
+    for part in (0, 5, 8, 16, 18, 33):
+        rc = lib.mff_stage1_part(None, None, None, None, None, None, 10, 10, ids, 1, None, None, None, None,
+                                 None, None, part)
+        assert rc < 0 and f"part={part}".encode() in lib.mff_last_error()
 
 
 def test_mask_roundtrip():
