@@ -435,7 +435,6 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
       }
 
       // ================================================================ ORD / ORDV sort
-      float th50 = 0.f, th20 = 0.f, tb50 = 0.f;
       if (fam & (F_ORD | F_ORDV)) {
         fresh(v);
 
@@ -456,9 +455,6 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
                     : (n >= 50 ? 49 : n - 1);             // bottom_k(50).max() CM:417-422
         const float xe = (e >= 0 && g < 13) ? bitsf(so[((e & 15) << 4) | (e >> 4)]) : 0.0f;
         lds_fence();  // the LVL section reuses the scratch
-        th50 = bpermf(gb + 10, xe);
-        th20 = bpermf(gb + 11, xe);
-        tb50 = bpermf(gb + 12, xe);
         if ((fam & F_ORD) && a.ord_th && g >= 10 && g < 13 && act) {
           const size_t pl = (size_t)a.D * a.S;
           a.ord_th[(size_t)(g - 10) * pl + sd] = xe;
@@ -783,7 +779,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
         for (int k = 0; k < K; ++k) {
           // integral and in [+0, 2^24] (v is sanitized: no -0; NaN / inf / negatives
           // have bit patterns above the one of 2^24)
-          const bool vok = (v[k] == rintf(v[k])) & (fbits(v[k]) <= 0x4b800000u);
+          const bool vok = (v[k] == rintf(v[k])) && (fbits(v[k]) <= 0x4b800000u);
           vokm |= (vok ? 1u : 0u) << k;
           cmx = max(cmx, fbits(c[k]) & present_bits(pb, k));
           cmn = min(cmn, fbits(c[k]) | absent_bits(pb, k));
