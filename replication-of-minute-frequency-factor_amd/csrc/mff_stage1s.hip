@@ -60,6 +60,15 @@ constexpr uint32_t kSerB = F_MOMV | F_SUMV | F_SUMC | F_CORR;  // close, volume
 constexpr uint32_t kSerH = F_OLS | F_MOMH;                     // high, low
 constexpr uint32_t kSerial = kSerA | kSerB | kSerH;
 constexpr uint32_t kSerAB = kSerA | kSerB;  // one pass over open, close, volume
+// The wave pair's split of sets A + B.  Timed alone with both waves on one set (c4):
+// set A 14.3 ms, set B 18.0 ms, the pair 17.3 ms: set B is the longer walk, so the
+// volume moments and sums (MOMV, SUMV: the running volume sum is set A's TRD sum
+// already) move to the set-A wave (MFF_PAIR_SPLIT=1).
+#ifndef MFF_PAIR_SPLIT
+#define MFF_PAIR_SPLIT 1
+#endif
+constexpr uint32_t kPairA = MFF_PAIR_SPLIT ? (kSerA | F_MOMV | F_SUMV) : kSerA;
+constexpr uint32_t kPairB = MFF_PAIR_SPLIT ? (F_SUMC | F_CORR) : kSerB;
 #ifndef MFF_PAIR_AB
 #define MFF_PAIR_AB 1
 #endif
@@ -447,7 +456,8 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       // ABSENT whatever they accumulated
       // (set A, and set B in the pair form, where it has set A's register budget; set B's
       // own kernel has no room for the second copy)
-      if (((SET == kSerA && MFF_SERA_FAST) || (SET == kSerB && PAIR && MFF_SERB_FAST)) &&
+      if (((SET == kSerA && MFF_SERA_FAST) || (PAIR && SET == kPairA && MFF_SERA_FAST) ||
+           (PAIR && SET == kPairB && MFF_SERB_FAST)) &&
           __builtin_amdgcn_ballot_w64((pm & 0xFu) != 0xFu && n > 0) == 0ull) {
         const std::true_type all;
         bar(m0 + 0, true, x.o.x, x.c.x, x.v.x, all);
@@ -783,8 +793,8 @@ __global__ __launch_bounds__(256, SET == kSerB ? 3 : 2) void k_stage1s(SArgs a) 
 // number of barriers (one per 16-bar chunk).
 __global__ __launch_bounds__(128, 2) void k_stage1s_pair(SArgs a) {
   __shared__ __attribute__((aligned(16))) float4 pbuf[2 * 3 * 64 * 4];
-  if (threadIdx.x < 64) s1s_body<kSerA, true, 1>(a, pbuf);
-  else s1s_body<kSerB, true, 1>(a, pbuf);
+  if (threadIdx.x < 64) s1s_body<kPairA, true, 1>(a, pbuf);
+  else s1s_body<kPairB, true, 1>(a, pbuf);
 }
 
 }  // namespace s1s
