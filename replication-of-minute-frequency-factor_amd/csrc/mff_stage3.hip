@@ -383,7 +383,8 @@ __device__ __forceinline__ int xr_shift(uint64_t span, uint32_t N) {
   return sh;
 }
 
-// block-wide exclusive scan of one u32 per thread; *total = block sum.  Ends synced.
+// block-wide exclusive scan of one u32 per thread; *total = block sum.  Does not end
+// synced: both callers pass a barrier before wsum is written again.
 template <int NT>
 __device__ __forceinline__ uint32_t xr_scan(uint32_t x, uint32_t* wsum, uint32_t* total) {
   const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
@@ -402,7 +403,6 @@ __device__ __forceinline__ uint32_t xr_scan(uint32_t x, uint32_t* wsum, uint32_t
     tot += wsum[w];
   }
   *total = tot;
-  __syncthreads();
   return off;
 }
 
@@ -478,6 +478,14 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
       }
     }
   };
+  // Counters are cleared inside phases that end in a barrier anyway: mm at the end of a
+  // segment (its readers are long past), h1 / bins / eqc / ctr / ctl[0] in the next
+  // segment's min / max phase (after the loop-end barrier, before their first use).
+  auto reset_mm = [&]() {
+    if (tid < 6) mm[tid] = (tid & 1) ? 0ull : ~0ull;
+  };
+  reset_mm();
+  __syncthreads();
   if (LOCAL) load(blockIdx.x);
   for (size_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
     if (!LOCAL) load(seg);
@@ -493,8 +501,9 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
       stn |= (sb == MFF_STATE_NULL ? 1u : 0u) << j;
     }
     if (LOCAL) load(seg + gridDim.x);  // in flight while this segment is ranked
-    if (tid < 6) mm[tid] = (tid & 1) ? 0ull : ~0ull;
-    __syncthreads();
+    for (int w = tid; w < XB1 / 2; w += XR_THREADS) h1[w] = 0u;
+    for (int w = tid; w < XB2 / 2; w += XR_THREADS) { bins[w] = 0u; eqc[w] = 0u; ctr[w] = 0u; }
+    if (tid == 0) ctl[0] = 0u;
     stats(0, 2, x, inc);  // finite min / max; the log scheme's stats only if linear fails
     __syncthreads();
     XrBucket bk;
@@ -523,11 +532,15 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
         bk.shn = xr_shift(mm[2] == ~0ull ? 0ull : mm[3] - mm[2], N1);
         bk.shp = xr_shift(mm[4] == ~0ull ? 0ull : mm[5] - mm[4], N1);
       }
-      // level 1: histogram -> sub-bucket counts -> level-2 bases
-      for (int w = tid; w < XB1 / 2; w += XR_THREADS) h1[w] = 0u;
-      for (int w = tid; w < XB2 / 2; w += XR_THREADS) { bins[w] = 0u; eqc[w] = 0u; }
-      if (tid == 0) ctl[0] = 0u;
-      __syncthreads();
+      // level 1: histogram -> sub-bucket counts -> level-2 bases (scheme 0's counters
+      // were cleared in the min / max phase; the log scheme after a failed linear one
+      // clears them here, behind the barrier that closed scheme 0's check)
+      if (scheme == 1 && __builtin_isfinite(bk.scale)) {
+        for (int w = tid; w < XB1 / 2; w += XR_THREADS) h1[w] = 0u;
+        for (int w = tid; w < XB2 / 2; w += XR_THREADS) { bins[w] = 0u; eqc[w] = 0u; }
+        if (tid == 0) ctl[0] = 0u;
+        __syncthreads();
+      }
 #pragma unroll
       for (int j = 0; j < PER; ++j) {
         if ((inc >> j) & 1u) {
@@ -627,16 +640,18 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
       if (lane == 0) atomicMax(&ctl[0], mo);
       __syncthreads();
       ok = ctl[0] <= (uint32_t)XR_MAXO;  // block-uniform
-      __syncthreads();
+      // ctl[0] is rewritten by the log scheme's clearing or the next segment's min / max
+      // phase: every thread reads it before either (a failed check syncs here)
+      if (!ok) __syncthreads();
     }
     if (!ok) {  // hand the segment to the sorting kernel
       if (tid == 0) list[1 + atomicAdd(&list[0], 1u)] = (uint32_t)seg;
+      reset_mm();
+      __syncthreads();
       continue;
     }
     // pack each bucket's non-reference keys behind its reference-equal run (the
     // reference stays at slot 0: the packed keys start at slot eqc >= 1)
-    for (int w = tid; w < XB2 / 2; w += XR_THREADS) ctr[w] = 0u;
-    __syncthreads();
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
       if (((inc & ~isref) >> j) & 1u) {
@@ -644,6 +659,7 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
         sk[get16(bins, b) + get16(eqc, b) + inc16_agg(ctr, b)] = ord64(x[j]);
       }
     }
+    reset_mm();
     __syncthreads();
     auto rank_of = [&](double cv, uint32_t b) {
       const uint64_t kk = ord64(cv);
