@@ -346,10 +346,10 @@ def main():
                 "traffic_calibrated": traffic_cal,
                 "valu": valu,
                 "kernel": "stage-1 pass over three streams: k_stage1s<OLS|MOMH> (own stream), "
-                          "k_stage1g<ORD|ORDV|LVL|PDF> + k_stage1 exact list, then k_stage1s_pair "
-                          "(wave pair: <SEG|MOMR|TRD|ORD> + <MOMV|SUMV|SUMC|CORR>) on the launch "
-                          "stream, doc_pdf k_pdf_sort / k_pdf_count (side stream); window = the "
-                          "whole pass",
+                          "k_stage1g<ORD|ORDV|LVL|PDF>, then k_stage1s_pair (wave pair: "
+                          "<SEG|MOMR|TRD|ORD|MOMV|SUMV> + <SUMC|CORR>) on the launch stream, "
+                          "k_stage1 exact list + doc_pdf k_pdf_sort / k_pdf_count (side stream); "
+                          "window = the whole pass",
                 "bytes_per_launch": bytes_launch,
                 "avg_kernel_ms": round(k_ms, 3),
             },

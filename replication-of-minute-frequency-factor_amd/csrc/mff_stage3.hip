@@ -282,7 +282,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_xs_rank(const double* val, con
 //    or, when that leaves a bucket too full, per sign linear in the IEEE bits above the
 //    smallest magnitude (scheme 1: a log-scale histogram, zero its own bucket); -inf / +inf
 //    take the first / last bucket;
-//  * level 2: level-1 bucket b (c_b values) is cut into n_b = 1 + c_b * XB1 / M equal
+//  * level 2: level-1 bucket b (c_b values) is cut into n_b = 1 + c_b * (XB2 - XB1) / M equal
 //    sub-ranges (sum n_b <= XB2), so a dense cluster gets proportionally finer buckets
 //    (histogram equalisation: ~M / XB1 values per bucket whatever the distribution);
 //  * ties: the key a bucket's slot 0 received is its reference; the keys equal to it are
@@ -291,8 +291,14 @@ __global__ __launch_bounds__(SORT_THREADS) void k_xs_rank(const double* val, con
 //    bucket's scan covers its non-reference keys only.
 // A segment with a bucket of more than XR_MAXO non-reference keys under both schemes is
 // appended to a list for the sorting kernel (k_xs_rank).
-constexpr int XB1 = 1024;
-constexpr int XB2 = 2048;
+#ifndef MFF_XB1
+#define MFF_XB1 1024
+#endif
+#ifndef MFF_XB2
+#define MFF_XB2 2048
+#endif
+constexpr int XB1 = MFF_XB1;
+constexpr int XB2 = MFF_XB2;
 #ifndef MFF_XR_THREADS
 #define MFF_XR_THREADS 1024
 #endif
@@ -558,8 +564,8 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const uint32_t c = (cw >> (16 * h)) & 0xFFFFu;
-            // 1 + c * XB1 / M sub-ranges: sum <= XB1 + XB1 = XB2
-            nb[2 * q + h] = c ? 1u + (uint32_t)((c * (uint32_t)XB1) / (uint32_t)M) : 0u;
+            // 1 + c * (XB2 - XB1) / M sub-ranges: sum <= XB1 + (XB2 - XB1) = XB2
+            nb[2 * q + h] = c ? 1u + (uint32_t)((c * (uint32_t)(XB2 - XB1)) / (uint32_t)M) : 0u;
             loc += nb[2 * q + h];
           }
         }
