@@ -61,9 +61,14 @@ struct QLoader {
   int nrow;
   __device__ int rows() const { return nrow; }
   __device__ int cols() const { return S; }
-  __device__ uint64_t at(int rt, int s) const {
-    const double x = q[((size_t)rt * D + d) * S + s];
-    return __builtin_isnan(x) ? ~0ull : ord64(x);
+  __device__ uint64_t at(int rt, int s) const { return key(raw(rt, s)); }
+  // the load and the key conversion apart, so the sort's passes issue a batch of loads
+  // before converting any of them
+  __device__ double raw(int rt, int s) const { return q[((size_t)rt * D + d) * S + s]; }
+  __device__ static uint64_t key(double x) {
+    // branch-free: a select, not a divergent region between the loads and their use
+    const uint64_t k = ord64(x);
+    return __builtin_isnan(x) ? ~0ull : k;
   }
 };
 

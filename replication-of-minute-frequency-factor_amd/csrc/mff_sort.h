@@ -188,6 +188,24 @@ __device__ void segment_sort(const Loader& ld, int M, uint64_t* out, uint64_t* t
 // one bin holds more than SORT_CAPB/2 keys: the caller then uses segment_sort.
 // LDS: sk [SORT_CAPB] keys, bins [SORT_NBIN + 1] u32, ctl [64] u32.  Ranges are sorted
 // by bitonic_regs<E> over the smallest 1024*E (E = 2..16) slots that hold them.
+// Walk every key of the loader that this thread owns ((row, column) with column =
+// tid + k * nt), SORT_LB keys' loads in flight at a time (a plain loop waits for each
+// load before the next: the passes were latency bound), calling f(key) for each.
+#ifndef SORT_LB
+#define SORT_LB 8
+#endif
+template <typename Loader, typename F>
+__device__ __forceinline__ void sort_walk(const Loader& ld, int tid, int nt, F&& f) {
+  const int rows = ld.rows(), cols = ld.cols();
+  for (int rw = 0; rw < rows; ++rw)
+    for (int c0 = tid; c0 < cols; c0 += SORT_LB * nt) {
+      double xx[SORT_LB];
+#pragma unroll
+      for (int j = 0; j < SORT_LB; ++j) xx[j] = ld.raw(rw, min(c0 + j * nt, cols - 1));  // unconditional loads
+#pragma unroll
+      for (int j = 0; j < SORT_LB; ++j) f(c0 + j * nt < cols ? Loader::key(xx[j]) : ~0ull);
+    }
+}
 constexpr int SORT_NBIN = 2048;
 constexpr int SORT_CAPB = 8192;  // keys per range (with the bins: 72 KiB of LDS, two workgroups per CU)
 constexpr int SORT_REG = 32;  // segment_sort_binned takes M <= SORT_REG * blockDim
@@ -197,14 +215,12 @@ __device__ bool segment_sort_binned(const Loader& ld, int M, uint64_t* out, uint
   const int nt = (int)blockDim.x, tid = (int)threadIdx.x;
   uint64_t mn = ~0ull, mx = 0ull;
   // the loader is walked as (row, column) so no thread divides an index
-  for (int rw = 0; rw < ld.rows(); ++rw)
-    for (int c = tid; c < ld.cols(); c += nt) {
-      const uint64_t k = ld.at(rw, c);
-      if (k != ~0ull) {
-        mn = min(mn, k);
-        mx = max(mx, k);
-      }
+  sort_walk(ld, tid, nt, [&](uint64_t k) {
+    if (k != ~0ull) {
+      mn = min(mn, k);
+      mx = max(mx, k);
     }
+  });
   // block min / max (ctl[0..1] lo/hi of min, ctl[2..3] of max, via 64-bit atomics)
   unsigned long long* c64 = reinterpret_cast<unsigned long long*>(ctl);
   if (tid == 0) {
@@ -220,11 +236,9 @@ __device__ bool segment_sort_binned(const Loader& ld, int M, uint64_t* out, uint
   const bool any = kmin != ~0ull;
   int sh = 0;
   while (any && ((kmax - kmin) >> sh) >= (uint64_t)SORT_NBIN) ++sh;
-  for (int rw = 0; rw < ld.rows(); ++rw)
-    for (int c = tid; c < ld.cols(); c += nt) {
-      const uint64_t k = ld.at(rw, c);
-      if (k != ~0ull) atomicAdd(&bins[(uint32_t)((k - kmin) >> sh)], 1u);
-    }
+  sort_walk(ld, tid, nt, [&](uint64_t k) {
+    if (k != ~0ull) atomicAdd(&bins[(uint32_t)((k - kmin) >> sh)], 1u);
+  });
   __syncthreads();
   // exclusive scan of the bins (SORT_NBIN / nt contiguous bins per thread), max bin
   const int per = SORT_NBIN / nt;
@@ -284,13 +298,11 @@ __device__ bool segment_sort_binned(const Loader& ld, int M, uint64_t* out, uint
     __syncthreads();  // the previous range's readers are done with sk
     for (int i = tid; i < P; i += nt) sk[i] = ~0ull;
     __syncthreads();
-    for (int rw = 0; rw < ld.rows(); ++rw)
-      for (int c = tid; c < ld.cols(); c += nt) {
-        const uint64_t k = ld.at(rw, c);
-        if (k == ~0ull) continue;
-        const int b = (int)((k - kmin) >> sh);
-        if (b >= b0 && b < b1) sk[atomicAdd(&bins[b], 1u) - base] = k;
-      }
+    sort_walk(ld, tid, nt, [&](uint64_t k) {
+      if (k == ~0ull) return;
+      const int b = (int)((k - kmin) >> sh);
+      if (b >= b0 && b < b1) sk[atomicAdd(&bins[b], 1u) - base] = k;
+    });
     __syncthreads();
     switch (P) {
       case 2048: bitonic_regs<2>(sk); break;
