@@ -334,7 +334,9 @@ def main():
                 "workload": f"c4: {S} stocks x 240 min x {D} days, all 58 CICC factors "
                             f"(stage 1 incl. doc_pdf frame-wide rank)",
                 "stocks": S, "days": D, "minutes": 240, "factors": 58,
-                "parallelism": f"stock-sharded x{world}",
+                "parallelism": f"stock-sharded x{world}" + (
+                    f" ({comm.backend}, world_size {comm.world_size} per torch.distributed)"
+                    if comm is not None else " (single process, no collectives)"),
             },
             "roofline": {
                 "bound": "hbm",

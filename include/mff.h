@@ -170,6 +170,14 @@ int mff_pdf_sort(const double* q_all, int R, int S_all, int D, int d0, int nd,
 int mff_pdf_count(const void* pdf_levels, int S_loc, int D, int d0, int nd,
                   const uint64_t* q_sorted, int M, uint32_t* counts, void* workspace,
                   void* stream);
+/* Frame-wide count (one cal_doc_pdf* call on a frame holding several dates: `.rank()`
+ * at CM:1015-1017 ranks every row of every date).  The D days' queries are sorted as ONE
+ * list (mff_pdf_sort with the [5][D][S] queries viewed as [5][1][D*S]); every day's level
+ * keys are counted against it and their words 2 n_less + n_eq ADDED to counts uint32 [M]
+ * (zeroed by the caller); mff_pdf_finalize with S_loc = D*S, D = 1 then writes the ranks.
+ * Requires 240*S*D < 2^31 and M <= 2^24. */
+int mff_pdf_count_frame(const void* pdf_levels, int S, int D, const uint64_t* q_sorted, int M,
+                        uint32_t* counts, void* stream);
 int mff_pdf_finalize(const double* q_local, const uint64_t* q_sorted,
                      const uint32_t* counts, int S_loc, int D, int d0, int nd, int M,
                      const int32_t* pdf_rows /* host, 5 entries, -1 = skip */,

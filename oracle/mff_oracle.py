@@ -948,6 +948,32 @@ def oracle_stage1(panel, names: Sequence[str] = None):
 
 
 FRAME_XDAY_NAMES = ["liq_amihud_1min", "corr_prvr", "trade_bottom20retRatio", "trade_bottom50retRatio"]
+FRAME_RANK_NAMES = ["doc_pdf60", "doc_pdf70", "doc_pdf80", "doc_pdf90", "doc_pdf95"]
+
+
+def oracle_frame_doc_pdf(panel):
+    """doc_pdf60..95 when ONE cal_doc_pdf* call gets all days of `panel` as a single
+    frame (CM:1011-1030 and the copies through 1138): the level key
+    close.last().over(code, date) / close and the levels stay per (code, date), but
+    `.rank()` (CM:1015-1017) is outside any `.over`, so it ranks every row of every date.
+    _doc_pdf runs on a frame whose groups are the (code, date) pairs.
+    Returns {name: (val [D][S], state [D][S])}."""
+    D, S = panel["present"].shape[:2]
+    parts = [day_frame_from_panel(panel, d) for d in range(D)]
+    lab = np.concatenate([np.char.add(np.asarray(p.code, dtype=str), f"|{d}") for d, p in enumerate(parts)])
+    cat = lambda k: np.concatenate([getattr(p, k) for p in parts])
+    frame = DayFrame(lab, None, cat("time"), cat("open"), cat("high"), cat("low"), cat("close"), cat("volume"))
+    code_index = {c: i for i, c in enumerate(panel["codes"])}
+    out = {}
+    for name, p in zip(FRAME_RANK_NAMES, (0.6, 0.7, 0.8, 0.9, 0.95)):
+        v, st = np.zeros((D, S)), np.zeros((D, S), np.uint8)
+        for key, x in _doc_pdf(frame, p).items():
+            code, d = str(key).rsplit("|", 1)
+            d, si = int(d), code_index[code]
+            st[d, si] = NULLV if x is None else VALUE
+            v[d, si] = 0.0 if x is None else x
+        out[name] = (v, st)
+    return out
 
 
 def oracle_frame_xday(panel):
@@ -956,9 +982,12 @@ def oracle_frame_xday(panel):
     order): ``.over('code')`` spans the whole frame instead of one day.
       liq_amihud_1min CM:739-760, corr_prvr CM:855-874, trade_bottom20retRatio
       CM:1211-1223, trade_bottom50retRatio CM:1232-1247.
+    Also doc_pdf60..95, whose `.rank()` spans every date of the frame
+    (:func:`oracle_frame_doc_pdf`).
     Returns {name: (val [D][S], state [D][S])}."""
     D, S = panel["present"].shape[:2]
     out = {n: (np.zeros((D, S)), np.zeros((D, S), np.uint8)) for n in FRAME_XDAY_NAMES}
+    out.update(oracle_frame_doc_pdf(panel))
 
     def put(name, d, s, x):
         v, st = out[name]

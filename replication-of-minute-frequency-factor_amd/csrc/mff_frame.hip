@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void k_frame_xday(FrameArgs a) {
     const size_t sd = (size_t)d * a.S + s;
     const uint32_t* mk = a.valid + sd * 8;
     const float* C = a.close + sd * NBAR;
-    const float* O = a.open + sd * NBAR;
+    const bool tail = a.row_b20 >= 0 || a.row_b50 >= 0;  // open may be NULL otherwise
     const float* V = a.volume + sd * NBAR;
     double amh = 0.0;
     double P[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
@@ -95,8 +95,8 @@ __global__ __launch_bounds__(256) void k_frame_xday(FrameArgs a) {
           vzp = v;
           hz = true;
         }
-        if (m >= 190) {
-          const double r = fdiv(c, (double)O[m]) - 1.0;
+        if (tail && m >= 190) {
+          const double r = fdiv(c, (double)a.open[sd * NBAR + m]) - 1.0;
           t50 = true;
           tot50 += v;
           r50 += v * r;

@@ -269,6 +269,8 @@ struct PdfArgs {
   int rows[5];
   int S, D, d0, nd, M, Z, Mz;
   int packed;  // count: u32 packed counters (PDF_LB), u64 recount on overflow
+  int frame;   // count: ONE sorted list [M] for every day (a multi-date frame ranked
+               // frame-wide, CM:1015-1017); each day's words are atomically added to counts[M]
 };
 
 // One (day, slice [P0, P1)) count.  C32: packed u32 counters (n_less part low, n_eq part
@@ -281,7 +283,8 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
   constexpr uint64_t K1 = 0xBFF0000000000000ull;  // ord64(1.0)
   typedef typename std::conditional<C32, uint32_t, uint64_t>::type CT;
   const int S = a.S;
-  const uint64_t* Q = a.q_sorted + (size_t)dd * a.M;
+  const int qd = a.frame ? 0 : dd;  // the sorted list this day's keys are counted against
+  const uint64_t* Q = a.q_sorted + (size_t)qd * a.M;
   const int nq = P1 - P0;
   uint64_t* L = reinterpret_cast<uint64_t*>(smem);  // [mz + 1 + PDF_PAD]
   CT* C = reinterpret_cast<CT*>(L + mz + 1 + PDF_PAD);  // [mz]
@@ -444,7 +447,7 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
     // or NaN are never looked up); one word per position, 2 n_less + n_eq: the average
     // rank n_less + (n_eq + 1) / 2 = (2 n_less + n_eq + 1) / 2 is linear in it, so the
     // ranks' words simply add up
-    uint32_t* out = a.counts + (size_t)dd * a.M + P0;
+    uint32_t* out = a.counts + (size_t)qd * a.M + P0;
     for (int i = threadIdx.x; i < nq; i += blockDim.x) {
       const uint64_t x = Q[P0 + i];
       uint32_t c2 = 0u;
@@ -453,7 +456,13 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
         sl.range(x, lo, hi);
         c2 = twice_rank(lower_bound_u64(L + 1, lo, hi, x));
       }
-      out[i] = c2;
+      // frame: every day adds its keys' words to the one list's counters (the words
+      // are linear in the rank, so the days' sum is the frame-wide 2 n_less + n_eq)
+      if (a.frame) {
+        if (c2 != 0u) atomicAdd(out + i, c2);
+      } else {
+        out[i] = c2;
+      }
     }
   }
   __syncthreads();  // the LDS is reused by the next slice count of this workgroup
@@ -640,6 +649,24 @@ int mff_pdf_count(const void* pdf_levels, int S_loc, int D, int d0, int nd,
   pdf_levels_args(a, pdf_levels, S_loc, D);
   a.counts = counts;
   a.S = S_loc; a.D = D; a.d0 = d0; a.nd = nd;
+  return pdf_launch(a, q_sorted, M, as_stream(stream), 0);
+}
+
+int mff_pdf_count_frame(const void* pdf_levels, int S, int D, const uint64_t* q_sorted, int M,
+                        uint32_t* counts, void* stream) {
+  clear_error();
+  MFF_REQUIRE(S > 0 && D > 0 && M > 0, "mff_pdf_count_frame: bad sizes S=%d D=%d M=%d", S, D, M);
+  MFF_REQUIRE(M <= PDF_MAXM, "mff_pdf_count_frame: %d queries exceed %d", M, PDF_MAXM);
+  // 2 n_less + n_eq over every key of the frame (<= 240 per stock-day) must fit u32
+  MFF_REQUIRE((long long)NBAR * S * D < (1ll << 31), "mff_pdf_count_frame: frame of %d x %d stock-days too large",
+              D, S);
+  MFF_REQUIRE(pdf_levels && q_sorted && counts, "mff_pdf_count_frame: NULL buffer");
+  PdfArgs a;
+  memset(&a, 0, sizeof(a));
+  pdf_levels_args(a, pdf_levels, S, D);
+  a.counts = counts;
+  a.S = S; a.D = D; a.d0 = 0; a.nd = D;
+  a.frame = 1;
   return pdf_launch(a, q_sorted, M, as_stream(stream), 0);
 }
 

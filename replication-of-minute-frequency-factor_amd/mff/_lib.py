@@ -34,6 +34,7 @@ SIGNATURES = {
     "mff_pdf_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "mff_pdf_sort": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, P]),
     "mff_pdf_count": (c_int, [P, c_int, c_int, c_int, c_int, P, c_int, P, P, P]),
+    "mff_pdf_count_frame": (c_int, [P, c_int, c_int, P, c_int, P, P]),
     "mff_pdf_finalize": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, IP, P, P, P]),
     "mff_pdf_rank_local": (c_int, [P, P, c_int, c_int, c_int, c_int, P, c_int, IP, P, P, P]),
     "mff_stage1_frame": (c_int, [P, P, P, P, c_int, c_int, IP, c_int, P, P, P]),

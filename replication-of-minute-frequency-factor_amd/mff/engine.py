@@ -44,6 +44,9 @@ class DevicePanel:
     mask: torch.Tensor
     codes: List[str] = field(default_factory=list)
     dates: List = field(default_factory=list)
+    # ingest with skip_bad: {input table index: reason} of the tables dropped (their days
+    # hold no bars)
+    dropped: dict = field(default_factory=dict)
 
     @property
     def D(self) -> int:
@@ -82,8 +85,13 @@ def validate_host_panel(panel) -> None:
 
 
 def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, comm=None,
-                    pdf_day_batch: Optional[int] = None, events=None):
+                    pdf_day_batch: Optional[int] = None, events=None, frame: bool = False):
     """Stage 1 for the requested factors (default: all 58, reference order).
+
+    ``frame``: the panel's D days are ONE reference frame (a cal_* handed a multi-date
+    frame): doc_pdf60..95 rank over every row of every date (CM:1015-1017, `.rank()`
+    outside `.over`) instead of per day (:func:`pdf_ranks_frame`).  Default: per day, the
+    driver's one-call-per-day-file semantics (MF:22).
 
     ``events``: optional (start, end) torch.cuda.Event pair recorded on the launch stream
     around the whole stage-1 pass: every stage-1 launch and the doc_pdf rank phases
@@ -106,9 +114,13 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             _lib.ptr(panel.mask), S, D, _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
             _lib.ptr(pdfq), _lib.ptr(levels), _lib.ptr(ws), main.cuda_stream]
     rows = [ids.index(i) if i in ids else -1 for i in catalog.PDF_IDS]
+    frame_pdf = frame and need_pdf and D > 1
+    if frame_pdf and comm is not None:
+        raise ValueError("frame-wide doc_pdf ranks of a multi-date frame are single-GPU; "
+                         "shard day files (per-day semantics) instead")
     if events is not None:
         events[0].record(main)
-    if need_pdf and PDF_OVERLAP:
+    if need_pdf and PDF_OVERLAP and not frame_pdf:
         # part 1 (sorted families: doc_pdf levels + queries), then the doc_pdf rank on a
         # side stream while part 2 (the serial families) runs on the launch stream
         hl = _side_stream(dev, 1) if HL_STREAM else None
@@ -150,7 +162,9 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             events[1].record(main)
         return val, state, ids
     _lib.check(lib.mff_stage1(*args), "mff_stage1")
-    if need_pdf:
+    if frame_pdf:
+        pdf_ranks_frame(panel, pdfq, levels, rows, val, state)
+    elif need_pdf:
         pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
     if events is not None:
         events[1].record(main)
@@ -223,6 +237,32 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
                                           _lib.ptr(q_sorted), M,
                                           _lib.int_array(rows), _lib.ptr(val), _lib.ptr(state), st),
                    "mff_pdf_rank_local")
+
+
+def pdf_ranks_frame(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows: List[int], val,
+                    state):
+    """doc_pdf ranks of a multi-date frame taken as ONE reference frame: `.rank()`
+    (CM:1015-1017) is outside any `.over`, so a frame holding D dates ranks every row of
+    every date.  The D days' 5*S queries are sorted as one list ([5][D][S] viewed as one
+    day of D*S stocks), every day's level keys are counted against it (the words
+    2 n_less + n_eq add up over days, mff_pdf_count_frame) and the ranks are written
+    through the same one-day view of the output rows."""
+    lib = _lib.load()
+    D, S = panel.D, panel.S
+    dev = panel.device
+    st = _stream(dev)
+    DS = D * S
+    M = 5 * DS
+    ws = torch.empty(lib.mff_pdf_workspace_bytes(DS, 1, 1), dtype=torch.uint8, device=dev)
+    q_sorted = torch.empty((1, M), dtype=torch.int64, device=dev)
+    _lib.check(lib.mff_pdf_sort(_lib.ptr(pdfq), 1, DS, 1, 0, 1, _lib.ptr(q_sorted), _lib.ptr(ws), st),
+               "mff_pdf_sort(frame)")
+    counts = torch.zeros((1, M), dtype=torch.int32, device=dev)
+    _lib.check(lib.mff_pdf_count_frame(_lib.ptr(levels), S, D, _lib.ptr(q_sorted), M, _lib.ptr(counts), st),
+               "mff_pdf_count_frame")
+    _lib.check(lib.mff_pdf_finalize(_lib.ptr(pdfq), _lib.ptr(q_sorted), _lib.ptr(counts), DS, 1, 0, 1, M,
+                                    _lib.int_array(rows), _lib.ptr(val), _lib.ptr(state), st),
+               "mff_pdf_finalize(frame)")
 
 
 class PdfKernels:
@@ -364,7 +404,7 @@ def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None):
     ov = torch.empty_like(val)
     os_ = torch.empty_like(state)
     R = 1 if comm is None else comm.world_size
-    if kind == "z" and R == 1 and S <= lib.mff_xs_zscore_local_max_stocks():
+    if kind == "z" and comm is None and S <= lib.mff_xs_zscore_local_max_stocks():
         _lib.check(lib.mff_xs_zscore_local(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(ov),
                                            _lib.ptr(os_), st), "mff_xs_zscore_local")
     elif kind == "z":

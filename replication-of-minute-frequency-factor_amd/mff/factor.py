@@ -10,9 +10,12 @@ environment variables (MFF_PV_PATH, MFF_EXPOSURE_DIR, MFF_KLINE_DIR) or argument
 override.
 
 Device work:
-  cal_exposure_by_min_data(cal_xxx)  -> stage-1 kernel over day-file batches
+  cal_exposure_by_min_data(cal_xxx)  -> ingest + stage-1 kernels over day-file batches
   cal_final_exposure(N, m, 'days')   -> stage-2 rolling kernel
-The evaluation methods (coverage, ic_test, group_test) run on the host.
+  cal_final_exposure(f, m, 'calendar') -> calendar resampling kernel
+  ic_test                            -> future-return, IC pair / rank / moment kernels
+  group_test                         -> qcut / period / reduce kernels
+coverage is a host group-by count.
 """
 from __future__ import annotations
 
@@ -302,14 +305,17 @@ class MinFreqFactor(Factor):
 
     def cal_exposure_by_min_data(self, calculate_method, path: str = None, n_jobs: int = None,
                                  folder_path: Optional[str] = None, batch_days: int = 64,
-                                 device=None):
+                                 device=None, strict: bool = False):
         """MF:50-112: compute the exposure from per-day minute files, updating an
         existing exposure incrementally (only dates after its max date).
 
         `calculate_method` is one of the mff ``cal_*`` functions (or a factor name): the
         day files are read in batches of `batch_days`, turned into one dense panel and
-        run through the stage-1 kernel.  Any other callable runs per file on the host
-        exactly as the reference does (joblib process pool, errors print and skip)."""
+        run through the stage-1 kernel.  A day file that cannot be read or breaks the
+        input contract is reported with the reference's message and dropped, the other
+        days of its batch unaffected (MF:18-25, 95); ``strict=True`` raises instead,
+        naming the file.  Any other callable runs per file on the host exactly as the
+        reference does (joblib process pool, errors print and skip)."""
         pd = _pd()
         factor_exposure = self._read_exposure(
             factor_name=self.factor_name,
@@ -329,7 +335,7 @@ class MinFreqFactor(Factor):
         if len(index) > 0:
             if name is not None and name in catalog.ID:
                 valid = self._gpu_batches(index["file_name"].tolist(), folder_path, name,
-                                          batch_days, device)
+                                          batch_days, device, strict)
             else:
                 from joblib import Parallel, delayed
 
@@ -345,23 +351,35 @@ class MinFreqFactor(Factor):
         else:
             self.factor_exposure = factor_exposure
 
-    def _gpu_batches(self, files, folder_path, name, batch_days, device):
-        import pyarrow as pa
-
+    def _gpu_batches(self, files, folder_path, name, batch_days, device, strict=False):
         from .factors import compute_long
+        from .ingest import NoTables
 
         out = []
         for b0 in range(0, len(files), batch_days):
-            tables = []
+            tables, names = [], []
             for f in files[b0:b0 + batch_days]:
                 try:
                     tables.append(self._read_day_file(os.path.join(folder_path, f)))
+                    names.append(f)
                 except Exception as e:  # MF:23-25: report and skip the day
+                    if strict:
+                        raise ValueError(f"{f}: {e}") from e
                     print(f"处理文件 {f} 时出错: {str(e)}")
             if not tables:
                 continue
-            res = compute_long(tables, [name], device, per_day=True)  # one reference call per file
-            out.append(res[name])
+            errors = {}
+            # one reference call per file (per-day semantics); a bad file drops its day only
+            try:
+                res = compute_long(tables, [name], device, per_day=True, skip_bad=True, errors=errors)
+            except NoTables as e:
+                errors, res = e.dropped, None
+            for k, msg in errors.items():
+                if strict:
+                    raise ValueError(f"{names[k]}: {msg}")
+                print(f"处理文件 {names[k]} 时出错: {msg}")
+            if res is not None:
+                out.append(res[name])
         return out
 
     def cal_final_exposure(self, frequency, method: str, mode: str = "calendar", pool="full"):

@@ -29,9 +29,13 @@ def _device(device=None):
 # factors whose reference windows over('code') cross days on a multi-day frame
 # (mff_stage1_frame, csrc/mff_frame.hip)
 FRAME_XDAY = ("liq_amihud_1min", "corr_prvr", "trade_bottom20retRatio", "trade_bottom50retRatio")
+# factors whose `.rank()` runs over the whole frame (CM:1015-1017): on a multi-day frame
+# every row of every date (engine.pdf_ranks_frame)
+FRAME_RANK = ("doc_pdf60", "doc_pdf70", "doc_pdf80", "doc_pdf90", "doc_pdf95")
 
 
-def compute_long(df, names: Sequence[str] | None = None, device=None, per_day: bool | None = None) -> Dict:
+def compute_long(df, names: Sequence[str] | None = None, device=None, per_day: bool | None = None,
+                 skip_bad: bool = False, errors: Dict | None = None) -> Dict:
     """Long frame(s) -> {name: long result frame} for the requested factors, computed in
     one stage-1 pass.
 
@@ -40,9 +44,15 @@ def compute_long(df, names: Sequence[str] | None = None, device=None, per_day: b
     reference frame: the four functions whose windows run over('code') only
     (liq_amihud_1min CM:746, corr_prvr CM:862-867, trade_bottom20/50retRatio CM:1216,
     1238-1240) then reach across days exactly as the reference does on that frame (rows of
-    a code in (date, time) order).  A list of tables is a list of day files, each its own
+    a code in (date, time) order), and doc_pdf60..95 rank every row of every date
+    (`.rank()` outside `.over`, CM:1015-1017).  A list of tables is a list of day files, each its own
     reference call (MinuteFrequentFactorCICC.py:22): per-day semantics.  ``per_day``
-    overrides the choice."""
+    overrides the choice.
+
+    A table that breaks the input contract (include/mff.h) raises ValueError, unless
+    ``skip_bad``: then its days are dropped (no rows), as the reference driver drops a
+    day file whose call raised (MinuteFrequentFactorCICC.py:18-25, 95), and ``errors``
+    (a dict, if given) receives {table index: reason}."""
     import torch
 
     from . import _lib, engine
@@ -53,8 +63,10 @@ def compute_long(df, names: Sequence[str] | None = None, device=None, per_day: b
 
     if per_day is None:
         per_day = isinstance(df, (list, tuple))
-    dp = ingest.to_device_panel(df, _device(device))  # GPU long -> dense (mff_ingest_rows)
-    val, state, ids = engine.compute_factors(dp, names)
+    dp = ingest.to_device_panel(df, _device(device), skip_bad=skip_bad)  # GPU long -> dense (mff_ingest_rows)
+    if errors is not None:
+        errors.update(dp.dropped)
+    val, state, ids = engine.compute_factors(dp, names, frame=not per_day)
     if not per_day and dp.D > 1 and any(n in FRAME_XDAY for n in names):
         lib = _lib.load()
         b = dp.bars

@@ -92,8 +92,14 @@ def _numeric(col, dtype):
 
 
 def _volume(col):
+    """A null volume is 0 shares: the reference's volume sums skip nulls and
+    liq_amihud_1min fills them with 0 (CM:743-744)."""
+    import pyarrow.compute as pc
+
     col = _one(col)
-    arr = _numeric(col, None) if col.null_count else col.to_numpy(zero_copy_only=False)
+    if col.null_count:
+        col = pc.fill_null(col, 0)
+    arr = col.to_numpy(zero_copy_only=False)
     arr = np.ascontiguousarray(arr)
     if arr.dtype not in _VOLUME_KIND:
         arr = arr.astype(np.float64)
@@ -191,7 +197,7 @@ class PanelIngest:
     :class:`mff.engine.DevicePanel`."""
 
     def __init__(self, codes: Sequence[str], day_numbers: Sequence[int], device,
-                 slots: int = 2):
+                 slots: int = 2, tables: int = 1):
         self.lib = _lib.load()
         self.codes = list(codes)
         self.day_numbers = [int(x) for x in day_numbers]
@@ -202,7 +208,10 @@ class PanelIngest:
         self.S, self.D = S, D
         self.bars = torch.empty((5, D, S, 240), dtype=torch.float32, device=self.dev)
         self.mask = torch.zeros((D, S, 8), dtype=torch.int32, device=self.dev)
-        self.err = torch.zeros(5, dtype=torch.int32, device=self.dev)
+        # contract-violation counters per pushed table ([tables][5]; push k uses row k, a
+        # push beyond `tables` shares the last row), so a caller can drop a bad day file
+        self.err = torch.zeros((max(1, tables), 5), dtype=torch.int32, device=self.dev)
+        self.table_days: List[np.ndarray] = []  # day indices each push touched
         self.stream = torch.cuda.Stream(self.dev)
         self.stream.wait_stream(torch.cuda.current_stream(self.dev))  # zero fills first
         self.slots = [None] * slots  # (pinned, device, event)
@@ -232,6 +241,9 @@ class PanelIngest:
         """Stage and launch one table already encoded by :func:`encode`."""
         stock, day, time, px, vol, kind = enc
         n = int(stock.size)
+        k = min(len(self.table_days), self.err.shape[0] - 1)
+        lo, hi = (int(day.min()), int(day.max())) if n else (0, -1)
+        self.table_days.append(np.arange(lo, hi + 1) if lo == hi or n == 0 else np.unique(day))
         if n == 0:
             return
         cols = [stock, day, time] + px + [vol]
@@ -250,45 +262,122 @@ class PanelIngest:
             b = self.bars
             _lib.check(self.lib.mff_ingest_rows(
                 p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], kind, n, self.S, self.D,
-                b.data_ptr(), self.mask.data_ptr(), self.err.data_ptr(),
+                b.data_ptr(), self.mask.data_ptr(), self.err[k].data_ptr(),
                 self.stream.cuda_stream), "mff_ingest_rows")
         self.rows += n
 
-    def finish(self):
+    def skip_table(self, k: int) -> None:
+        """Record a table that could not be pushed (its encode raised): nothing staged."""
+        self.table_days.append(np.zeros(0, dtype=np.int64))
+
+    def finish(self, skip_bad: bool = False):
+        """Check the per-table error counters and return the DevicePanel.
+
+        A table breaking the input contract raises ValueError (naming the table's index)
+        unless ``skip_bad``: then every day the table touched is dropped from the panel
+        (its presence bits cleared: every stock-day ABSENT, no rows, as when the
+        reference's per-file call fails, MinuteFrequentFactorCICC.py:18-25, 95) and the
+        reasons are returned in ``panel.dropped`` {table index: message}."""
         from .engine import DevicePanel
 
         torch.cuda.current_stream(self.dev).wait_stream(self.stream)
         err = self.err.cpu().numpy()  # synchronises the caller's stream
-        bad = [f"{ERRORS[i]} ({int(err[i])} rows)" for i in range(5) if err[i]]
-        if bad:
-            raise ValueError("; ".join(bad))
+        dropped = {}
+        for k in range(err.shape[0]):
+            bad = [f"{ERRORS[i]} ({int(err[k, i])} rows)" for i in range(5) if err[k, i]]
+            if bad:
+                dropped[k] = "; ".join(bad)
+        if dropped and not skip_bad:
+            if err.shape[0] == 1:
+                raise ValueError(dropped[0])
+            raise ValueError("; ".join(f"table {k}: {m}" for k, m in sorted(dropped.items())))
+        for k in dropped:
+            days = self.table_days[k] if k < len(self.table_days) else np.zeros(0, np.int64)
+            if days.size:
+                self.mask[torch.as_tensor(days, device=self.dev)] = 0
         dates = [_EPOCH + _dt.timedelta(days=x) for x in self.day_numbers]
-        return DevicePanel(self.bars, self.mask, self.codes, dates)
+        dp = DevicePanel(self.bars, self.mask, self.codes, dates)
+        dp.dropped = dropped
+        return dp
 
 
-def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None):
+class NoTables(ValueError):
+    """Every table was dropped (skip_bad): ``dropped`` {table index: reason}."""
+
+    def __init__(self, dropped):
+        super().__init__(f"no readable table: {dropped}")
+        self.dropped = dropped
+
+
+def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None, skip_bad: bool = False):
     """One or more long tables -> DevicePanel (universes: the tables' sorted codes and
-    dates, or the given code universe)."""
+    dates, or the given code universe).
+
+    ``skip_bad`` (the reference driver's per-file error semantics,
+    MinuteFrequentFactorCICC.py:18-25, 95): a table that cannot be read as a day frame or
+    breaks the input contract (include/mff.h: bars on the 240-minute grid, no duplicate
+    bars, prices finite > 0, volume integral in range) is dropped with every day it
+    touches -- its stock-days come out ABSENT -- and ``panel.dropped`` maps the table's
+    index in ``tables`` to the reason.  Otherwise the first such table raises ValueError."""
     from concurrent.futures import ThreadPoolExecutor
 
-    tabs = [_table(t) for t in (tables if isinstance(tables, (list, tuple)) else [tables])]
+    raw = list(tables) if isinstance(tables, (list, tuple)) else [tables]
+    dropped = {}
     # pyarrow / numpy kernels release the GIL: tables are encoded by a few host threads
     # (in order, a bounded window ahead) while earlier ones are copied and scattered
-    workers = max(1, min(4, len(tabs), os.cpu_count() or 1))
+    workers = max(1, min(4, len(raw), os.cpu_count() or 1))
+
+    def prep(t):
+        t = _dict_codes(_table(t))
+        for k in ("code", "date"):
+            if k not in t.column_names:
+                raise ValueError(f"missing column {k!r}")
+        return t, _code_values(t.column("code")), np.unique(_date32(t.column("date"))).tolist()
+
     with ThreadPoolExecutor(workers) as pool:
-        tabs = list(pool.map(_dict_codes, tabs))
-        ucodes, udays = universes(tabs)
-        if codes is not None:
-            ucodes = list(codes)
-        ing = PanelIngest(ucodes, udays, device)
-        futs = [pool.submit(encode, t, ing.codes, ing.day_numbers) for t in tabs[:workers]]
-        for i in range(len(tabs)):
-            enc = futs[i].result()
-            if i + workers < len(tabs):
-                futs.append(pool.submit(encode, tabs[i + workers], ing.codes, ing.day_numbers))
-            ing.push_encoded(enc)
-            futs[i] = None
-    return ing.finish()
+        futs = [pool.submit(prep, t) for t in raw]
+        keep, tabs, cset, dset = [], [], set(), set()
+        for i, f in enumerate(futs):
+            try:
+                t, cs, ds = f.result()
+            except Exception as e:  # noqa: BLE001 -- reported like the reference (MF:23-25)
+                if not skip_bad:
+                    raise
+                dropped[i] = str(e)
+                continue
+            keep.append(i)
+            tabs.append(t)
+            cset.update(cs)
+            dset.update(ds)
+        if not tabs:
+            raise NoTables(dropped)
+        ucodes = sorted(cset) if codes is None else list(codes)
+        ing = PanelIngest(ucodes, sorted(dset), device, tables=len(tabs))
+
+        def enc_safe(t):
+            try:
+                return encode(t, ing.codes, ing.day_numbers), None
+            except Exception as e:  # noqa: BLE001
+                if not skip_bad:
+                    raise
+                return None, str(e)
+
+        futs = [pool.submit(enc_safe, t) for t in tabs[:workers]]
+        for j in range(len(tabs)):
+            enc, msg = futs[j].result()
+            if j + workers < len(tabs):
+                futs.append(pool.submit(enc_safe, tabs[j + workers]))
+            if enc is None:
+                dropped[keep[j]] = msg
+                ing.skip_table(j)
+            else:
+                ing.push_encoded(enc)
+            futs[j] = None
+    dp = ing.finish(skip_bad=skip_bad)
+    for j, msg in dp.dropped.items():
+        dropped[keep[j]] = msg
+    dp.dropped = dict(sorted(dropped.items()))
+    return dp
 
 
 __all__: List[str] = ["PanelIngest", "to_device_panel", "universes", "encode"]

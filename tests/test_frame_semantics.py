@@ -54,3 +54,30 @@ def test_frame_oracle_cross_day_terms_by_hand():
     pr_v, pr_s = fx["corr_prvr"]
     assert pr_s[0, 0] == O.VALUE and np.isnan(pr_v[0, 0])  # one pair on day 0: NaN (S3)
     assert pr_s[1, 0] == O.VALUE and abs(pr_v[1, 0] - 1.0) < 1e-12  # two pairs, both falling
+
+
+def test_frame_doc_pdf_oracle_equals_per_day_on_one_day():
+    """doc_pdf60..95 of a one-day frame: the frame-wide rank is the day's rank."""
+    panel = synth.make_panel(25, 1, config=32, ragged=True)
+    ov, os_ = O.oracle_stage1(panel, O.FRAME_RANK_NAMES)
+    fx = O.oracle_frame_doc_pdf(panel)
+    for i, nm in enumerate(O.FRAME_RANK_NAMES):
+        v, s = fx[nm]
+        assert (s == os_[i]).all(), nm
+        assert (v == ov[i]).all(), nm
+
+
+def test_frame_doc_pdf_ranks_every_date_by_hand():
+    """CM:1015-1017 on a 2-day frame: `.rank()` is outside `.over`, so the four rows of
+    both dates are ranked together.  Keys c_last/c: day 0 (10.5/10, 1.0), day 1
+    (10/11, 1.0) -> frame ranks (4, 2.5), (1, 2.5); per day they would be (2, 1), (1, 2)."""
+    fx = O.oracle_frame_xday(_two_day_panel())
+    # day 0: levels rank 2.5 (share 2/3), rank 4 (share 1/3), cum-summed by ascending rank
+    assert fx["doc_pdf60"][0][0, 0] == 2.5
+    for nm in ("doc_pdf70", "doc_pdf80", "doc_pdf90", "doc_pdf95"):
+        assert fx[nm][0][0, 0] == 4.0, nm
+    # day 1: rank 1 (share 3/7), rank 2.5 (share 4/7): every threshold at rank 2.5
+    for nm in O.FRAME_RANK_NAMES:
+        assert fx[nm][0][1, 0] == 2.5 and fx[nm][1][1, 0] == O.VALUE, nm
+    per_day = O.oracle_stage1(_two_day_panel(), ["doc_pdf60"])[0][0][:, 0]
+    assert per_day.tolist() == [1.0, 2.0]

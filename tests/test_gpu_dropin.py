@@ -41,7 +41,9 @@ def test_cal_functions_on_long_frames(dev, panel_and_oracle):
     panel, (ov, os_) = panel_and_oracle
     df = long_frame(panel)
     res = CM.compute_long(df)
-    xday = O.oracle_frame_xday(panel)  # one 3-day frame: over('code') spans the dates
+    # one 3-day frame: over('code') spans the dates, and doc_pdf's .rank() (CM:1015-1017)
+    # ranks every row of every date
+    xday = O.oracle_frame_xday(panel)
     bad = []
     for i, nm in enumerate(catalog.NAMES):
         out = res[nm]
@@ -61,6 +63,13 @@ def test_cal_functions_on_long_frames(dev, panel_and_oracle):
     v, s = _dense(res["liq_amihud_1min"], "liq_amihud_1min", panel)
     i = catalog.ID["liq_amihud_1min"]
     assert (np.abs(v[1:] - ov[i][1:]) > 0).any()
+    # doc_pdf ranks of the frame span all three dates: larger than any one day's ranks
+    for nm in O.FRAME_RANK_NAMES:
+        v, s = _dense(res[nm], nm, panel)
+        i = catalog.ID[nm]
+        ok = (s == O.VALUE) & (os_[i] == O.VALUE)
+        assert ok.any() and (v[ok] != ov[i][ok]).any(), nm
+        assert v[ok].max() > ov[i][ok].max(), nm
     one = CM.cal_mmt_pm(long_frame(panel, 0))  # single day, single factor
     v, s = _dense(one, "mmt_pm", {"codes": panel["codes"], "dates": panel["dates"][:1]})
     assert not compare(v, s, ov[0][:1], os_[0][:1], "mmt_pm")
