@@ -140,7 +140,9 @@ def ingest_extras(panel, days: int, host_days: int):
     day = (idx // (240 * S)).to(torch.int32)
     clock = torch.where(m < 120, 570 + m, 660 + m)
     tm = (clock // 60) * 10000000 + (clock % 60) * 100000
-    cols = [panel.bars[f, :D].reshape(-1)[idx].double() for f in range(5)]
+    cols = [panel.bars[f, :D].reshape(-1)[idx].double() for f in range(4)]
+    cols.append(panel.bars[4, :D].reshape(-1)[idx].view(torch.int32).to(torch.int64).bitwise_and(0xFFFFFFFF)
+                .double())  # u32 shares
     bars = torch.empty((5, D, S, 240), dtype=torch.float32, device=dev)
     mask = torch.zeros((D, S, 8), dtype=torch.int32, device=dev)
     err = torch.zeros(5, dtype=torch.int32, device=dev)
@@ -183,7 +185,8 @@ def ingest_extras(panel, days: int, host_days: int):
                               + (np.where(m_idx < 120, 570 + m_idx, 660 + m_idx) % 60) * 100000)
                              .astype("int64")),
             **{k: pa.array(planes[f, d][s_idx, m_idx].astype("float64"))
-               for f, k in enumerate(("open", "high", "low", "close", "volume"))}}))
+               for f, k in enumerate(("open", "high", "low", "close"))},
+            "volume": pa.array(planes[4, d].view("uint32")[s_idx, m_idx].astype("int64"))}))
     rows = sum(t.num_rows for t in tabs)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -194,6 +197,81 @@ def ingest_extras(panel, days: int, host_days: int):
                 round(hd * S / dt), "ingest_host_path_sample": f"{hd} day tables x {S} stocks, {rows} rows"})
     del dp
     return out
+
+
+def e2e_extras(panel, days: int):
+    """The drop-in path end to end ("End-to-end time including host->device
+    is reported separately"): `days` day files of the bench panel written as the
+    reference's parquet day files (code, date, time, OHLCV; MF:68-78), then
+      * MinFreqFactor(f).cal_exposure_by_min_data(cal_f) for one factor from cold
+        (parquet read + host encode + H2D + ingest kernel + stage-1 pass + long frames);
+      * the other 57 factors one after another, as a notebook would (the batch result
+        cache serves them: no re-read, no re-ingest);
+      * MinFreqFactor.cal_exposures_by_min_data() for all 58 from cold.
+    Rates are stock-days of the files per second of wall time, host work included."""
+    import shutil
+    import tempfile
+
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    import torch
+    from mff import catalog, factor, factors, synth
+
+    S = panel.S
+    nd = min(days, panel.D)
+    tmp = tempfile.mkdtemp(prefix="mff_e2e_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        folder = os.path.join(tmp, "kl")
+        os.makedirs(folder)
+        codes = np.array([f"{s:06d}.SZ" for s in range(S)])
+        pres = synth.unpack_mask(panel.mask[:nd].cpu().numpy().view("uint32"))
+        planes = panel.bars[:, :nd].cpu().numpy()
+        rows = 0
+        for d in range(nd):
+            s_idx, m_idx = pres[d].nonzero()
+            clock = np.where(m_idx < 120, 570 + m_idx, 660 + m_idx)
+            date = np.datetime64("2020-01-02") + np.timedelta64(d, "D")
+            t = pa.table({"code": pa.array(codes[s_idx]), "date": pa.array(np.full(s_idx.size, date)),
+                          "time": pa.array(((clock // 60) * 10000000 + (clock % 60) * 100000).astype("int64")),
+                          **{k: pa.array(planes[f, d][s_idx, m_idx].astype("float64"))
+                             for f, k in enumerate(("open", "high", "low", "close"))},
+                          "volume": pa.array(planes[4, d].view("uint32")[s_idx, m_idx].astype("int64"))})
+            pq.write_table(t, os.path.join(folder, f"{(date + 0).astype(object):%Y%m%d}_kline.parquet"))
+            rows += t.num_rows
+        del pres, planes
+        exp = os.path.join(tmp, "exp")
+        os.makedirs(exp)
+        MinFreqFactor = factor.MinFreqFactor
+        out = {"e2e_sample": f"{nd} parquet day files x {S} stocks ({rows} rows), batch_days 64"}
+        factor.clear_result_cache()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        f = MinFreqFactor("vol_return1min")
+        f.cal_exposure_by_min_data(factors.cal_vol_return1min, path=exp, folder_path=folder)
+        t1 = time.perf_counter()
+        for nm in catalog.NAMES:
+            if nm != "vol_return1min":
+                g = MinFreqFactor(nm)
+                g.cal_exposure_by_min_data(getattr(factors, "cal_" + nm), path=exp, folder_path=folder)
+        t2 = time.perf_counter()
+        factor.clear_result_cache()
+        t3 = time.perf_counter()
+        allf = MinFreqFactor.cal_exposures_by_min_data(path=exp, folder_path=folder)
+        t4 = time.perf_counter()
+        factor.clear_result_cache()
+        assert len(allf) == 58 and len(f.factor_exposure) > 0
+        sd = nd * S
+        out.update({
+            "e2e_first_factor_s": round(t1 - t0, 3),
+            "e2e_first_factor_stock_days_per_s": round(sd / (t1 - t0)),
+            "e2e_58_sequential_s": round(t2 - t0, 3),
+            "e2e_58_sequential_stock_days_per_s": round(sd / (t2 - t0)),
+            "e2e_58_one_call_s": round(t4 - t3, 3),
+            "e2e_58_one_call_stock_days_per_s": round(sd / (t4 - t3)),
+        })
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def main():
@@ -209,6 +287,7 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--ingest-days", type=int, default=20)
     ap.add_argument("--ingest-host-days", type=int, default=4)
+    ap.add_argument("--e2e-days", type=int, default=8)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -298,6 +377,8 @@ def main():
         del val, state
         if rank == 0:
             extras.update(ingest_extras(panel, args.ingest_days, args.ingest_host_days))
+            if args.e2e_days > 0:
+                extras.update(e2e_extras(panel, args.e2e_days))
         # c5: the same panel made ragged in place (suspension runs, missing bars, gap and
         # flat zero-volume stock-days), one stage-1 pass timed like the headline
         g = torch.Generator(device=dev)

@@ -16,10 +16,11 @@
  *    caller may capture them into a hipGraph.
  *  - Return 0 on success, negative on error; mff_last_error() gives a thread-local
  *    message.  No C++ exception crosses this ABI.
- *  - Panel layout: field planes open/high/low/close/volume, each float32 [D][S][240]
- *    (day, stock, minute 0..239 = 09:30..11:29, 13:00..14:59); presence mask
- *    uint32 [D][S][8], bit (m % 32) of word (m / 32) set when bar m exists.
- *    Volume must be integral, 0 <= v <= 2^24 (fp32-exact), prices finite > 0.
+ *  - Panel layout: field planes open/high/low/close float32 and volume uint32 (shares),
+ *    each [D][S][240] (day, stock, minute 0..239 = 09:30..11:29, 13:00..14:59); presence
+ *    mask uint32 [D][S][8], bit (m % 32) of word (m / 32) set when bar m exists.
+ *    Prices finite > 0; volume 0 <= v <= MFF_VOLUME_MAX (the all-ones word is the sorts'
+ *    absent-bar key).  Values of absent bars are don't-care.
  *  - Output layout: val float64 [rows][D][S], state uint8 [rows][D][S] with
  *    0 = ABSENT (the reference emits no row), 1 = NULL (polars null),
  *    2 = VALUE (may be NaN / +-inf).
@@ -66,7 +67,8 @@ const char* mff_factor_name(int id);
 #define MFF_INGEST_ERR_TIME 1   /* time off the 240-bar grid: row skipped */
 #define MFF_INGEST_ERR_DUP 2    /* (stock, day, minute) already present */
 #define MFF_INGEST_ERR_PRICE 3  /* open/high/low/close not finite > 0 */
-#define MFF_INGEST_ERR_VOLUME 4 /* volume not integral in [0, 2^24] */
+#define MFF_INGEST_ERR_VOLUME 4 /* volume not integral in [0, MFF_VOLUME_MAX] */
+#define MFF_VOLUME_MAX 4294967294u /* 2^32 - 2 shares per bar */
 
 /*
  * Ingest: long day-frame rows -> dense panel.
@@ -74,7 +76,8 @@ const char* mff_factor_name(int id);
  * and the time -> minute map minute_in_trade (CM:98-106).  Row i: stock[i] / day[i]
  * (dense indices into the caller's sorted code / date universes, int32), time[i]
  * (HHMMSSmmm, int64), the four prices (float64) and volume (volume_kind).  Writes the
- * five fp32 planes `bars` [5][D][S][240] at (day, stock, minute) and ORs the presence
+ * four fp32 price planes and the u32 volume plane of `bars` [5][D][S][240] (4 B per bar
+ * each; the caller views the volume plane as uint32) at (day, stock, minute), ORs the presence
  * bit into `valid` [D][S][8]; `valid` and `errors` (uint32[5], MFF_INGEST_ERR_*) must be
  * zeroed by the caller before the first call into a panel, so a panel may be filled by
  * several calls (day-file batches).  Contract violations are counted, never trapped;
@@ -111,13 +114,13 @@ size_t mff_stage1_workspace_bytes(int S, int D);
  * 17, before the mff_pdf_* phases and before the LVL/PDF rows are read; part 2 need not
  * wait for it). */
 int mff_stage1_part(const float* open, const float* high, const float* low,
-                    const float* close, const float* volume, const uint32_t* valid,
+                    const float* close, const uint32_t* volume, const uint32_t* valid,
                     int S, int D, const int32_t* factor_ids /* host */, int nf,
                     double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
                     void* workspace, void* stream, int part);
 size_t mff_pdf_levels_bytes(int S, int D);
 int mff_stage1(const float* open, const float* high, const float* low,
-               const float* close, const float* volume, const uint32_t* valid,
+               const float* close, const uint32_t* volume, const uint32_t* valid,
                int S, int D, const int32_t* factor_ids /* host */, int nf,
                double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
                void* workspace, void* stream);
@@ -135,7 +138,7 @@ int mff_stage1(const float* open, const float* high, const float* low,
  * day, and the 14:40+ / 14:10+ volume share uses the code's total over the whole frame.
  * open may be NULL unless a trade_bottom* row is requested.
  */
-int mff_stage1_frame(const float* open, const float* close, const float* volume,
+int mff_stage1_frame(const float* open, const float* close, const uint32_t* volume,
                      const uint32_t* valid, int S, int D, const int32_t* factor_ids /* host */,
                      int nf, double* val, uint8_t* state, void* stream);
 

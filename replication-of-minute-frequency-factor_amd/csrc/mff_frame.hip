@@ -37,7 +37,7 @@ namespace mff {
 struct FrameArgs {
   const float* open;
   const float* close;
-  const float* volume;
+  const uint32_t* volume;  // u32 shares
   const uint32_t* valid;
   double* val;
   uint8_t* state;
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256) void k_frame_xday(FrameArgs a) {
     const uint32_t* mk = a.valid + sd * 8;
     const float* C = a.close + sd * NBAR;
     const bool tail = a.row_b20 >= 0 || a.row_b50 >= 0;  // open may be NULL otherwise
-    const float* V = a.volume + sd * NBAR;
+    const uint32_t* V = a.volume + sd * NBAR;
     double amh = 0.0;
     double P[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     double x0 = 0.0, y0 = 0.0;
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void k_frame_xday(FrameArgs a) {
 
 using namespace mff;
 
-extern "C" int mff_stage1_frame(const float* open, const float* close, const float* volume,
+extern "C" int mff_stage1_frame(const float* open, const float* close, const uint32_t* volume,
                                 const uint32_t* valid, int S, int D, const int32_t* factor_ids, int nf,
                                 double* val, uint8_t* state, void* stream) {
   clear_error();

@@ -193,6 +193,9 @@ __device__ __forceinline__ uint64_t pick(const uint64_t (&x)[K], int k) {
 __device__ __forceinline__ float gval(const float (&x)[K], int m) {
   return bpermf(gbase() + (m >> 4), pick(x, m & 15));
 }
+__device__ __forceinline__ uint32_t gvalu(const uint32_t (&x)[K], int m) {
+  return bpermu(gbase() + (m >> 4), pick(x, m & 15));
+}
 // bar m known at compile time
 template <int M>
 __device__ __forceinline__ float gvalc(const float (&x)[K]) {

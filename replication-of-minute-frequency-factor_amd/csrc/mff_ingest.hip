@@ -5,7 +5,8 @@
 // minute_in_trade (MinuteFrequentFactorCalculateMethodsCICC.py:98-106) is the time ->
 // minute map of the 240-bar grid 09:30-11:29, 13:00-14:59.  Here the host only encodes
 // code / date to dense indices (sorted universes) and ships the numeric columns; this
-// kernel maps time -> minute, casts the f64 columns to the fp32 planes [5][D][S][240],
+// kernel maps time -> minute, casts the f64 prices to the fp32 planes and the volume to
+// the u32 share plane ([5][D][S][240], 4 B a bar each),
 // sets the presence bits [D][S][8] and checks the engine's input contract (include/mff.h)
 // on the fly, counting violations instead of trapping.
 //
@@ -96,8 +97,9 @@ __global__ __launch_bounds__(256) void k_ingest(IngestArgs a) {
         }
         const double v = load_volume(a.vol, a.vol_kind, i);
         e_px += bad ? 1u : 0u;
-        e_vol += (v >= 0.0 && v <= 16777216.0 && v == rint(v)) ? 0u : 1u;
-        a.bars[4 * plane + cell] = (float)v;
+        const bool vok = v >= 0.0 && v <= (double)MFF_VOLUME_MAX && v == rint(v);
+        e_vol += vok ? 0u : 1u;
+        reinterpret_cast<uint32_t*>(a.bars)[4 * plane + cell] = vok ? (uint32_t)v : 0u;
       }
     }
     // presence bits: one atomicOr per distinct mask word of this wave

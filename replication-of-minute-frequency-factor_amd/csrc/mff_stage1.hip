@@ -14,9 +14,10 @@
 //  * a set's variance is exactly 0 iff its values are identical (C3): every mean is
 //    taken as x0 + sum(x - x0)/n with x0 a member, so identical values give exact
 //    zeros; OLS windows test constancy with exact integer change counts;
-//  * doc_pdf thresholds: exact integer comparison 20*cum > k*sum(v) on integral
-//    volumes; an exact tie (the only case where float rounding decides) or
-//    non-integral volume falls back to the reference's sequential float cum-sum.
+//  * volumes are u32 shares (include/mff.h), summed exactly in f64;
+//  * doc_pdf thresholds: exact comparison 20*cum > k*sum(v) of the integer sums; an
+//    exact tie (the only case where float rounding decides) falls back to the
+//    reference's sequential float cum-sum.
 #include "../../include/mff.h"
 #include "mff_internal.h"
 #include "mff_wave.h"
@@ -28,7 +29,7 @@ constexpr int WPB = 4;    // waves per block
 constexpr int SPW = TILE / WPB;
 
 struct S1Args {
-  const float* fld[5];     // open, high, low, close, volume planes [D][S][240]
+  const float* fld[5];     // open, high, low, close (fp32), volume (u32 shares) planes [D][S][240]
   const uint32_t* mask;    // [D][S][8]
   double* val;             // [nf][D][S]
   uint8_t* state;          // [nf][D][S]
@@ -179,7 +180,7 @@ __device__ __forceinline__ double msum(const double (&x)[4], const bool (&f)[4])
 // general path: the tile kernel below, and the list-mode fallback of the 16-lane kernel
 // (mff_stage1g.hip) for stock-days whose closes are not on the 0.01 tick grid or whose
 // doc_pdf threshold is an exact tie.
-__device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, float* vw, bool emit_levels = false) {
+__device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, uint32_t* vw, bool emit_levels = false) {
   const int lane = lane_id();
   const bool lv = lane < 60;
   const uint32_t fam = a.fam;
@@ -203,7 +204,8 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
     const int mf = first_of(B), ml = last_of(B);
 
     // ---- bar planes (absent slots sanitised: prices 1, volume 0)
-    float o[4], h[4], lo[4], c[4], v[4];
+    float o[4], h[4], lo[4], c[4];
+    uint32_t v[4] = {0u, 0u, 0u, 0u};  // volume (u32 shares)
     auto load = [&](int f, float (&x)[4], float dflt) {
       float4 t = make_float4(dflt, dflt, dflt, dflt);
       if (lv) t = reinterpret_cast<const float4*>(a.fld[f] + sd * NBAR)[lane];
@@ -220,11 +222,15 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
     if (fam & needH) load(1, h, 1.0f);
     if (fam & needH) load(2, lo, 1.0f);
     if (fam & needC) load(3, c, 1.0f);
-    if (fam & needV) load(4, v, 0.0f);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] += 0.0f;  // -0 -> +0
+    if ((fam & needV) && lv) {
+      const uint4 t = reinterpret_cast<const uint4*>(a.fld[4] + sd * NBAR)[lane];
+      v[0] = p[0] ? t.x : 0u;
+      v[1] = p[1] ? t.y : 0u;
+      v[2] = p[2] ? t.z : 0u;
+      v[3] = p[3] ? t.w : 0u;
+    }
 
-    // sum of volume (exact for integral volumes), present bars
+    // sum of volume (exact: integers below 2^53), present bars
     double vd_[4];
     double sumv = 0.0;
     if (fam & needV) {
@@ -340,7 +346,8 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
     }
 
     // ================================================================ previous-bar views
-    float cp[4], vp[4];
+    float cp[4];
+    uint32_t vp[4];
     bool hp[4];
     if (fam & (F_SUMC | F_CORR)) {
       prev_valid(c, p, cp, hp);
@@ -351,7 +358,7 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const double pc = hp[k] ? ((double)c[k] - (double)cp[k]) / (double)cp[k] : 0.0;
-        am[k] = (v[k] > 0.0f) ? fabs(pc) / (double)v[k] : 0.0;
+        am[k] = (v[k] != 0u) ? fabs(pc) / (double)v[k] : 0.0;
       }
       out.val(27, msum(am, p));
     }
@@ -377,7 +384,7 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
       out.val(36, pearson(cd, y, ok));
       // corr_pvl CM:905-916: corr(close, volume.shift(-1))
       {
-        float vn[4];
+        uint32_t vn[4];
         bool hn[4];
         next_valid(v, p, vn, hn);
 #pragma unroll
@@ -390,9 +397,10 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
       // corr_prvr CM:850-874 / corr_pvr CM:919-932: rows with volume != 0
       bool pz[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) pz[k] = p[k] && v[k] != 0.0f;
+      for (int k = 0; k < 4; ++k) pz[k] = p[k] && v[k] != 0u;
       if (any(ballot4(pz))) {
-        float cpz[4], vpz[4];
+        float cpz[4];
+        uint32_t vpz[4];
         bool hz[4];
         prev_valid(c, pz, cpz, hz);
         prev_valid(v, pz, vpz, hz);
@@ -462,13 +470,13 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
     if (fam & (F_ORD | F_ORDV)) {
       uint32_t key[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) key[k] = p[k] ? fbits(v[k]) : 0xffffffffu;
+      for (int k = 0; k < 4; ++k) key[k] = p[k] ? v[k] : 0xffffffffu;  // volumes < 2^32 - 1
       bitonic256(key);  // ascending; sorted element e at slot e&3 of lane e>>2
       if (fam & F_ORD) {
         // top_k(k).min() / bottom_k(k).max() thresholds (CM:391-396, 417-422)
-        const float th50 = bitsf(elem(key, n >= 50 ? n - 50 : 0));
-        const float th20 = bitsf(elem(key, n >= 20 ? n - 20 : 0));
-        const float tb50 = bitsf(elem(key, n >= 50 ? 49 : n - 1));
+        const uint32_t th50 = elem(key, n >= 50 ? n - 50 : 0);
+        const uint32_t th20 = elem(key, n >= 20 ? n - 20 : 0);
+        const uint32_t tb50 = elem(key, n >= 50 ? 49 : n - 1);
         double q50[4], q20[4], qb50[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -490,7 +498,7 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int e = l4 + k;
-          const double x = (double)bitsf(key[k]);
+          const double x = (double)key[k];
           if (e < n && e >= n - 10) t10 += x;
           if (e < n && e >= n - 5) t5 += x;
         }
@@ -507,7 +515,7 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
       // levels = distinct closes (key c_last/c is strictly monotone in c for fp32 c).
       // sort (close desc, bar asc): ascending key order, bars of a level in frame order.
       if (lv) {
-        *reinterpret_cast<float4*>(vw + 4 * lane) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<uint4*>(vw + 4 * lane) = make_uint4(v[0], v[1], v[2], v[3]);
       }
       uint64_t key[4];
 #pragma unroll
@@ -532,7 +540,7 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
         lend[k] = valid[k] && ((l4 + k) == n - 1 || hn != hi[k]);
       }
       double cum[4] = {vs[0], vs[1], vs[2], vs[3]};
-      scan4(cum);  // exact: integral volumes
+      scan4(cum);  // exact: integer volumes, sums below 2^53
       double pcum[4];
       bool hpc[4];
       prev_valid(cum, lend, pcum, hpc);
@@ -562,13 +570,6 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
             ++idx;
           }
       }
-      // integral-volume contract check (exact level arithmetic)
-      bool vint = true;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        vint = vint && (!p[k] || (v[k] == rintf(v[k]) && v[k] <= 16777216.0f));
-      vint = __all(vint);
-
       if (fam & F_LVL) {
         // doc_kurt / doc_skew / doc_std over level shares VD_l (CM:937-1003)
         double Vl[4], xl[4];
@@ -591,7 +592,7 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, flo
         const double kk[5] = {12.0, 14.0, 16.0, 18.0, 19.0};
         const double pp[5] = {0.6, 0.7, 0.8, 0.9, 0.95};
         int est[5];
-        bool need_seq = !vint;
+        bool need_seq = false;
         const Bits LE = ballot4(lend);
         const int first_level_end = first_of(LE);
 #pragma unroll
@@ -754,10 +755,10 @@ __global__ __launch_bounds__(256) void k_stage1(S1Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int nf = a.nf;
   double* sv = reinterpret_cast<double*>(smem);                        // [nf][TILE]
-  float* vscr = reinterpret_cast<float*>(smem + (size_t)nf * TILE * 8);  // [WPB][256]
+  uint32_t* vscr = reinterpret_cast<uint32_t*>(smem + (size_t)nf * TILE * 8);  // [WPB][256]
   uint8_t* ss = smem + (size_t)nf * TILE * 8 + WPB * 256 * 4;            // [nf][TILE]
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  float* vw = vscr + wave * 256;
+  uint32_t* vw = vscr + wave * 256;
 
   if (a.list) {  // list mode: grid-stride over the listed stock-days, direct writes
     const int cnt = *a.list_count;

@@ -40,7 +40,7 @@ int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, c
                uint32_t fam_mask, int list_grid, hipStream_t st, uint32_t* lvl_count = nullptr,
                uint64_t* lvl_key = nullptr, uint8_t* lvl_w = nullptr);
 int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
-                  uint32_t fam, double* val, uint8_t* state, const float* ord_th, hipStream_t st);
+                  uint32_t fam, double* val, uint8_t* state, const uint32_t* ord_th, hipStream_t st);
 
 // 16 stock-days of one day per block iteration; MFF_GITER iterations per block
 #ifndef MFF_GITER
@@ -59,7 +59,7 @@ namespace g16 {
 constexpr int NB = 256;  // OLS betas per stock-day (LDS, 8 B each)
 
 struct GArgs {
-  const float* fld[5];
+  const float* fld[5];  // open high low close: fp32; [4] volume: u32 shares (include/mff.h)
   const uint32_t* mask;
   double* val;
   uint8_t* state;
@@ -73,7 +73,7 @@ struct GArgs {
   int* fb_list;
   int* fb_count;
   uint32_t fam_exact;  // families whose non-fast stock-days go to the exact list
-  float* ord_th;       // ORD thresholds [3][D][S] (top-50 min, top-20 min, bottom-50 max)
+  uint32_t* ord_th;    // ORD volume thresholds [3][D][S] (top-50 min, top-20 min, bottom-50 max)
                        // for the serial returns kernel's products, or null
   int S, D;
   uint32_t fam;
@@ -223,7 +223,8 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
 
     if (n > 0) {
       // ---------------------------------------------------------------- loads
-      float o[K], h[K], lo[K], c[K], v[K];
+      float o[K], h[K], lo[K], c[K];
+      uint32_t v[K];  // volume (u32 shares)
       auto load = [&](int f, float (&x)[K], float dflt) {
         if (ln) {
           const float4* p4 = reinterpret_cast<const float4*>(a.fld[f] + sd * NBAR + 16 * g);
@@ -241,6 +242,21 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
       const uint32_t needHL = F_OLS | F_MOMH;
       const uint32_t needC = F_SEG | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD;
       const uint32_t needV = F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD;
+      auto loadv = [&](uint32_t (&x)[K]) {  // volume, absent bars 0
+        if (ln) {
+          const uint4* p4 = reinterpret_cast<const uint4*>(a.fld[4] + sd * NBAR + 16 * g);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint4 t = p4[q];
+            x[4 * q + 0] = t.x; x[4 * q + 1] = t.y; x[4 * q + 2] = t.z; x[4 * q + 3] = t.w;
+          }
+#pragma unroll
+          for (int k = 0; k < K; ++k) x[k] &= present_bits(pb, k);
+        } else {
+#pragma unroll
+          for (int k = 0; k < K; ++k) x[k] = 0u;
+        }
+      };
       auto sanitize = [&](float (&x)[K], float dflt) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -416,8 +432,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
       // phase B/C planes: volume, close, open
       double sumv = 0.0;
       if (fam & needV) {
-        load(4, v, 0.0f);
-        sanitize(v, 0.0f);
+        loadv(v);
         double t = 0.0;
 #pragma unroll
         for (int k = 0; k < K; ++k) t += (double)v[k];
@@ -440,7 +455,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
 
         uint32_t key[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) key[k] = fbits(v[k]) | absent_bits(pb, k);  // v sanitized
+        for (int k = 0; k < K; ++k) key[k] = v[k] | absent_bits(pb, k);  // v sanitized; < 2^32 - 1
         gsort256u(key);
         // the sorted keys go through the group's LDS scratch (element e = 16 g + k at slot
         // 16 k + g: conflict-free stores), and each lane reads the one element it needs:
@@ -453,7 +468,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
                     : g == 10 ? (n >= 50 ? n - 50 : 0)    // top_k(50).min()   CM:391-396
                     : g == 11 ? (n >= 20 ? n - 20 : 0)    // top_k(20).min()
                     : (n >= 50 ? 49 : n - 1);             // bottom_k(50).max() CM:417-422
-        const float xe = (e >= 0 && g < 13) ? bitsf(so[((e & 15) << 4) | (e >> 4)]) : 0.0f;
+        const uint32_t xe = (e >= 0 && g < 13) ? so[((e & 15) << 4) | (e >> 4)] : 0u;
         lds_fence();  // the LVL section reuses the scratch
         if ((fam & F_ORD) && a.ord_th && g >= 10 && g < 13 && act) {
           const size_t pl = (size_t)a.D * a.S;
@@ -573,7 +588,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
       if (fam & F_MOMV) {
         fresh(v);
 
-        const double x0 = (double)gval(v, fb);
+        const double x0 = (double)gvalu(v, fb);
         double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k)
@@ -611,7 +626,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
         const double spre = gsum(a0), scls = gsum(a1), shead = gsum(a2), stail = gsum(a3);
         if (gany(mpre != 0u)) R.val(28, spre);
         if (gany(mcls != 0u)) R.val(29, scls);
-        const double vfirst = (double)gval(v, fb);
+        const double vfirst = (double)gvalu(v, fb);
         R.val(30, vfirst / sumv);
         R.val(31, scls / sumv);
         R.val(32, vfirst);
@@ -625,16 +640,18 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
         fresh(v);
 
         // last present close / volume of this lane -> carries from the left
-        float lc = 1.f, lvv = 0.f, lcz = 1.f, lvz = 0.f;
+        float lc = 1.f, lcz = 1.f;
+        uint32_t lvv = 0u, lvz = 0u;
         const uint32_t pz = pb & 0xFFFFu;
         uint32_t nzm = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
           if ((pb >> k) & 1u) { lc = c[k]; lvv = v[k]; }
-          if (((pb >> k) & 1u) && v[k] != 0.0f) { lcz = c[k]; lvz = v[k]; nzm |= 1u << k; }
+          if (((pb >> k) & 1u) && v[k] != 0u) { lcz = c[k]; lvz = v[k]; nzm |= 1u << k; }
         }
         (void)pz;
-        float cpv, vpv, cpz, vpz;
+        float cpv, cpz;
+        uint32_t vpv, vpz;
         bool hp, hz, hpv, hzv;
         carry_left(lc, pb != 0u, cpv, hp);
         carry_left(lvv, pb != 0u, vpv, hpv);
@@ -647,7 +664,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
 #pragma unroll
           for (int k = 0; k < K; ++k)
             if ((pb >> k) & 1u) {
-              if (h_ && v[k] > 0.0f) am += fabs((double)c[k] - (double)cp) / ((double)cp * (double)v[k]);
+              if (h_ && v[k] != 0u) am += fabs((double)c[k] - (double)cp) / ((double)cp * (double)v[k]);
               cp = c[k];
               h_ = true;
             }
@@ -663,10 +680,10 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
           uint32_t nz2 = nzm;
           if (z1 >= 0 && (z1 >> 4) == g) nz2 &= ~(1u << (z1 & 15));
           const int z2 = gfirst(nz2);
-          const double cf1 = (double)gval(c, f1), vf1 = (double)gval(v, f1);
-          const double cf2 = f2 >= 0 ? (double)gval(c, f2) : 0.0, vf2 = f2 >= 0 ? (double)gval(v, f2) : 0.0;
-          const double cz1 = z1 >= 0 ? (double)gval(c, z1) : 1.0, vz1 = z1 >= 0 ? (double)gval(v, z1) : 1.0;
-          const double cz2 = z2 >= 0 ? (double)gval(c, z2) : 1.0, vz2 = z2 >= 0 ? (double)gval(v, z2) : 1.0;
+          const double cf1 = (double)gval(c, f1), vf1 = (double)gvalu(v, f1);
+          const double cf2 = f2 >= 0 ? (double)gval(c, f2) : 0.0, vf2 = f2 >= 0 ? (double)gvalu(v, f2) : 0.0;
+          const double cz1 = z1 >= 0 ? (double)gval(c, z1) : 1.0, vz1 = z1 >= 0 ? (double)gvalu(v, z1) : 1.0;
+          const double cz2 = z2 >= 0 ? (double)gval(c, z2) : 1.0, vz2 = z2 >= 0 ? (double)gvalu(v, z2) : 1.0;
           // shifts = first pair of each variant (exact zeros for constant sides)
           const double x1 = (cf2 - cf1) / cf1, y1 = vf2;   // prv: (pct_change(close), volume)
           const double x2 = cf1, y2 = vf1;                 // pv
@@ -685,7 +702,8 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
             for (int i = 0; i < 3; ++i)
 #pragma unroll
               for (int j = 0; j < 5; ++j) P[i][j] = 0.0;
-            float cp = cpv, vp = vpv;
+            float cp = cpv;
+            uint32_t vp = vpv;
             bool h_ = hp;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -714,7 +732,8 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
             for (int i = 0; i < 2; ++i)
 #pragma unroll
               for (int j = 0; j < 5; ++j) P[i][j] = 0.0;
-            float czp = cpz, vzp = vpz;
+            float czp = cpz;
+            uint32_t vzp = vpz;
             bool hz_ = hz;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
@@ -737,11 +756,11 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
           // pass 3: pvl, right-to-left with the next present volume (CM:905-916)
           {
             double a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0;
-            float fvv = 0.f;
+            uint32_t fvv = 0u;
 #pragma unroll
             for (int k = K - 1; k >= 0; --k)
               if ((pb >> k) & 1u) fvv = v[k];
-            float vn;
+            uint32_t vn;
             bool hn;
             carry_right(fvv, pb != 0u, vn, hn);
 #pragma unroll
@@ -773,18 +792,15 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
         // Closes are > 0, so the float order is the bit order; absent bars sort last.
         // A stock-day with a non-integral volume still sorts (volume 0) for the level
         // list, and its LVL/PDF values go to the exact path.
-        uint32_t vokm = 0u;  // bars with an integral volume in [0, 2^24]
         uint32_t cmx = 0u, cmn = 0xffffffffu;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-          // integral and in [+0, 2^24] (v is sanitized: no -0; NaN / inf / negatives
-          // have bit patterns above the one of 2^24)
-          const bool vok = (v[k] == rintf(v[k])) && (fbits(v[k]) <= 0x4b800000u);
-          vokm |= (vok ? 1u : 0u) << k;
           cmx = max(cmx, fbits(c[k]) & present_bits(pb, k));
           cmn = min(cmn, fbits(c[k]) | absent_bits(pb, k));
         }
-        const bool ok = (pb & ~vokm) == 0u;
+        // the level volumes below are exact u32 cumulative sums: a day whose volume
+        // reaches 2^32 shares goes to the exact kernel (f64 sums, exact below 2^53)
+        const bool ok = sumv < 4294967296.0;
         cmx = gmax_u(cmx);
         cmn = gmin_u(cmn);
         const float clastf = gval(c, lb);
@@ -810,9 +826,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
 #pragma unroll
           for (int k = 0; k < K; ++k) {
             const uint32_t slot = (uint32_t)(16 * k + g);
-            // absent bars hold 0 (sanitized); a non-integral volume's truncation only
-            // reaches stock-days the exact kernel finishes (the list keys use closes)
-            sv[slot] = (uint32_t)v[k];
+            sv[slot] = v[k];  // absent bars hold 0 (sanitized)
             key[k] = ((cmx - fbits(c[k])) << 8) | slot | absent_bits(pb, k);
           }
           gsort256u(key);
@@ -848,7 +862,8 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
         if (!wide && kd && g == 0) base = atomicAdd(a.lvl_count + d, (uint32_t)L);
         if (!wide) {
           // Compact the levels (run ends, descending close) into LDS by level index:
-          //   lv[l] = cumulative volume through level l (exact u32: sum(v) <= 240 * 2^24),
+          //   lv[l] = cumulative volume through level l (exact u32 when sum(v) < 2^32; a
+          //   larger day is not `fast`: its values come from the exact kernel),
           //   lc[l] = cw << 8 | e, its last sorted element (cw < 2^24 on this path),
           // so level l has volume lv[l] - lv[l-1] and e_l - e_(l-1) bars, and everything
           // per level below runs over ceil(L/16) slots per lane (a lane's levels
@@ -969,9 +984,9 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
 
 using namespace mff;
 
-// workspace: list count (256 B) | exact list int [S*D] | ORD thresholds float [3][S*D]
+// workspace: list count (256 B) | exact list int [S*D] | ORD volume thresholds u32 [3][S*D]
 extern "C" size_t mff_stage1_workspace_bytes(int S, int D) {
-  return 256 + (size_t)S * (size_t)D * (sizeof(int) + 3 * sizeof(float));
+  return 256 + (size_t)S * (size_t)D * (sizeof(int) + 3 * sizeof(uint32_t));
 }
 
 namespace mff {
@@ -999,7 +1014,7 @@ extern "C" size_t mff_pdf_levels_bytes(int S, int D) {
 // values and doc_pdf levels of the listed stock-days, so the serial families need not
 // wait for it).
 static int stage1_parts(const float* open, const float* high, const float* low, const float* close,
-                        const float* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
+                        const uint32_t* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
                         int nf, double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
                         void* workspace, void* stream, int part) {
   clear_error();
@@ -1012,7 +1027,8 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
   MFF_REQUIRE(factor_ids != nullptr, "mff_stage1: factor_ids is NULL");
   MFF_REQUIRE(valid && val && state, "mff_stage1: NULL device buffer");
   MFF_REQUIRE(workspace != nullptr, "mff_stage1: workspace is NULL (mff_stage1_workspace_bytes)");
-  const float* fld[5] = {open, high, low, close, volume};
+  // the volume plane travels with the price planes (its rows are read as u32)
+  const float* fld[5] = {open, high, low, close, reinterpret_cast<const float*>(volume)};
   g16::GArgs a;
   memset(&a, 0, sizeof(a));
   for (int f = 0; f < 5; ++f) a.fld[f] = fld[f];
@@ -1038,7 +1054,7 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
   int* cnt = reinterpret_cast<int*>(workspace);
   a.fb_count = cnt;
   a.fb_list = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + 256);
-  a.ord_th = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + 256 + (size_t)S * D * sizeof(int));
+  a.ord_th = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(workspace) + 256 + (size_t)S * D * sizeof(int));
   const char* impl = getenv("MFF_STAGE1_IMPL");
   const bool w64 = impl && strcmp(impl, "w64") == 0;
   const long long nblk = (long long)((S + 16 * MFF_GITER - 1) / (16 * MFF_GITER)) * D;
@@ -1113,7 +1129,7 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
 }
 
 extern "C" int mff_stage1(const float* open, const float* high, const float* low, const float* close,
-                          const float* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
+                          const uint32_t* volume, const uint32_t* valid, int S, int D, const int32_t* factor_ids,
                           int nf, double* val, uint8_t* state, double* pdf_query, void* pdf_levels,
                           void* workspace, void* stream) {
   return stage1_parts(open, high, low, close, volume, valid, S, D, factor_ids, nf, val, state, pdf_query,
@@ -1121,7 +1137,7 @@ extern "C" int mff_stage1(const float* open, const float* high, const float* low
 }
 
 extern "C" int mff_stage1_part(const float* open, const float* high, const float* low, const float* close,
-                               const float* volume, const uint32_t* valid, int S, int D,
+                               const uint32_t* volume, const uint32_t* valid, int S, int D,
                                const int32_t* factor_ids, int nf, double* val, uint8_t* state,
                                double* pdf_query, void* pdf_levels, void* workspace, void* stream, int part) {
   return stage1_parts(open, high, low, close, volume, valid, S, D, factor_ids, nf, val, state, pdf_query,

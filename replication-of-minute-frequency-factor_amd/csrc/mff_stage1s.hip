@@ -44,14 +44,14 @@ namespace mff {
 namespace s1s {
 
 struct SArgs {
-  const float* fld[5];
+  const float* fld[5];  // open high low close: fp32; [4] volume: u32 shares (include/mff.h)
   const uint32_t* mask;
   double* val;
   uint8_t* state;
   int S, D;
   uint32_t fam;
   int8_t row[NF];
-  const float* ord_th;  // ORD thresholds [3][D][S] from the 16-lane sort kernel
+  const uint32_t* ord_th;  // ORD volume thresholds [3][D][S] from the 16-lane sort kernel
 };
 
 // the serial families, in launch groups (each gets its own register allocation)
@@ -189,7 +189,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   const int f2 = M.first_in(fb + 1, NBAR - 1);
   const float* O = a.fld[0] + sd * NBAR;
   const float* C = a.fld[3] + sd * NBAR;
-  const float* V = a.fld[4] + sd * NBAR;
+  const uint32_t* V = reinterpret_cast<const uint32_t*>(a.fld[4]) + sd * NBAR;
 
   // ---------------------------------------------------------------- shifts
   double x0r = 0.0, x0v = 0.0;
@@ -224,7 +224,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   int nu = 0, ndn = 0;
   // ORD: products of close/open over the bars at or beyond the volume thresholds
   double p50 = 1.0, p20 = 1.0, pb50 = 1.0;
-  float th50 = 0.f, th20 = 0.f, tb50 = 0.f;
+  uint32_t th50 = 0u, th20 = 0u, tb50 = 0u;
   if (fam & F_ORD) {
     const size_t pl = (size_t)a.D * a.S;
     th50 = a.ord_th[sd];
@@ -261,7 +261,8 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   double x5 = 0, y5 = 0, x6 = 0;
   int nzc = 0;
   // carries: previous present bar, previous present non-zero-volume bar
-  float cp = 1.f, vp = 0.f, czp = 1.f, vzp = 1.f;
+  float cp = 1.f, czp = 1.f;
+  uint32_t vp = 0u, vzp = 1u;
   double rcp_ = 1.0, rcz = 1.0, rvz = 1.0;  // their reciprocals (frcp)
   bool hp = false, hz = false;
 
@@ -325,10 +326,12 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   };
 
 
-  // ALLP: every lane has this bar (the quad's wave-uniform fast path): no presence selects
-  auto bar = [&](int m, bool pk, float of, float cf, float vf, auto allp) {
+  // ALLP: every lane has this bar (the quad's wave-uniform fast path): no presence selects.
+  // vb: the volume's u32 bits as staged (float lanes of the LDS image)
+  auto bar = [&](int m, bool pk, float of, float cf, float vb, auto allp) {
     constexpr bool ALLP = decltype(allp)::value;
     if (ALLP) pk = true;
+    const uint32_t vf = __float_as_uint(vb);  // shares
     if (fam & (F_MOMR | F_TRD | F_ORD)) {
       const double q = fdiv((double)cf, (double)of);  // close / open
       const double r = q - 1.0;
@@ -364,7 +367,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         if (m == 189) { S189 = tv; R189 = trv; }
         if (m == 219) { S219 = tv; R219 = trv; }
         if (m <= 50) {
-          const double iw = vf == 0.0f ? __builtin_inf() : frcp((double)vf);  // inf when v = 0: r/0 semantics
+          const double iw = vf == 0u ? __builtin_inf() : frcp((double)vf);  // inf when v = 0: r/0 semantics
           const double ta = pk ? r * iw : 0.0;
           a50 += ta;
           if (m <= 20) {
@@ -395,10 +398,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     double rc = 1.0, rv = 1.0;
     if (fam & (F_SUMC | F_CORR)) {
       rc = frcp(c);
-      rv = frcp(vf != 0.0f ? v : 1.0);
+      rv = frcp(vf != 0u ? v : 1.0);
     }
     if (fam & F_SUMC) {
-      if (hp && vf > 0.0f) amh += fabs(c - (double)cp) * (rcp_ * rv);  // |dc| / (c_prev * v)
+      if (hp && vf != 0u) amh += fabs(c - (double)cp) * (rcp_ * rv);  // |dc| / (c_prev * v)
     }
     if (fam & F_CORR) {
       const double dc = c - xc, dv = v - yv;
@@ -416,7 +419,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       }
       dcp = dc;
       dvp = dv;
-      if (vf != 0.0f) {  // rows with volume != 0 (CM:855-866, 924-930)
+      if (vf != 0u) {  // rows with volume != 0 (CM:855-866, 924-930)
         if (hz) {
           const double pcz = fdivr(c - (double)czp, (double)czp, rcz);
           const double pvz = fdivr(v - (double)vzp, (double)vzp, rvz);
@@ -801,7 +804,7 @@ __global__ __launch_bounds__(128, 2) void k_stage1s_pair(SArgs a) {
 
 // launch the serial kernel for the families of `fam` it covers (mff_stage1g.hip)
 int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
-                  uint32_t fam, double* val, uint8_t* state, const float* ord_th, hipStream_t st) {
+                  uint32_t fam, double* val, uint8_t* state, const uint32_t* ord_th, hipStream_t st) {
   using namespace s1s;
   SArgs a;
   memset(&a, 0, sizeof(a));

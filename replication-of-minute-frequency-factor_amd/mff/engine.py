@@ -25,6 +25,7 @@ from . import _lib, catalog
 from .synth import pack_mask, stack_fields
 
 ABSENT, NULL, VALUE = 0, 1, 2
+VOLUME_MAX = 2 ** 32 - 2  # MFF_VOLUME_MAX: u32 shares per bar (all-ones = absent sort key)
 ROLL_METHODS = {"o": 0, "m": 1, "z": 2, "std": 3}
 
 
@@ -36,7 +37,8 @@ def _stream(device) -> int:
 class DevicePanel:
     """One device's dense panel.
 
-    bars: float32 [5][D][S][240] (open, high, low, close, volume planes)
+    bars: [5][D][S][240] 4-byte words: open, high, low, close (float32) and the volume
+          plane's u32 shares (include/mff.h); a float32 tensor, plane 4 viewed as ints
     mask: int32 [D][S][8] presence bits (bit m%32 of word m//32)
     """
 
@@ -75,9 +77,10 @@ class DevicePanel:
 
 def validate_host_panel(panel) -> None:
     pres = panel["present"]
-    v = panel["volume"][pres]
-    if v.size and (np.any(v < 0) or np.any(v > 2 ** 24) or np.any(v != np.rint(v))):
-        raise ValueError("volume must be integral and within [0, 2**24] (fp32-exact)")
+    v = np.asarray(panel["volume"][pres], dtype=np.float64)
+    if v.size and (not np.all(np.isfinite(v)) or np.any(v < 0) or np.any(v > VOLUME_MAX)
+                   or np.any(v != np.rint(v))):
+        raise ValueError(f"volume must be integral and within [0, {VOLUME_MAX}] shares")
     for k in ("open", "high", "low", "close"):
         x = panel[k][pres]
         if x.size and (not np.all(np.isfinite(x)) or np.any(x <= 0)):

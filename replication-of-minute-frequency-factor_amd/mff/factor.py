@@ -311,76 +311,68 @@ class MinFreqFactor(Factor):
 
         `calculate_method` is one of the mff ``cal_*`` functions (or a factor name): the
         day files are read in batches of `batch_days`, turned into one dense panel and
-        run through the stage-1 kernel.  A day file that cannot be read or breaks the
-        input contract is reported with the reference's message and dropped, the other
-        days of its batch unaffected (MF:18-25, 95); ``strict=True`` raises instead,
-        naming the file.  Any other callable runs per file on the host exactly as the
-        reference does (joblib process pool, errors print and skip)."""
-        pd = _pd()
+        run through the stage-1 kernel (every factor at once; the batch's results are kept
+        in a host cache keyed by the files' path / size / mtime, so the next factor over
+        the same files costs no re-read and no re-ingest, see :func:`result_cache_info`).
+        A day file that cannot be read or breaks the input contract is reported with the
+        reference's message and dropped, the other days of its batch unaffected
+        (MF:18-25, 95); ``strict=True`` raises instead, naming the file.  Any other
+        callable runs per file on the host exactly as the reference does (joblib process
+        pool, errors print and skip)."""
         factor_exposure = self._read_exposure(
             factor_name=self.factor_name,
             default_path=os.path.join(_EXPOSURE_DIR, "CICC Factor"), path=path)
         folder_path = folder_path or _KLINE_DIR
-        file_names = sorted(f for f in os.listdir(folder_path) if f.endswith(".parquet"))
-        index = pd.DataFrame({"file_name": file_names})
-        index["date"] = pd.to_datetime(index["file_name"].str[:8], format="%Y%m%d").dt.date
-        if factor_exposure is not None:  # MF:79-81
-            end_date = max(frames._as_date(x) for x in factor_exposure["date"])
-            index = index[index["date"] > end_date]
+        files = _pending_files(folder_path, factor_exposure)
 
         name = getattr(calculate_method, "_mff_factor", None)
         if isinstance(calculate_method, str):
             name = calculate_method[4:] if calculate_method.startswith("cal_") else calculate_method
         valid = []
-        if len(index) > 0:
+        if files:
             if name is not None and name in catalog.ID:
-                valid = self._gpu_batches(index["file_name"].tolist(), folder_path, name,
-                                          batch_days, device, strict)
+                valid = _gpu_batches(files, folder_path, [name], batch_days, device, strict)[name]
             else:
                 from joblib import Parallel, delayed
 
                 results = Parallel(n_jobs=-1 if n_jobs is None else n_jobs)(
                     delayed(self._process_single_file)(f, folder_path, calculate_method)
-                    for f in index["file_name"])
+                    for f in files)
                 valid = [r for r in results if r is not None]
+        self.factor_exposure = _merge(factor_exposure, valid)
 
-        if factor_exposure is None:
-            self.factor_exposure = _sort(pd.concat(valid, ignore_index=True)) if valid else None
-        elif valid:
-            self.factor_exposure = _sort(pd.concat([factor_exposure] + valid, ignore_index=True))
-        else:
-            self.factor_exposure = factor_exposure
-
-    def _gpu_batches(self, files, folder_path, name, batch_days, device, strict=False):
-        from .factors import compute_long
-        from .ingest import NoTables
-
-        out = []
-        for b0 in range(0, len(files), batch_days):
-            tables, names = [], []
-            for f in files[b0:b0 + batch_days]:
-                try:
-                    tables.append(self._read_day_file(os.path.join(folder_path, f)))
-                    names.append(f)
-                except Exception as e:  # MF:23-25: report and skip the day
-                    if strict:
-                        raise ValueError(f"{f}: {e}") from e
-                    print(f"处理文件 {f} 时出错: {str(e)}")
-            if not tables:
-                continue
-            errors = {}
-            # one reference call per file (per-day semantics); a bad file drops its day only
-            try:
-                res = compute_long(tables, [name], device, per_day=True, skip_bad=True, errors=errors)
-            except NoTables as e:
-                errors, res = e.dropped, None
-            for k, msg in errors.items():
-                if strict:
-                    raise ValueError(f"{names[k]}: {msg}")
-                print(f"处理文件 {names[k]} 时出错: {msg}")
-            if res is not None:
-                out.append(res[name])
-        return out
+    @classmethod
+    def cal_exposures_by_min_data(cls, calculate_methods=None, path: str = None,
+                                  folder_path: Optional[str] = None, batch_days: int = 64,
+                                  device=None, strict: bool = False):
+        """Many factors over the same day files in ONE read / ingest / stage-1 pass per
+        batch (the reference re-reads every file per factor, MF:87-94): returns
+        {name: MinFreqFactor} with each factor's exposure updated exactly as
+        ``cal_exposure_by_min_data`` would (its own stored exposure and resume date).
+        calculate_methods: mff ``cal_*`` functions or names (default: all 58)."""
+        names = []
+        for m in (catalog.NAMES if calculate_methods is None else calculate_methods):
+            nm = m if isinstance(m, str) else getattr(m, "_mff_factor", None)
+            if nm is None:
+                raise ValueError(f"{m!r} is not an mff cal_* function")
+            nm = nm[4:] if nm.startswith("cal_") else nm
+            if nm not in catalog.ID:
+                raise ValueError(f"unknown factor {nm!r}")
+            names.append(nm)
+        folder_path = folder_path or _KLINE_DIR
+        out, groups = {}, {}
+        for nm in names:
+            f = cls(nm)
+            ex = f._read_exposure(factor_name=nm, default_path=os.path.join(_EXPOSURE_DIR, "CICC Factor"),
+                                  path=path)
+            out[nm] = (f, ex)
+            groups.setdefault(tuple(_pending_files(folder_path, ex)), []).append(nm)
+        for files, grp in groups.items():
+            res = _gpu_batches(list(files), folder_path, grp, batch_days, device, strict) if files else {}
+            for nm in grp:
+                f, ex = out[nm]
+                f.factor_exposure = _merge(ex, res.get(nm, []))
+        return {nm: out[nm][0] for nm in names}
 
     def cal_final_exposure(self, frequency, method: str, mode: str = "calendar", pool="full"):
         """MF:114-245.  mode='days': per-code rolling over present rows on the GPU
@@ -429,6 +421,119 @@ class MinFreqFactor(Factor):
         ov, os_ = engine.rolling(v, s, frequency, method)
         torch.cuda.synchronize(dev)
         return frames.to_long(ov[0].cpu().numpy(), os_[0].cpu().numpy(), codes, dates, name)
+
+
+def _pending_files(folder_path, factor_exposure):
+    """Day files of the folder (YYYYMMDD*.parquet, MF:68-78) after the exposure's max
+    date (MF:79-81), sorted."""
+    pd = _pd()
+    file_names = sorted(f for f in os.listdir(folder_path) if f.endswith(".parquet"))
+    index = pd.DataFrame({"file_name": file_names})
+    index["date"] = pd.to_datetime(index["file_name"].str[:8], format="%Y%m%d").dt.date
+    if factor_exposure is not None:
+        end_date = max(frames._as_date(x) for x in factor_exposure["date"])
+        index = index[index["date"] > end_date]
+    return index["file_name"].tolist()
+
+
+def _merge(factor_exposure, valid):
+    """MF:97-110: old exposure + new rows, sorted [date, code]."""
+    pd = _pd()
+    if factor_exposure is None:
+        return _sort(pd.concat(valid, ignore_index=True)) if valid else None
+    if valid:
+        return _sort(pd.concat([factor_exposure] + valid, ignore_index=True))
+    return factor_exposure
+
+
+# ---------------------------------------------------------------- day-file batch results
+# Dense stage-1 results of every factor per day-file batch, keyed by the batch's files
+# (absolute path, size, mtime): a notebook running the 58 cal_* one after another over
+# the same folder reads and ingests every file once.  Entries are added while they fit
+# MFF_RESULT_CACHE_BYTES (default 8 GiB; 0 disables) and never evicted by a later insert
+# (a scan longer than the cache keeps its head cached instead of thrashing);
+# clear_result_cache() frees it.
+_RESULTS: "OrderedDict" = None
+_RESULTS_BYTES = 0
+
+
+def clear_result_cache() -> None:
+    global _RESULTS, _RESULTS_BYTES
+    _RESULTS, _RESULTS_BYTES = None, 0
+
+
+def result_cache_info() -> dict:
+    return {"batches": 0 if _RESULTS is None else len(_RESULTS), "bytes": _RESULTS_BYTES,
+            "cap": int(os.environ.get("MFF_RESULT_CACHE_BYTES", str(8 << 30)))}
+
+
+def _batch_key(folder_path, files, device):
+    try:
+        key = []
+        for f in files:
+            p = os.path.abspath(os.path.join(folder_path, f))
+            st = os.stat(p)
+            key.append((p, st.st_size, st.st_mtime_ns))
+        return (str(device),) + tuple(key)
+    except OSError:
+        return None
+
+
+def _batch_results(files, folder_path, device):
+    """(val [58][D][S], state, codes, dates, {file name: error}) of one batch of day files
+    (all 58 factors, per-day semantics), from the cache or computed."""
+    global _RESULTS, _RESULTS_BYTES
+    from collections import OrderedDict
+
+    from .factors import compute_dense
+    from .ingest import NoTables
+
+    key = _batch_key(folder_path, files, device)
+    if key is not None and _RESULTS is not None and key in _RESULTS:
+        return _RESULTS[key]
+    tables, names, errors = [], [], {}
+    for f in files:
+        try:
+            tables.append(MinFreqFactor._read_day_file(os.path.join(folder_path, f)))
+            names.append(f)
+        except Exception as e:  # noqa: BLE001 -- MF:23-25: report and skip the day
+            errors[f] = str(e)
+    res = None
+    if tables:
+        try:  # one reference call per file (per-day semantics); a bad file drops its day only
+            v, s, _, codes, dates, dropped = compute_dense(tables, None, device, per_day=True, skip_bad=True)
+            res = (v, s, codes, dates)
+        except NoTables as e:
+            dropped = e.dropped
+        errors.update({names[k]: msg for k, msg in dropped.items()})
+    out = (res, dict(sorted(errors.items())))
+    nbytes = 0 if res is None else res[0].nbytes + res[1].nbytes
+    cap = int(os.environ.get("MFF_RESULT_CACHE_BYTES", str(8 << 30)))
+    if key is not None and _RESULTS_BYTES + nbytes <= cap:
+        if _RESULTS is None:
+            _RESULTS = OrderedDict()
+        _RESULTS[key] = out
+        _RESULTS_BYTES += nbytes
+    return out
+
+
+def _gpu_batches(files, folder_path, names, batch_days, device, strict=False):
+    """{name: [long frames of each batch]} over the day files, batch_days at a time."""
+    out = {nm: [] for nm in names}
+    for b0 in range(0, len(files), batch_days):
+        res, errors = _batch_results(files[b0:b0 + batch_days], folder_path, device)
+        for f, msg in errors.items():
+            if strict:
+                raise ValueError(f"{f}: {msg}")
+            print(f"处理文件 {f} 时出错: {msg}")
+        if res is None:
+            continue
+        v, s, codes, dates = res
+        for nm in names:
+            i = catalog.ID[nm]
+            out[nm].append(frames.to_long(v[i], s[i], codes, dates, nm,
+                                          first="date" if nm == "shape_skratio" else "code"))
+    return out
 
 
 def _arrow_float_mapper(t):

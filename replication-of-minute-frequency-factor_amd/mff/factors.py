@@ -34,6 +34,39 @@ FRAME_XDAY = ("liq_amihud_1min", "corr_prvr", "trade_bottom20retRatio", "trade_b
 FRAME_RANK = ("doc_pdf60", "doc_pdf70", "doc_pdf80", "doc_pdf90", "doc_pdf95")
 
 
+def compute_dense(df, names: Sequence[str] | None = None, device=None, per_day: bool | None = None,
+                  skip_bad: bool = False):
+    """Long frame(s) -> the dense stage-1 result on the host: (val f64 [nf][D][S], state u8
+    [nf][D][S], names, codes, dates, dropped {table index: reason}).  Semantics as
+    :func:`compute_long`."""
+    import torch
+
+    from . import _lib, engine, ingest
+
+    names = list(catalog.NAMES if names is None else
+                 [n[4:] if n.startswith("cal_") else n for n in names])
+    if per_day is None:
+        per_day = isinstance(df, (list, tuple))
+    dp = ingest.to_device_panel(df, _device(device), skip_bad=skip_bad)  # GPU long -> dense (mff_ingest_rows)
+    val, state, ids = engine.compute_factors(dp, names, frame=not per_day)
+    if not per_day and dp.D > 1 and any(n in FRAME_XDAY for n in names):
+        lib = _lib.load()
+        b = dp.bars
+        _lib.check(lib.mff_stage1_frame(_lib.ptr(b[0]), _lib.ptr(b[3]), _lib.ptr(b[4]), _lib.ptr(dp.mask),
+                                        dp.S, dp.D, _lib.int_array(ids), len(ids), _lib.ptr(val),
+                                        _lib.ptr(state), torch.cuda.current_stream(dp.device).cuda_stream),
+                   "mff_stage1_frame")
+    torch.cuda.synchronize(dp.device)
+    return val.cpu().numpy(), state.cpu().numpy(), names, dp.codes, dp.dates, dp.dropped
+
+
+def to_long_frames(val, state, names, codes, dates) -> Dict:
+    """Dense rows -> {name: long frame} with the reference's column order (CM:683)."""
+    return {nm: frames.to_long(val[i], state[i], codes, dates, nm,
+                               first="date" if nm == "shape_skratio" else "code")
+            for i, nm in enumerate(names)}
+
+
 def compute_long(df, names: Sequence[str] | None = None, device=None, per_day: bool | None = None,
                  skip_bad: bool = False, errors: Dict | None = None) -> Dict:
     """Long frame(s) -> {name: long result frame} for the requested factors, computed in
@@ -45,40 +78,18 @@ def compute_long(df, names: Sequence[str] | None = None, device=None, per_day: b
     (liq_amihud_1min CM:746, corr_prvr CM:862-867, trade_bottom20/50retRatio CM:1216,
     1238-1240) then reach across days exactly as the reference does on that frame (rows of
     a code in (date, time) order), and doc_pdf60..95 rank every row of every date
-    (`.rank()` outside `.over`, CM:1015-1017).  A list of tables is a list of day files, each its own
-    reference call (MinuteFrequentFactorCICC.py:22): per-day semantics.  ``per_day``
-    overrides the choice.
+    (`.rank()` outside `.over`, CM:1015-1017).  A list of tables is a list of day files,
+    each its own reference call (MinuteFrequentFactorCICC.py:22): per-day semantics.
+    ``per_day`` overrides the choice.
 
     A table that breaks the input contract (include/mff.h) raises ValueError, unless
     ``skip_bad``: then its days are dropped (no rows), as the reference driver drops a
     day file whose call raised (MinuteFrequentFactorCICC.py:18-25, 95), and ``errors``
     (a dict, if given) receives {table index: reason}."""
-    import torch
-
-    from . import _lib, engine
-
-    names = list(catalog.NAMES if names is None else
-                 [n[4:] if n.startswith("cal_") else n for n in names])
-    from . import ingest
-
-    if per_day is None:
-        per_day = isinstance(df, (list, tuple))
-    dp = ingest.to_device_panel(df, _device(device), skip_bad=skip_bad)  # GPU long -> dense (mff_ingest_rows)
+    v, s, names, codes, dates, dropped = compute_dense(df, names, device, per_day, skip_bad)
     if errors is not None:
-        errors.update(dp.dropped)
-    val, state, ids = engine.compute_factors(dp, names, frame=not per_day)
-    if not per_day and dp.D > 1 and any(n in FRAME_XDAY for n in names):
-        lib = _lib.load()
-        b = dp.bars
-        _lib.check(lib.mff_stage1_frame(_lib.ptr(b[0]), _lib.ptr(b[3]), _lib.ptr(b[4]), _lib.ptr(dp.mask),
-                                        dp.S, dp.D, _lib.int_array(ids), len(ids), _lib.ptr(val),
-                                        _lib.ptr(state), torch.cuda.current_stream(dp.device).cuda_stream),
-                   "mff_stage1_frame")
-    torch.cuda.synchronize(dp.device)
-    v, s = val.cpu().numpy(), state.cpu().numpy()
-    return {nm: frames.to_long(v[i], s[i], dp.codes, dp.dates, nm,
-                               first="date" if nm == "shape_skratio" else "code")
-            for i, nm in enumerate(names)}
+        errors.update(dropped)
+    return to_long_frames(v, s, names, codes, dates)
 
 
 def _make(name: str):
@@ -94,7 +105,7 @@ def _make(name: str):
     return fn
 
 
-__all__ = ["compute_long"]
+__all__ = ["compute_long", "compute_dense"]
 for _n in catalog.NAMES:
     globals()["cal_" + _n] = _make(_n)
     __all__.append("cal_" + _n)

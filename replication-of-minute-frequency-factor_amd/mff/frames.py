@@ -72,8 +72,8 @@ def _as_date(x):
 
 
 def to_dense(df, codes: Sequence[str] | None = None) -> Dict:
-    """Long frame -> host panel dict (see mff.synth): float32 planes [D][S][240], present
-    mask, sorted codes and dates."""
+    """Long frame -> host panel dict (see mff.synth): float32 price planes and a float64
+    volume plane [D][S][240], present mask, sorted codes and dates."""
     cols = _columns(df)
     for k in ("code", "date", "time") + FIELDS:
         if k not in cols:
@@ -95,9 +95,10 @@ def to_dense(df, codes: Sequence[str] | None = None) -> Dict:
     if np.unique(flat).size != flat.size:
         raise ValueError("duplicate (code, date, time) rows")
     panel = {}
-    for k in FIELDS:
-        arr = np.full(D * S * MINUTES, np.nan, dtype=np.float32)
-        arr[flat] = np.asarray(cols[k], dtype=np.float64).astype(np.float32)
+    for k in FIELDS:  # prices fp32 like the device planes; volume f64 (u32 shares on the device)
+        dt_ = np.float64 if k == "volume" else np.float32
+        arr = np.full(D * S * MINUTES, np.nan, dtype=dt_)
+        arr[flat] = np.asarray(cols[k], dtype=np.float64).astype(dt_)
         panel[k] = arr.reshape(D, S, MINUTES)
     pres = np.zeros(D * S * MINUTES, dtype=bool)
     pres[flat] = True

@@ -5,8 +5,9 @@ The reference hands every ``cal_*`` a long frame read from one parquet day file
 volume).  Here the host does only what needs strings or dates: it encodes ``code`` and
 ``date`` to dense indices into sorted universes (pyarrow compute kernels, no Python
 loop over rows) and stages the numeric columns in pinned memory.  The device kernel
-``mff_ingest_rows`` (csrc/mff_ingest.hip) maps time -> minute (CM:98-106), casts to the
-fp32 planes, sets the presence bits and counts contract violations.
+``mff_ingest_rows`` (csrc/mff_ingest.hip) maps time -> minute (CM:98-106), casts the
+prices to the fp32 planes and the volume to u32 shares, sets the presence bits and counts
+contract violations.
 
 Batches of day files stream through two pinned staging slots on a side stream: the
 host encodes batch k+1 while batch k is copied (H2D, async) and scattered, and the
@@ -29,7 +30,7 @@ from . import _lib
 FIELDS = ("open", "high", "low", "close", "volume")
 ERRORS = ("stock/day index out of range", "bars off the 240-minute grid",
           "duplicate (code, date, time) rows", "prices must be finite and > 0",
-          "volume must be integral and within [0, 2**24] (fp32-exact)")
+          "volume must be integral and within [0, 2**32 - 2] shares")
 _VOLUME_KIND = {np.dtype(np.float64): 0, np.dtype(np.int64): 1, np.dtype(np.float32): 2,
                 np.dtype(np.int32): 3}
 _EPOCH = _dt.date(1970, 1, 1)

@@ -8,8 +8,10 @@ Two generators with the same distribution:
   (60 GB at config 4 cannot be generated on the host and pushed over PCIe per run).
 
 Panel layout (host dict):
-  ``open/high/low/close/volume``: float32 [D][S][240]; absent bars hold NaN so a kernel
-  that reads an absent bar poisons its output instead of passing by luck.
+  ``open/high/low/close/volume``: float32 [D][S][240] (volume may be float64 for share
+  counts beyond fp32's integers); absent bars hold NaN so a kernel that reads an absent
+  price poisons its output instead of passing by luck.  On the device (stack_fields) the
+  volume plane holds u32 shares, absent bars 0.
   ``present``: bool [D][S][240]; ``codes``: sorted code strings; ``dates``: ISO dates.
 
 Prices: per-stock start lognormal(ln 15, 0.8) clipped to [1, 500]; per-minute log-return
@@ -148,9 +150,17 @@ def unpack_mask(words: np.ndarray) -> np.ndarray:
     return bits[:, :MINUTES].reshape(*sh, MINUTES)
 
 
+def volume_u32(volume: np.ndarray) -> np.ndarray:
+    """Host volume (float, NaN on absent bars) -> the device's u32 share counts (absent 0)."""
+    v = np.asarray(volume, dtype=np.float64)
+    return np.where(np.isfinite(v) & (v >= 0) & (v < 2.0 ** 32), v, 0.0).astype(np.uint32)
+
+
 def stack_fields(panel: Dict) -> np.ndarray:
-    """Host panel -> the device bar layout float32 [5][D][S][240] (open, high, low, close, volume)."""
-    return np.stack([panel[k] for k in ("open", "high", "low", "close", "volume")])
+    """Host panel -> the device bar layout [5][D][S][240] as float32 words: open, high,
+    low, close (fp32) and the volume plane's u32 shares (include/mff.h)."""
+    px = [np.asarray(panel[k], dtype=np.float32) for k in ("open", "high", "low", "close")]
+    return np.stack(px + [volume_u32(panel["volume"]).view(np.float32)])
 
 
 def subpanel(panel: Dict, stocks=None, days=None) -> Dict:
@@ -166,7 +176,8 @@ def make_panel_device(S: int, D: int, device, config: int = 3, day_chunk: int = 
                       ragged: bool = False, seed_offset: int = 0):
     """Same distribution as :func:`make_panel`, generated on ``device`` with torch.
 
-    Returns (bars float32 [5][D][S][240], mask int32 [D][S][8]).  Used only where the
+    Returns (bars float32 [5][D][S][240] -- plane 4 holds u32 share counts --, mask int32
+    [D][S][8]).  Used only where the
     panel is too large for the host path (bench configs 3/4)."""
     import torch
 
@@ -192,8 +203,9 @@ def make_panel_device(S: int, D: int, device, config: int = 3, day_chunk: int = 
             vol = torch.round(vscale[:, None] * prof[None, :] * torch.exp(torch.randn((S, MINUTES), generator=g, **f64) * 0.6)) * 100.0
             vol = torch.where(torch.rand((S, MINUTES), generator=g, **f64) < 0.01, torch.zeros_like(vol), vol)
             vol = torch.clamp(vol, max=VOL_CAP - (VOL_CAP % 100))
-            for k, x in enumerate((opn, hi, low, close, vol)):
+            for k, x in enumerate((opn, hi, low, close)):
                 bars[k, d] = x.to(torch.float32)
+            bars[4, d] = vol.to(torch.int64).to(torch.int32).view(torch.float32)  # u32 shares
             p_prev = close[:, -1]
     mask = torch.full((D, S, 8), -1, device=device, dtype=torch.int32)
     mask[..., 7] = 0xFFFF  # bars 224..239; bits 240..255 stay clear
@@ -243,4 +255,4 @@ def make_ragged_device(bars, mask, g, day_chunk: int = 50) -> None:
             px = bars[3, d0 + fd, fs, 0]
             for k in range(4):
                 bars[k, d0 + fd, fs, :] = px[:, None]
-            bars[4, d0 + fd, fs, :] = 0.0
+            bars[4, d0 + fd, fs, :] = 0.0  # the bits of 0 shares

@@ -169,3 +169,39 @@ def test_incremental_update_through_gpu_batches(dev, tmp_path):
         v, s = _dense(out, f"{name}_4_{meth}", panel)
         rv, rs = O.oracle_stage2(ov[0], os_[0], 4, meth)
         assert not compare(v, s, rv, rs, f"{name}_4_{meth}", atol=1e-9)
+
+
+def test_all_factors_one_ingest_and_result_cache(dev, tmp_path, monkeypatch):
+    """cal_exposures_by_min_data: every factor from one read / ingest / pass per batch;
+    afterwards single-factor calls over the same files hit the batch result cache (no
+    file is read again) and equal the oracle."""
+    import mff_oracle as O
+    from MinuteFrequentFactorCICC import MinFreqFactor
+    import MinuteFrequentFactorCalculateMethodsCICC as CM
+    from mff import catalog, factor, synth
+    panel = synth.make_panel(25, 4, config=24, ragged=True)
+    folder = str(tmp_path / "kl")
+    os.mkdir(folder)
+    write_day_files(panel, folder)
+    ov, os_ = O.oracle_stage1(panel)
+    factor.clear_result_cache()
+    reads = []
+    orig = MinFreqFactor._read_day_file
+    monkeypatch.setattr(MinFreqFactor, "_read_day_file", staticmethod(lambda p: reads.append(p) or orig(p)))
+    out = MinFreqFactor.cal_exposures_by_min_data(path=str(tmp_path / "exp"), folder_path=folder, batch_days=3)
+    assert list(out) == catalog.NAMES and len(reads) == 4
+    bad = []
+    for i, nm in enumerate(catalog.NAMES):
+        v, s = _dense(out[nm].factor_exposure, nm, panel)
+        bad += compare(v, s, ov[i], os_[i], nm)
+    assert factor.result_cache_info()["batches"] == 2
+    for nm in ("corr_pv", "doc_pdf95", "shape_skratio"):
+        g = MinFreqFactor(nm)
+        g.cal_exposure_by_min_data(getattr(CM, "cal_" + nm), path=str(tmp_path / "exp"), folder_path=folder,
+                                   batch_days=3)
+        assert list(g.factor_exposure.columns) == list(out[nm].factor_exposure.columns)
+        v, s = _dense(g.factor_exposure, nm, panel)
+        bad += compare(v, s, ov[catalog.ID[nm]], os_[catalog.ID[nm]], f"{nm}/cached")
+    assert len(reads) == 4, "a cached batch re-read its files"
+    assert not bad, "\n".join(bad)
+    factor.clear_result_cache()

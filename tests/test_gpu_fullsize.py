@@ -35,7 +35,8 @@ def _host_sub(bars, mask, days, stocks):
     m = mask.index_select(0, di).index_select(1, si).cpu().numpy().view(np.uint32)
     pres = synth.unpack_mask(m)
     out = {k: np.where(pres, b[f], np.float32(np.nan)).astype(np.float32)
-           for f, k in enumerate(("open", "high", "low", "close", "volume"))}
+           for f, k in enumerate(("open", "high", "low", "close"))}
+    out["volume"] = np.where(pres, b[4].view(np.uint32).astype(np.float64), np.nan)  # u32 shares
     out["present"] = pres
     out["codes"] = [f"{s:06d}.SZ" for s in stocks]
     out["dates"] = list(days)

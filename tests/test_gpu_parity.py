@@ -89,8 +89,9 @@ def test_stage1_w64_kernel_golden(dev, monkeypatch):
 
 def test_stage1_level_fallback_and_off_tick(dev):
     """Levels off the 0.01 grid and wide intraday ranges go through the sorted-level path;
-    stock-days with non-integral volume go through the listed wave64 fallback.  The
-    DevicePanel is built directly (the host validator would refuse fractional volume)."""
+    bars of 30 M+ shares (beyond fp32's integers: the volume plane is u32) take the fast
+    path, and stock-days whose volume reaches 2^32 shares (the fast path's u32 level sums)
+    the listed wave64 fallback."""
     import mff_oracle as O
     from mff import synth, catalog, engine
     panel = synth.make_panel(41, 3, config=14, ragged=True)
@@ -104,8 +105,12 @@ def test_stage1_level_fallback_and_off_tick(dev):
     ramp = np.linspace(-1.0, 1.0, c.shape[2])
     c[:, 18:21] = (np.round(10000 + 700 * ramp) * 0.01).astype(np.float32)
     c[:, 21:24] = (np.round(3000 + 200 * ramp + rng.integers(0, 3, c[:, 21:24].shape)) * 0.01).astype(np.float32)
-    v = panel["volume"]
-    v[:, 20:25] = v[:, 20:25] + np.float32(0.5)
+    v = panel["volume"].astype(np.float64)
+    v[:, 24:27] = v[:, 24:27] * 37.0 + 30_000_001.0  # odd counts > 2^24 on every bar
+    v[:, 27:29] = v[:, 27:29] * 50.0 + 3_000_000_001.0  # a day's total >= 2^32: exact path
+    v[:, 29, 5] = 2.0 ** 32 - 2  # the largest admitted bar
+    panel["volume"] = v
+    engine.validate_host_panel(panel)
     ov, os_ = O.oracle_stage1(panel)
     bars = torch.from_numpy(np.ascontiguousarray(synth.stack_fields(panel))).to(dev)
     mask = torch.from_numpy(synth.pack_mask(panel["present"]).view(np.int32)).to(dev)

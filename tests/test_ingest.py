@@ -71,8 +71,10 @@ def _check_panel(dp, ref):
     assert np.array_equal(mask, synth.pack_mask(ref["present"]))
     bars = dp.bars.cpu().numpy()
     pres = ref["present"]
-    for k, f in enumerate(frames.FIELDS):
+    for k, f in enumerate(frames.FIELDS[:4]):
         assert np.array_equal(bars[k][pres], ref[f][pres]), f
+    # the volume plane holds u32 shares
+    assert np.array_equal(bars[4].view(np.uint32)[pres], synth.volume_u32(ref["volume"])[pres])
 
 
 @pytest.mark.gpu
@@ -131,7 +133,8 @@ def test_ingest_errors(dev):
         (df.assign(time=113000000), "grid"),
         (df.assign(time=93000500), "grid"),
         (df.assign(volume=1.5), "volume"),
-        (df.assign(volume=2.0 ** 24 + 2), "volume"),
+        (df.assign(volume=2.0 ** 32 - 1), "volume"),
+        (df.assign(volume=2.0 ** 40), "volume"),
         (df.assign(volume=-1.0), "volume"),
         (df.assign(close=0.0), "prices"),
         (df.assign(high=float("nan")), "prices"),
@@ -140,6 +143,11 @@ def test_ingest_errors(dev):
     for bad, msg in cases:
         with pytest.raises(ValueError, match=msg):
             ingest.to_device_panel(bad, dev)
+    # u32 shares: beyond fp32's integers, up to 2^32 - 2 (int64 and float64 columns)
+    for v in (30_000_001, 2 ** 32 - 2):
+        for col in (np.array([v], np.int64), np.array([float(v)])):
+            dp = ingest.to_device_panel(df.assign(volume=col), dev)
+            assert int(dp.bars[4].view(torch.int32).cpu().numpy().view(np.uint32)[0, 0, 0]) == v
     with pytest.raises(ValueError, match="index out of range"):
         ingest.to_device_panel(df, dev, codes=["B"])
 
@@ -153,7 +161,9 @@ def test_cal_function_through_ingest(dev):
     panel, df = _frame(S=11, D=2, config=21)
     ov, os_ = O.oracle_stage1(panel)
     res = factors.compute_long(df, ["vol_return1min", "doc_pdf80"], dev)
+    # one 2-date frame: doc_pdf ranks over both dates (CM:1015-1017)
+    exp = {"vol_return1min": (ov[catalog.ID["vol_return1min"]], os_[catalog.ID["vol_return1min"]]),
+           "doc_pdf80": O.oracle_frame_doc_pdf(panel)["doc_pdf80"]}
     for name in ("vol_return1min", "doc_pdf80"):
         v, s, _, _ = frames.from_long(res[name], name, codes=panel["codes"], dates=panel["dates"])
-        i = catalog.ID[name]
-        assert not compare(v, s, ov[i], os_[i], name), name
+        assert not compare(v, s, *exp[name], name), name
