@@ -17,4 +17,5 @@ for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $pmc --kernel-include-regex "$KRE" -d $OUT/p$i -o pmc --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-extras --steps 1 --warmup 0 --stocks $S --days $D > $OUT/p$i.log 2>&1 || { echo "PMC pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
-python3 $R/profiles/pmc_table.py $OUT > $OUT/table.txt && cat $OUT/table.txt
+python3 $R/profiles/pmc_table.py $OUT > $OUT/table.txt
+python3 $R/profiles/pmc_json.py $OUT $S $D $TAG $OUT/pmc_stage1.json

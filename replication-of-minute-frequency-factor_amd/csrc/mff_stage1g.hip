@@ -220,6 +220,10 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
     R.r[0] = R.r[1] = R.r[2] = R.r[3] = 0.0;
     R.st = 0u;
     double qv = qnan();  // lane t < 5: doc_pdf query t (the level close ratio)
+    // doc_pdf level list of this group's stock-day (appended after the result stores):
+    // level count, last close, close-word base (the levels themselves stay in scratch)
+    uint32_t emitL = 0u, emitB = 0u;
+    float emitC = 1.0f;
 
     if (n > 0) {
       // ---------------------------------------------------------------- loads
@@ -854,12 +858,11 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
         const uint32_t lastm = (n - 1 >= e0 && n - 1 < e0 + K) ? 1u << (n - 1 - e0) : 0u;
         const uint32_t endm = (diffm | lastm) & validm;
         const int L = gcount(endm);
-        uint64_t* kd = a.lvl_key ? a.lvl_key + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
-        uint8_t* wd = a.lvl_w ? a.lvl_w + (size_t)d * ((size_t)a.S * NBAR) : nullptr;
-        // the list reservation is issued here and its value first used after the
-        // compaction, the moments and the doc_pdf thresholds (the atomic's round trip)
-        uint32_t base = 0u;
-        if (!wide && kd && g == 0) base = atomicAdd(a.lvl_count + d, (uint32_t)L);
+        if (!wide && a.lvl_key) {
+          emitL = (uint32_t)L;
+          emitC = clastf;
+          emitB = cbase;
+        }
         if (!wide) {
           // Compact the levels (run ends, descending close) into LDS by level index:
           //   lv[l] = cumulative volume through level l (exact u32 when sum(v) < 2^32; a
@@ -929,20 +932,6 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
             if (Sv == 0u) e = 0;
             if (g < 5 && e < L) qv = fdiv_f32in(clastf, bitsf(cbase - (lc[e] >> 8)));
           }
-          if (kd) {  // doc_pdf level list: key c_last / close (correctly rounded), bars at the level
-            // levels interleaved over the group's lanes (level l from lane l % 16), so one
-            // store instruction writes 16 consecutive entries per group: 128 contiguous
-            // bytes of keys and 16 of weights (the lanes' own contiguous levels strided
-            // the stores 32 B apart: 3.1 ms of the 15 ms kernel)
-            base = bpermu(gb, base);
-            for (int l = g; l < L; l += 16) {
-              const uint32_t cwb = lc[l];
-              const uint32_t ee = cwb & 0xFFu;
-              const uint32_t ep = l > 0 ? (lc[l - 1] & 0xFFu) : 0xFFFFFFFFu;  // -1 before level 0
-              kd[base + l] = dbits(fdiv_f32in(clastf, bitsf(cbase - (cwb >> 8)))) | 0x8000000000000000ull;  // ord64 of a positive
-              wd[base + l] = (uint8_t)(ee - ep);
-            }
-          }
           lds_fence();
         }
         if (!fast && !wide && (fam & (a.fam_exact))) {
@@ -957,6 +946,23 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
           for (int t = 0; t < 5; ++t) R.null(PDF0 + t);  // filled by mff_pdf_finalize (or the fallback)
         }
       }
+    }
+
+    // ---------------------------------------------------------------- doc_pdf level list
+    // One reservation per wave for its four groups' levels: every stock-day of the block
+    // is day d, so one returning atomic per 4 stock-days on the day's counter instead of
+    // one per stock-day (5,000 serialized adds per day at c4: 1.3 ms of the kernel).
+    // Issued before the result stores, its value used after them.
+    const bool emit = a.lvl_key != nullptr;  // uniform
+    uint32_t lpre = 0u, lwb = 0u;
+    if (emit) {
+      const uint32_t l0 = (uint32_t)__builtin_amdgcn_readlane((int)emitL, 0);
+      const uint32_t l1 = (uint32_t)__builtin_amdgcn_readlane((int)emitL, 16);
+      const uint32_t l2 = (uint32_t)__builtin_amdgcn_readlane((int)emitL, 32);
+      const uint32_t l3 = (uint32_t)__builtin_amdgcn_readlane((int)emitL, 48);
+      lpre = grp == 0 ? 0u : grp == 1 ? l0 : grp == 2 ? l0 + l1 : l0 + l1 + l2;
+      const uint32_t tot = l0 + l1 + l2 + l3;
+      if (tot != 0u && lane == 0) lwb = atomicAdd(a.lvl_count + d, tot);
     }
 
     // ---------------------------------------------------------------- stores
@@ -975,6 +981,24 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
       if (a.pdfq && g < 5) {
         a.pdfq[(size_t)g * plane + sd] = qv;
       }
+    }
+    if (emit) {
+      // key c_last / close (correctly rounded), bars at the level; levels interleaved
+      // over the group's lanes (level l from lane l % 16), so one store instruction
+      // writes 16 consecutive entries per group: 128 contiguous bytes of keys and 16 of
+      // weights.  The levels are still in the group's scratch (lc, from the LVL section).
+      const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)lwb) + lpre;
+      const uint32_t* lc = reinterpret_cast<const uint32_t*>(scr) + NBAR;
+      uint64_t* kd = a.lvl_key + (size_t)d * ((size_t)a.S * NBAR);
+      uint8_t* wd = a.lvl_w + (size_t)d * ((size_t)a.S * NBAR);
+      for (int l = g; l < (int)emitL; l += 16) {
+        const uint32_t cwb = lc[l];
+        const uint32_t ee = cwb & 0xFFu;
+        const uint32_t ep = l > 0 ? (lc[l - 1] & 0xFFu) : 0xFFFFFFFFu;  // -1 before level 0
+        kd[base + l] = dbits(fdiv_f32in(emitC, bitsf(emitB - (cwb >> 8)))) | 0x8000000000000000ull;  // ord64 of a positive
+        wd[base + l] = (uint8_t)(ee - ep);
+      }
+      lds_fence();  // the next iteration rewrites the scratch
     }
   }
 }
