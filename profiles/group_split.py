@@ -30,7 +30,10 @@ def main():
     dev = torch.device("cuda:0")
     bars, mask = synth.make_panel_device(S, D, dev, config=4)
     panel = engine.DevicePanel(bars, mask)
+    only = os.environ.get("SPLIT_SET")
     for tag, names in SETS.items():
+        if only and tag != only:
+            continue
         ts = []
         for _ in range(4):
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
