@@ -346,6 +346,7 @@ def main():
     valu = valu_roofline(pmc, k_ms, S_loc * D)
 
     extras = {}
+    per_kernel = None
     if not args.no_extras:
         val, state, _ = step()
         torch.cuda.synchronize()
@@ -362,6 +363,14 @@ def main():
                 ts.append((time.perf_counter() - t) * 1e3)
             return float(np.median(ts))
         extras["stage1_pass_ms"] = round(k_ms, 3)
+        # each stage-1 launch alone (serial, HIP events on the launch stream): the
+        # per-kernel algorithmic GB/s against the HBM peak
+        kt = engine.stage1_launch_times(panel)
+        per_kernel = {k: {"ms": round(x["ms"], 3), "GBps": round(x["bytes"] / (x["ms"] * 1e-3) / 1e9, 1),
+                          "frac": round(x["bytes"] / (x["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                      for k, x in kt.items() if x["ms"] > 0}
+        per_kernel["serial_sum_ms"] = round(sum(x["ms"] for x in kt.values()), 3)
+        torch.cuda.synchronize()
         extras["step_ms_rank0"] = round(elapsed / args.steps * 1e3, 3)
         # algorithmic bytes of stage 2 / stage-3: 8 + 1 B in and out per (factor, day, stock)
         xs_bytes = 18.0 * val.numel()
@@ -426,6 +435,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_pmc_round": pmc.get("round") if pmc else None,
                 "traffic_calibrated": traffic_cal,
                 "valu": valu,
                 "kernel": "stage-1 pass over three streams: k_stage1s<OLS|MOMH> (own stream), "
@@ -435,6 +445,8 @@ def main():
                           "window = the whole pass",
                 "bytes_per_launch": bytes_launch,
                 "avg_kernel_ms": round(k_ms, 3),
+                # every launch of the pass alone (serial), algorithmic bytes / its own time
+                "kernels": per_kernel,
             },
             "cpu_baseline": cpu,
             "extras": extras,

@@ -268,6 +268,71 @@ def pdf_ranks_frame(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor
                "mff_pdf_finalize(frame)")
 
 
+def stage1_launch_times(panel: DevicePanel):
+    """The stage-1 launches of all 58 factors one after another on the current stream
+    (no overlap), each bracketed by HIP events: the per-kernel standalone durations and
+    algorithmic bytes bench.py reports beside the pass (the pass itself overlaps them on
+    three streams).  Returns {kernel: {"ms", "bytes"}}; bytes per stock-day are
+    SURVEY §8(d)'s: the mask (32 B) + 960 B per plane a kernel reads + 9 B per output row,
+    plus the doc_pdf side channel each doc_pdf launch reads or writes (queries 8 B x 5,
+    the level list 9 B per level, counted from the launch's own output)."""
+    lib = _lib.load()
+    ids = catalog.resolve(None)
+    nf, D, S = len(ids), panel.D, panel.S
+    dev = panel.device
+    st = torch.cuda.current_stream(dev)
+    val = torch.empty((nf, D, S), dtype=torch.float64, device=dev)
+    state = torch.empty((nf, D, S), dtype=torch.uint8, device=dev)
+    pdfq = torch.empty((5, D, S), dtype=torch.float64, device=dev)
+    levels = torch.empty(lib.mff_pdf_levels_bytes(S, D), dtype=torch.uint8, device=dev)
+    ws = torch.empty(lib.mff_stage1_workspace_bytes(S, D), dtype=torch.uint8, device=dev)
+    b = panel.bars
+    args = [_lib.ptr(b[0]), _lib.ptr(b[1]), _lib.ptr(b[2]), _lib.ptr(b[3]), _lib.ptr(b[4]),
+            _lib.ptr(panel.mask), S, D, _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
+            _lib.ptr(pdfq), _lib.ptr(levels), _lib.ptr(ws), st.cuda_stream]
+    rows = [ids.index(i) for i in catalog.PDF_IDS]
+    M = 5 * S
+    q_sorted = torch.empty((D, M), dtype=torch.int64, device=dev)
+    sws = torch.empty(lib.mff_pdf_workspace_bytes(S, 1, D), dtype=torch.uint8, device=dev)
+    steps = [
+        ("k_stage1g<ORD|ORDV|LVL|PDF>", lambda: _lib.check(lib.mff_stage1_part(*args, 17), "part 17")),
+        ("k_stage1 (exact list)", lambda: _lib.check(lib.mff_stage1_part(*args, 32), "part 32")),
+        ("k_pdf_sort", lambda: _lib.check(lib.mff_pdf_sort(_lib.ptr(pdfq), 1, S, D, 0, D, _lib.ptr(q_sorted),
+                                                            _lib.ptr(sws), st.cuda_stream), "sort")),
+        ("k_pdf_count<fused>", lambda: _lib.check(lib.mff_pdf_rank_local(
+            _lib.ptr(levels), _lib.ptr(pdfq), S, D, 0, D, _lib.ptr(q_sorted), M, _lib.int_array(rows),
+            _lib.ptr(val), _lib.ptr(state), st.cuda_stream), "rank_local")),
+        ("k_stage1s<OLS|MOMH>", lambda: _lib.check(lib.mff_stage1_part(*(args[:-1] + [st.cuda_stream]), 4),
+                                                   "part 4")),
+        ("k_stage1s_pair", lambda: _lib.check(lib.mff_stage1_part(*args, 10), "part 10")),
+    ]
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(steps) + 1)]
+    evs[0].record(st)
+    for i, (_, fn) in enumerate(steps):
+        fn()
+        evs[i + 1].record(st)
+    torch.cuda.synchronize(dev)
+    nlev = int(levels[:4 * D].view(torch.int32).to(torch.int64).sum().item())  # per-day entry counts
+    sd = S * D
+    fam_rows = {}
+    for i in ids:
+        fam_rows[catalog.FAMILY[catalog.NAMES[i]]] = fam_rows.get(catalog.FAMILY[catalog.NAMES[i]], 0) + 1
+    nrows = lambda fams: sum(fam_rows.get(f, 0) for f in fams)
+    plane = 960
+    bytes_ = {
+        # c, v planes + mask; ORD / ORDV / LVL rows and the five doc_pdf rows (NULL, filled
+        # later); the queries; the level list (key 8 B + bars 1 B)
+        "k_stage1g<ORD|ORDV|LVL|PDF>": sd * (32 + 2 * plane + 9 * (nrows(("ORDV", "LVL")) + 5) + 40) + 9 * nlev,
+        "k_stage1 (exact list)": 0,
+        "k_pdf_sort": sd * (40 + 40),
+        "k_pdf_count<fused>": 9 * nlev + sd * (40 + 40 + 9 * 5),
+        "k_stage1s<OLS|MOMH>": sd * (32 + 2 * plane + 9 * nrows(("OLS", "MOMH"))),
+        "k_stage1s_pair": sd * (32 + 3 * plane + 9 * (nf - nrows(("ORDV", "LVL", "PDF", "OLS", "MOMH"))) + 12),
+    }
+    return {name: {"ms": evs[i].elapsed_time(evs[i + 1]), "bytes": bytes_[name]}
+            for i, (name, _) in enumerate(steps)}
+
+
 class PdfKernels:
     """The device phases of the stock-sharded doc_pdf rank (libmff, this rank's stream).
     `_pdf_ranks_sharded` only moves tensors between these phases and the collectives, so
