@@ -191,6 +191,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   const float* C = a.fld[3] + sd * NBAR;
   const uint32_t* V = reinterpret_cast<const uint32_t*>(a.fld[4]) + sd * NBAR;
 
+  // sets with an all-present form of the bar walk
+  constexpr bool kAllpSet = (SET == kSerA && MFF_SERA_FAST) || (PAIR && SET == kPairA && MFF_SERA_FAST) ||
+                            (PAIR && SET == kPairB && MFF_SERB_FAST);
+
   // ---------------------------------------------------------------- shifts
   double x0r = 0.0, x0v = 0.0;
   double x1 = 0, xc = 0, yv = 0;
@@ -444,7 +448,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   struct Q4 {
     float4 o, h, l, c, v;
   };
-  auto quad = [&](int m0, uint32_t pm, uint32_t lm, const Q4& x, const float4& lh0, const float4& ll0,
+  // full: every lane of the wave has all 240 bars (or none): the whole walk takes the
+  // all-present form, with no per-quad test and no join between the two forms (the join
+  // copied every accumulator into the general form's registers after each quad)
+  auto quad = [&](auto full, int m0, uint32_t pm, uint32_t lm, const Q4& x, const float4& lh0, const float4& ll0,
                   const float4& lh1, const float4& ll1) {
     // lagged bars: m0-50, m0-49 = (lh0, ll0).z .w; m0-48, m0-47 = (lh1, ll1).x .y
     if (fam & kSerH) {
@@ -459,9 +466,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       // ABSENT whatever they accumulated
       // (set A, and set B in the pair form, where it has set A's register budget; set B's
       // own kernel has no room for the second copy)
-      if (((SET == kSerA && MFF_SERA_FAST) || (PAIR && SET == kPairA && MFF_SERA_FAST) ||
-           (PAIR && SET == kPairB && MFF_SERB_FAST)) &&
-          __builtin_amdgcn_ballot_w64((pm & 0xFu) != 0xFu && n > 0) == 0ull) {
+      if (kAllpSet && (decltype(full)::value || __builtin_amdgcn_ballot_w64((pm & 0xFu) != 0xFu && n > 0) == 0ull)) {
         const std::true_type all;
         bar(m0 + 0, true, x.o.x, x.c.x, x.v.x, all);
         bar(m0 + 1, true, x.o.y, x.c.y, x.v.y, all);
@@ -552,7 +557,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     carry.o = carry.h = carry.l = carry.c = one4;
     carry.v = zero4;
     uint32_t pw1 = 0u, pw2 = 0u;  // mask words w-1, w-2
-    auto step = [&](float4(*sb)[64 * CQ], int c, int h, uint32_t bits, uint32_t lbits) {
+    auto step = [&](auto full, float4(*sb)[64 * CQ], int c, int h, uint32_t bits, uint32_t lbits) {
       float4 X[NB][CQ];
       if constexpr (PAIR && MFF_PAIR_QREAD) {
         // as below, but the DMA of chunk c+1 goes out first and the chunk is read one quad
@@ -574,7 +579,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
 #pragma unroll
           for (int ii = 0; ii < NB; ++ii) Z[ii][0] = Y[k & 1][ii];
           __builtin_amdgcn_sched_barrier(0);
-          quad(BC * c + 4 * k, bits >> (BC * h + 4 * k), 0u, toq(Z, 0, 0), one4, one4, one4, one4);
+          quad(full, BC * c + 4 * k, bits >> (BC * h + 4 * k), 0u, toq(Z, 0, 0), one4, one4, one4, one4);
           __builtin_amdgcn_sched_barrier(0);
         }
         return;
@@ -627,29 +632,35 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         if constexpr (LAG) {
           const Q4 l1 = toq(X, NP, k);
           const Q4 l0 = k > 0 ? toq(X, NP, k - 1) : carry;
-          quad(BC * c + 4 * k, bits >> (BC * h + 4 * k), lbits >> (BC * h + 4 * k), x, l0.h, l0.l, l1.h, l1.l);
+          quad(full, BC * c + 4 * k, bits >> (BC * h + 4 * k), lbits >> (BC * h + 4 * k), x, l0.h, l0.l, l1.h, l1.l);
         } else {
-          quad(BC * c + 4 * k, bits >> (BC * h + 4 * k), 0u, x, one4, one4, one4, one4);
+          quad(full, BC * c + 4 * k, bits >> (BC * h + 4 * k), 0u, x, one4, one4, one4, one4);
         }
       }
       if constexpr (LAG) carry = toq(X, NP, CQ - 1);
     };
-    dma(sbA, 0, 0);
-    if constexpr (NBUF == 2) dma(sbB, 1, 0);
-    for (int w = 0; w < 8; ++w) {
-      const uint32_t bits = mw[0];
-      const uint32_t lbits = (pw1 << 18) | (pw2 >> 14);  // bit i: bar 32w + i - 50
-      const int nc = (w == 7 ? 16 : 32) / BC;            // bars 224..239: half a word
-      for (int h = 0; h < nc; h += NBUF) {
-        const int c = (32 / BC) * w + h;
-        step(sbA, c, h, bits, lbits);
-        if constexpr (NBUF == 2) step(sbB, c + 1, h + 1, bits, lbits);
-      }
+    auto walk = [&](auto full) {
+      dma(sbA, 0, 0);
+      if constexpr (NBUF == 2) dma(sbB, 1, 0);
+      for (int w = 0; w < 8; ++w) {
+        const uint32_t bits = mw[0];
+        const uint32_t lbits = (pw1 << 18) | (pw2 >> 14);  // bit i: bar 32w + i - 50
+        const int nc = (w == 7 ? 16 : 32) / BC;            // bars 224..239: half a word
+        for (int h = 0; h < nc; h += NBUF) {
+          const int c = (32 / BC) * w + h;
+          step(full, sbA, c, h, bits, lbits);
+          if constexpr (NBUF == 2) step(full, sbB, c + 1, h + 1, bits, lbits);
+        }
 #pragma unroll
-      for (int i = 0; i < 7; ++i) mw[i] = mw[i + 1];
-      pw2 = pw1;
-      pw1 = bits;
-    }
+        for (int i = 0; i < 7; ++i) mw[i] = mw[i + 1];
+        pw2 = pw1;
+        pw1 = bits;
+      }
+    };
+    // the pair's two waves walk the same stock-days, so they take the same branch (and
+    // pass the same barriers either way)
+    if (kAllpSet && __builtin_amdgcn_ballot_w64(n > 0 && n != NBAR) == 0ull) walk(std::true_type());
+    else walk(std::false_type());
   }
 
   // ---------------------------------------------------------------- finishing
