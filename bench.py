@@ -24,7 +24,9 @@ the committed rocprofv3 PMC passes (profiles/pmc_stage1.json: FETCH_SIZE x 2 per
 gfx950 correction + WRITE_SIZE, summed over the launches), or null; traffic_calibrated:
 the same with the LDS-DMA kernels' factor measured by profiles/ubench/rowload.hip.
 valu: the issue side from the same PMC passes (VALU wave-instructions per stock-day,
-f64 share, fraction of the chip's VALU issue cycles) -- what actually binds the pass.
+f64 share, fraction of the VALU pipe-cycles busy: ~0.8 over the pass, 0.8-0.9 in the
+three stage-1 kernels) -- what actually binds the pass.  kernels: every launch of the
+pass alone (serial), its algorithmic bytes over its own duration.
 
 cpu_baseline: the CPU oracle (oracle/mff_oracle.py, a numpy restatement of the reference
 cal_* functions) timed on this host, rank 0 at N=1, on a bounded sample of the same
@@ -87,9 +89,12 @@ def cpu_baseline(days: int, stocks: int, workers: int):
 
 def valu_roofline(pmc, k_ms: float, stock_days: int):
     """The issue side of the pass from the committed PMC passes (profiles/pmc_stage1.json):
-    VALU wave-instructions per stock-day and the fraction of the chip's VALU issue
-    cycles they occupy (wave64 on a 32-lane SIMD: 2 cycles for 32-bit ops, 4 for f64 ops
-    at the 16-lane f64 rate; 1,024 SIMDs at 2.4 GHz)."""
+    VALU wave-instructions per stock-day, their f64 share, and the fraction of the
+    chip's VALU pipe-cycles busy over the pass: SQ_ACTIVE_INST_VALU (quad-cycles, summed
+    over waves: a SIMD's VALU serves one wave at a time) x 4 / (1,024 SIMDs x the
+    cycles the GPU was busy, GRBM_GUI_ACTIVE / 8 XCDs), both from the same profiled run.
+    Per kernel: the same with the kernel's own counters (the launches overlap in the
+    pass, so these are upper bounds of what each kernel leaves idle)."""
     if not pmc:
         return None
     sq = pmc.get("sq", {})
@@ -98,10 +103,15 @@ def valu_roofline(pmc, k_ms: float, stock_days: int):
         return None
     f64 = sum(sq.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
                                         "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
-    cyc = 2.0 * (n - f64) + 4.0 * f64
+
+    def busy(cs):
+        g, a = cs.get("GRBM_GUI_ACTIVE"), cs.get("SQ_ACTIVE_INST_VALU")
+        return round(4.0 * a / (1024 * g / 8.0), 3) if g and a else None
     return {"valu_instr_per_stock_day": round(n / stock_days, 1),
             "f64_share": round(f64 / n, 3),
-            "issue_frac": round(cyc / (1024 * 2.4e9 * k_ms * 1e-3), 3),
+            "valu_busy": busy(sq),
+            "per_kernel": {k: {"valu_per_stock_day": e.get("valu_per_stock_day"), "valu_busy": busy(e)}
+                           for k, e in pmc.get("per_kernel", {}).items()},
             "pmc_round": pmc.get("round")}
 
 
