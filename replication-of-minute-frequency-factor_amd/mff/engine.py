@@ -222,7 +222,13 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
     M = R * 5 * S_all
     st = _stream(dev)
     if comm is not None:
-        _pdf_ranks_sharded(comm, pdfq, S_all, PdfKernels(lib, levels, S, D, rows, val, state, st))
+        if day_batch is None:
+            # per day of a window: gathered + sorted lists (i64), counts + their copy by
+            # owner (i32), the sort's ping-pong buffer
+            per_day = 2 * M * 8 + 2 * M * 4 + lib.mff_pdf_workspace_bytes(S_all, R, 1)
+            day_batch = max(1, workspace_budget // max(per_day, 1))
+        _pdf_ranks_sharded(comm, pdfq, S_all, PdfKernels(lib, levels, S, D, rows, val, state, st),
+                           day_batch=day_batch)
         return
     if day_batch is None:
         per_day = lib.mff_pdf_workspace_bytes(S, R, 1) + M * 8 + M * 8
@@ -352,13 +358,14 @@ class PdfKernels:
                                     _lib.ptr(ws), self.st), "mff_pdf_sort")
         return out
 
-    def count(self, q_sorted):
-        """This rank's level keys against every day's full sorted list: int32 [D][M] =
-        2 n_less + n_eq at each value's first sorted position."""
-        D, M = q_sorted.shape
-        counts = torch.empty((D, M), dtype=torch.int32, device=q_sorted.device)
+    def count(self, q_sorted, d0: int = 0):
+        """This rank's level keys of days d0 .. d0 + nd against each of those days' full
+        sorted list (q_sorted [nd][M]): int32 [nd][M] = 2 n_less + n_eq at each value's
+        first sorted position."""
+        nd, M = q_sorted.shape
+        counts = torch.empty((nd, M), dtype=torch.int32, device=q_sorted.device)
         ws = torch.empty(256, dtype=torch.uint8, device=q_sorted.device)
-        _lib.check(self.lib.mff_pdf_count(_lib.ptr(self.levels), self.S, self.D, 0, D, _lib.ptr(q_sorted), M,
+        _lib.check(self.lib.mff_pdf_count(_lib.ptr(self.levels), self.S, self.D, d0, nd, _lib.ptr(q_sorted), M,
                                           _lib.ptr(counts), _lib.ptr(ws), self.st), "mff_pdf_count")
         return counts
 
@@ -379,20 +386,22 @@ class PdfKernels:
                                                  _lib.ptr(self.state), self.st), "mff_pdf_finalize_own")
 
 
-def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern):
-    """doc_pdf across stock shards.  Day d is owned by the rank whose
-    contiguous day block holds it:
+def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern, day_batch: Optional[int] = None):
+    """doc_pdf across stock shards.  The days go in windows of at most
+    ``day_batch`` x R days (the exchange buffers below are O(window x M) per rank; None:
+    one window); inside a window, day d is owned by the rank whose contiguous day block
+    holds it:
       1. all_to_all: every rank's queries of the owner's days -> the owner, which sorts
          them (the sort is not replicated: 1/R of the days per rank);
-      2. all_gather of the sorted day lists [D][M];
-      3. every rank counts its own level keys against each day's full list -> [D][M]
+      2. all_gather of the sorted day lists [W][M];
+      3. every rank counts its own level keys against each day's full list -> [W][M]
          (one word per sorted query, 2 n_less + n_eq: linear in the average rank);
       4. reduce_scatter (sum) of the counts by day block: each owner gets its days' totals;
       5. the owner looks every query of its days up (origin layout) and one all_to_all
-         returns each rank the counts of its own queries; each rank finalizes its
-         stock-days (rank = (c + 1) / 2).
-    Only step 2 moves O(D x M) bytes per rank; step 4 replaces a ring all-reduce of the
-    whole [D][M] (2x the bytes per rank on a link-bound ring).  pdfq: [5][D][S_loc]."""
+         returns each rank the counts of its own queries.
+    Each rank then finalizes its stock-days (rank = (c + 1) / 2) once for all windows.
+    Only step 2 moves O(W x M) bytes per rank; step 4 replaces a ring all-reduce of the
+    whole [W][M] (2x the bytes per rank on a link-bound ring).  pdfq: [5][D][S_loc]."""
     from .dist import shard_bounds
 
     D = int(pdfq.shape[1])
@@ -400,36 +409,40 @@ def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern):
     dev = pdfq.device
     R, rank = comm.world_size, comm.rank
     M = R * 5 * S_all
-    blocks = [shard_bounds(D, R, r) for r in range(R)]
-    nd_max = max(1, max(b1 - b0 for b0, b1 in blocks))
+    W = D if day_batch is None else max(1, min(D, int(day_batch) * R))
     q_pad = _pad_last(pdfq, S_all, float("nan"))  # [5][D][S_all]
-    send = torch.full((R, 5, nd_max, S_all), float("nan"), dtype=torch.float64, device=dev)
-    for r, (b0, b1) in enumerate(blocks):
-        send[r, :, :b1 - b0] = q_pad[:, b0:b1]
-    recv = comm.all_to_all(send)  # [R][5][nd_max][S_all]: every rank's queries of my days
-    del send, q_pad
-    b0, b1 = blocks[rank]
-    nd = b1 - b0
-    mine = torch.zeros((nd_max, M), dtype=torch.int64, device=dev)
-    if nd > 0:
-        mine[:nd] = kern.sort(recv, R, S_all, nd)
-    gathered = comm.all_gather(mine)  # [R][nd_max][M]
-    q_sorted = torch.cat([gathered[r, :e - s] for r, (s, e) in enumerate(blocks)])  # [D][M]
-    del gathered
-    counts = kern.count(q_sorted)  # [D][M], this rank's keys
-    del q_sorted
-    cs = torch.zeros((R, nd_max, M), dtype=torch.int32, device=dev)
-    for r, (s, e) in enumerate(blocks):
-        cs[r, :e - s] = counts[s:e]
-    del counts
-    my_counts = comm.reduce_scatter_sum(cs)  # [nd_max][M], summed over ranks
-    del cs
-    origin = kern.origin(recv, R, S_all, mine, my_counts)  # [R][5][nd_max][S_all]
-    back = comm.all_to_all(origin)  # slice r: my queries' counts on rank r's days
-    del origin, recv, mine, my_counts
-    own = torch.empty((5, D, S_loc), dtype=torch.int32, device=dev)
-    for r, (s, e) in enumerate(blocks):
-        own[:, s:e] = back[r, :, :e - s, :S_loc]
+    own = torch.zeros((5, D, S_loc), dtype=torch.int32, device=dev)
+    for w0 in range(0, D, W):  # every rank walks the same windows (same D, same W)
+        w1 = min(D, w0 + W)
+        blocks = [tuple(w0 + x for x in shard_bounds(w1 - w0, R, r)) for r in range(R)]
+        nd_max = max(1, max(b1 - b0 for b0, b1 in blocks))
+        send = torch.full((R, 5, nd_max, S_all), float("nan"), dtype=torch.float64, device=dev)
+        for r, (b0, b1) in enumerate(blocks):
+            send[r, :, :b1 - b0] = q_pad[:, b0:b1]
+        recv = comm.all_to_all(send)  # [R][5][nd_max][S_all]: every rank's queries of my days
+        del send
+        b0, b1 = blocks[rank]
+        nd = b1 - b0
+        mine = torch.zeros((nd_max, M), dtype=torch.int64, device=dev)
+        if nd > 0:
+            mine[:nd] = kern.sort(recv, R, S_all, nd)
+        gathered = comm.all_gather(mine)  # [R][nd_max][M]
+        q_sorted = torch.cat([gathered[r, :e - s] for r, (s, e) in enumerate(blocks)])  # [W][M]
+        del gathered
+        counts = kern.count(q_sorted, w0)  # [W][M], this rank's keys
+        del q_sorted
+        cs = torch.zeros((R, nd_max, M), dtype=torch.int32, device=dev)
+        for r, (s, e) in enumerate(blocks):
+            cs[r, :e - s] = counts[s - w0:e - w0]
+        del counts
+        my_counts = comm.reduce_scatter_sum(cs)  # [nd_max][M], summed over ranks
+        del cs
+        origin = kern.origin(recv, R, S_all, mine, my_counts)  # [R][5][nd_max][S_all]
+        back = comm.all_to_all(origin)  # slice r: my queries' counts on rank r's days
+        del origin, recv, mine, my_counts
+        for r, (s, e) in enumerate(blocks):
+            own[:, s:e] = back[r, :, :e - s, :S_loc]
+        del back
     kern.finalize(pdfq, own)
 
 

@@ -189,12 +189,12 @@ class _NumpyPdf:
         out = np.sort(_ord64(np.moveaxis(a, 2, 0).reshape(nd, -1)), axis=1)
         return torch.from_numpy(out.view(np.int64).copy())
 
-    def count(self, q_sorted):
+    def count(self, q_sorted, d0=0):
         import numpy as np
         qs = q_sorted.numpy().view(np.uint64)
         out = np.zeros(qs.shape, np.int32)
         for d in range(qs.shape[0]):
-            k = self.keys[d]
+            k = self.keys[d0 + d]
             lt = np.searchsorted(k, qs[d], side="left")
             le = np.searchsorted(k, qs[d], side="right")
             out[d] = 2 * lt + (le - lt)
@@ -221,7 +221,7 @@ class _NumpyPdf:
             self.state[r][ok] = 2
 
 
-def _pdf_worker(rank, world, port, resq):
+def _pdf_worker(rank, world, port, resq, day_batch=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import sys
@@ -239,20 +239,21 @@ def _pdf_worker(rank, world, port, resq):
     val = np.zeros((5, 5, s1 - s0))
     state = np.zeros((5, 5, s1 - s0), np.uint8)
     S_all = engine._agreed_max(comm, s1 - s0, torch.device("cpu"))
-    engine._pdf_ranks_sharded(comm, q, S_all, _NumpyPdf(sub, val, state, list(range(5))))
+    engine._pdf_ranks_sharded(comm, q, S_all, _NumpyPdf(sub, val, state, list(range(5))), day_batch=day_batch)
     comm.barrier()
     dist_.destroy_process_group()
     resq.put((rank, (val, state)))
 
 
-def test_gloo_sharded_doc_pdf_exchange_world2():
+@pytest.mark.parametrize("day_batch", [None, 1])  # one window / windows of 2 days (5 = 2 + 2 + 1)
+def test_gloo_sharded_doc_pdf_exchange_world2(day_batch):
     import numpy as np
     import mff_oracle as O
     from mff import synth
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_pdf_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_pdf_worker, args=(r, 2, port, q, day_batch)) for r in range(2)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=180) for _ in ps)
