@@ -209,6 +209,191 @@ __device__ __forceinline__ void sort_walk(const Loader& ld, int tid, int nt, F&&
 constexpr int SORT_NBIN = 2048;
 constexpr int SORT_CAPB = 8192;  // keys per range (with the bins: 72 KiB of LDS, two workgroups per CU)
 constexpr int SORT_REG = 32;  // segment_sort_binned takes M <= SORT_REG * blockDim
+
+// Rank placement of one range (segment_sort_binned): the range's keys sit in LDS grouped
+// by day bin; each bin is cut into sub-buckets in proportion to its count (histogram
+// equalisation over RS_NS sub-buckets per range, linear in the key inside the bin), the
+// keys are scattered by sub-bucket, the key that took a sub-bucket's slot 0 is its
+// reference (keys equal to it are only counted: the doc_pdf queries hold long exact ties,
+// e.g. the level 1.0), the other keys are packed behind the reference run, and every key
+// writes itself to its final position: sub-bucket start + #smaller keys in the sub-bucket
+// + its index among the equal ones.  About 10 block phases per range instead of the 91
+// stages of a 8192-key bitonic network.  A sub-bucket with more than RS_MAXO keys that
+// differ from its reference (or a range over more than RS_NS bins) returns false with the
+// keys back in sk[0, size) for the bitonic.  The tables use sk's top slots, so a range
+// holds at most RS_CAP keys on this path.
+#ifndef MFF_SORT_RANK
+#define MFF_SORT_RANK 1
+#endif
+constexpr int RS_NS = 1024;    // sub-buckets per range
+constexpr int RS_MAXO = 48;    // non-reference keys per sub-bucket
+constexpr int RS_CAP = SORT_CAPB - (RS_NS * 4 + 3 * RS_NS * 2) / 8;  // 6912: tables in sk[RS_CAP, SORT_CAPB)
+constexpr int RS_KP = (RS_CAP + SORT_THREADS - 1) / SORT_THREADS;     // keys per thread (7)
+
+__device__ __forceinline__ uint32_t rs_get16(const uint32_t* w, uint32_t i) { return (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; }
+__device__ __forceinline__ uint32_t rs_inc16(uint32_t* w, uint32_t i) {
+  return (atomicAdd(&w[i >> 1], 1u << (16 * (i & 1))) >> (16 * (i & 1))) & 0xFFFFu;
+}
+// exclusive scan of one u32 per thread over a 1024-thread block; *total = the sum; ends synced
+__device__ __forceinline__ uint32_t rs_scan(uint32_t x, uint32_t* wsum, uint32_t* total) {
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6;
+  uint32_t incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t off = incl - x, tot = 0u;
+#pragma unroll
+  for (int w = 0; w < SORT_THREADS / 64; ++w) {
+    off += w < wave ? wsum[w] : 0u;
+    tot += wsum[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return off;
+}
+
+// keys of bins [b0, b1) in sk[0, size), bin b at [st(b), bins[b]) - base where st(b0) = base,
+// st(b) = bins[b - 1] (segment_sort_binned's cursors after the placement); writes
+// out[base + position].  Requires blockDim.x == SORT_THREADS.
+__device__ bool range_rank_sort(uint64_t* sk, const uint32_t* bins, int b0, int b1, uint32_t base,
+                                uint32_t size, uint64_t kmin, int sh, uint64_t* out) {
+  __shared__ uint32_t rs_wsum[SORT_THREADS / 64];
+  __shared__ uint32_t rs_max;
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  const int nb = b1 - b0;
+  if (nb > RS_NS || size > (uint32_t)RS_CAP) return false;  // block-uniform; sk untouched
+  uint32_t* sbn = reinterpret_cast<uint32_t*>(sk + RS_CAP);  // [RS_NS] bin's first sub-bucket | count << 16
+  uint32_t* cnt = sbn + RS_NS;                                // [RS_NS / 2] counts, then starts (u16 pairs)
+  uint32_t* eqc = cnt + RS_NS / 2;                            // [RS_NS / 2] keys equal to the reference
+  uint32_t* ctr = eqc + RS_NS / 2;                            // [RS_NS / 2] pack cursors
+  uint64_t x[RS_KP];
+  uint32_t bp[RS_KP], ej[RS_KP];  // sub-bucket << 16 | slot; index among the equal keys / packed slot
+  uint32_t isref = 0u;
+#pragma unroll
+  for (int j = 0; j < RS_KP; ++j) {
+    const int i = tid + j * SORT_THREADS;
+    x[j] = i < (int)size ? sk[i] : ~0ull;
+  }
+  // sub-buckets per bin: 1 + c (RS_NS - nb) / size (sum <= RS_NS), one bin per thread
+  uint32_t nsb = 0u;
+  if (tid < nb) {
+    const int b = b0 + tid;
+    const uint32_t c = bins[b] - (b == b0 ? base : bins[b - 1]);
+    nsb = c ? 1u + (c * (uint32_t)(RS_NS - nb)) / size : 0u;
+  }
+  uint32_t tot;
+  const uint32_t sb0 = rs_scan(nsb, rs_wsum, &tot);  // ends synced: every key is in registers
+  if (tid < nb) sbn[tid] = sb0 | (nsb << 16);
+  if (tid < RS_NS / 2) {
+    cnt[tid] = 0u;
+    eqc[tid] = 0u;
+    ctr[tid] = 0u;
+  }
+  if (tid == 0) rs_max = 0u;
+  __syncthreads();
+  // histogram: slot in the sub-bucket
+#pragma unroll
+  for (int j = 0; j < RS_KP; ++j) {
+    bp[j] = 0u;
+    if (tid + j * SORT_THREADS < (int)size) {
+      const uint64_t o = x[j] - kmin;
+      const uint32_t b = (uint32_t)(o >> sh);
+      const uint32_t t = sbn[b - (uint32_t)b0], n = t >> 16;
+      const uint64_t ob = o - ((uint64_t)b << sh);  // < 2^sh
+      const uint32_t f = (uint32_t)(sh >= 10 ? ob >> (sh - 10) : ob << (10 - sh));  // < 1024, monotone
+      const uint32_t sb = (t & 0xFFFFu) + min(n - 1u, (f * n) >> 10);
+      bp[j] = (sb << 16) | rs_inc16(cnt, sb);
+    }
+  }
+  __syncthreads();
+  // counts -> starts: thread w < RS_NS / 2 owns the word of sub-buckets 2w, 2w + 1
+  {
+    const uint32_t w = tid < RS_NS / 2 ? cnt[tid] : 0u;
+    const uint32_t c0 = w & 0xFFFFu, c1 = w >> 16;
+    uint32_t all;
+    const uint32_t off = rs_scan(c0 + c1, rs_wsum, &all);
+    if (tid < RS_NS / 2) cnt[tid] = off | ((off + c0) << 16);
+  }
+  __syncthreads();
+  // scatter: the key at a sub-bucket's slot 0 is its reference
+#pragma unroll
+  for (int j = 0; j < RS_KP; ++j)
+    if (tid + j * SORT_THREADS < (int)size) sk[rs_get16(cnt, bp[j] >> 16) + (bp[j] & 0xFFFFu)] = x[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RS_KP; ++j) {
+    ej[j] = 0u;
+    if (tid + j * SORT_THREADS < (int)size) {
+      const uint32_t sb = bp[j] >> 16;
+      if (sk[rs_get16(cnt, sb)] == x[j]) {
+        isref |= 1u << j;
+        ej[j] = rs_inc16(eqc, sb);
+      }
+    }
+  }
+  __syncthreads();
+  // the fullest sub-bucket's non-reference keys decide
+  {
+    uint32_t mo = 0u;
+    if (tid < RS_NS / 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t sb = 2u * (uint32_t)tid + h;
+        const uint32_t s1 = sb + 1 < (uint32_t)RS_NS ? rs_get16(cnt, sb + 1) : size;
+        mo = max(mo, s1 - rs_get16(cnt, sb) - rs_get16(eqc, sb));
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mo = max(mo, (uint32_t)__shfl_xor((int)mo, o, 64));
+    if (lane == 0) atomicMax(&rs_max, mo);
+  }
+  __syncthreads();
+  if (rs_max > (uint32_t)RS_MAXO) {  // block-uniform: back to element order for the bitonic
+#pragma unroll
+    for (int j = 0; j < RS_KP; ++j) {
+      const int i = tid + j * SORT_THREADS;
+      if (i < (int)size) sk[i] = x[j];
+    }
+    __syncthreads();
+    return false;
+  }
+  // pack the non-reference keys behind the reference run (slot 0 keeps the reference)
+#pragma unroll
+  for (int j = 0; j < RS_KP; ++j) {
+    if (tid + j * SORT_THREADS < (int)size && !((isref >> j) & 1u)) {
+      const uint32_t sb = bp[j] >> 16;
+      ej[j] = rs_get16(cnt, sb) + rs_get16(eqc, sb) + rs_inc16(ctr, sb);
+      sk[ej[j]] = x[j];
+    }
+  }
+  __syncthreads();
+  // final positions: #smaller non-reference keys, the reference run if smaller, and the
+  // index among the equal keys (references: their eqc ticket; others: equal packed keys
+  // at lower slots)
+#pragma unroll
+  for (int j = 0; j < RS_KP; ++j) {
+    if (tid + j * SORT_THREADS < (int)size) {
+      const uint32_t sb = bp[j] >> 16;
+      const uint32_t st = rs_get16(cnt, sb), e = rs_get16(eqc, sb);
+      const uint32_t en = sb + 1 < (uint32_t)RS_NS ? rs_get16(cnt, sb + 1) : size;
+      const bool rf = (isref >> j) & 1u;
+      const uint64_t kk = x[j];
+      uint32_t less = 0u, eqb = 0u;
+      for (uint32_t q = st + e; q < en; ++q) {
+        const uint64_t y = sk[q];
+        less += y < kk ? 1u : 0u;
+        eqb += (!rf && y == kk && q < ej[j]) ? 1u : 0u;
+      }
+      const uint32_t pos = rf ? st + less + ej[j] : st + less + (sk[st] < kk ? e : 0u) + eqb;
+      out[base + pos] = kk;
+    }
+  }
+  return true;
+}
 template <typename Loader>
 __device__ bool segment_sort_binned(const Loader& ld, int M, uint64_t* out, uint64_t* sk, uint32_t* bins,
                                     uint32_t* ctl) {
@@ -275,7 +460,9 @@ __device__ bool segment_sort_binned(const Loader& ld, int M, uint64_t* out, uint
   }
   if (tid == 0) bins[SORT_NBIN] = tot;
   // ranges: bin b belongs to range start[b] / T (T + maxbin <= SORT_CAPB)
-  const uint32_t T = (uint32_t)SORT_CAPB - maxbin;
+  // the rank placement takes ranges of at most RS_CAP keys (its tables use sk's top)
+  const uint32_t cap = MFF_SORT_RANK && maxbin <= (uint32_t)RS_CAP / 2 ? (uint32_t)RS_CAP : (uint32_t)SORT_CAPB;
+  const uint32_t T = cap - maxbin;
   int* rbeg = reinterpret_cast<int*>(ctl + 32);  // [32] first bin of each range, -1 = empty
   if (tid < 32) rbeg[tid] = -1;
   __syncthreads();
@@ -296,14 +483,21 @@ __device__ bool segment_sort_binned(const Loader& ld, int M, uint64_t* out, uint
     int P = 2048;
     while (P < (int)size) P <<= 1;
     __syncthreads();  // the previous range's readers are done with sk
-    for (int i = tid; i < P; i += nt) sk[i] = ~0ull;
-    __syncthreads();
+    if (!MFF_SORT_RANK) {
+      for (int i = tid; i < P; i += nt) sk[i] = ~0ull;
+      __syncthreads();
+    }
     sort_walk(ld, tid, nt, [&](uint64_t k) {
       if (k == ~0ull) return;
       const int b = (int)((k - kmin) >> sh);
       if (b >= b0 && b < b1) sk[atomicAdd(&bins[b], 1u) - base] = k;
     });
     __syncthreads();
+    if (MFF_SORT_RANK && range_rank_sort(sk, bins, b0, b1, base, size, kmin, sh, out)) continue;
+    if (MFF_SORT_RANK) {  // the bitonic's padding (the rank path's tables may sit there)
+      for (int i = (int)size + tid; i < P; i += nt) sk[i] = ~0ull;
+      __syncthreads();
+    }
     switch (P) {
       case 2048: bitonic_regs<2>(sk); break;
       case 4096: bitonic_regs<4>(sk); break;

@@ -120,7 +120,7 @@ def test_stage1_level_fallback_and_off_tick(dev):
 
 
 def test_doc_pdf_merge_path(dev):
-    """M = 5*S = 8,500 > 8,192 queries per day: the sort finishes with a global merge pass."""
+    """M = 5*S = 8,500 queries per day: more than one LDS range of the bucketed sort."""
     import mff_oracle as O
     from mff import synth
     panel = synth.make_panel(1700, 1, config=12)
