@@ -33,7 +33,7 @@ SCHEDULES = [
     {"EXACT_SIDE": False},
     {"PDF_OVERLAP": False},
     {"PDF_FIRST": True},
-    {"SORT_FIRST": True},
+    {"SORT_FIRST": False},
     {"HL_STREAM": False},
     {"HL_AT": "part1"},
     {"PDF_FIRST": True, "HL_AT": "pdf"},
