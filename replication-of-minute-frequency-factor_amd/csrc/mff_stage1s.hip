@@ -79,6 +79,9 @@ constexpr uint32_t kPairB = MFF_PAIR_SPLIT ? (F_SUMC | F_CORR) : kSerB;
 #ifndef MFF_SERB_FAST
 #define MFF_SERB_FAST 1
 #endif
+#ifndef MFF_SERH_FAST
+#define MFF_SERH_FAST 1
+#endif
 #ifndef MFF_CAPTURE_BRANCH
 #define MFF_CAPTURE_BRANCH 0
 #endif
@@ -280,13 +283,27 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   // MOMH
   double hs1 = 0, hs2 = 0;
 
-  auto olsbar = [&](int m, bool pk, float hf, float lf, bool lpk, float lhf, float llf) {
+  // ALLP (the full-wave walk: every lane has all 240 bars, or none): bar m is present, bar
+  // m - 50 leaves the window from m = 50 on, and window m is complete from m = 49 on, all
+  // wave-uniform tests of m instead of per-lane masks and counters
+  auto olsbar = [&](int m, bool pk, float hf, float lf, bool lpk, float lhf, float llf, auto allp) {
+    constexpr bool ALLP = decltype(allp)::value;
+    if (ALLP) {
+      pk = true;
+      lpk = m >= 50;
+    }
     if (pk) {
       if (fam & F_OLS) {
         const double dx = (double)lf - x0, dy = (double)hf - y0;
-        Rx += dx; Ry += dy; Rxx += dx * dx; Ryy += dy * dy; Rxy += dx * dy; ++cR;
-        if (hph && lf != plo) lcx = m;
-        if (hph && hf != phi) lcy = m;
+        Rx += dx; Ry += dy; Rxx += dx * dx; Ryy += dy * dy; Rxy += dx * dy;
+        if (!ALLP) ++cR;
+        if (ALLP) {
+          lcx = (m > 0 && lf != plo) ? m : lcx;
+          lcy = (m > 0 && hf != phi) ? m : lcy;
+        } else {
+          if (hph && lf != plo) lcx = m;
+          if (hph && hf != phi) lcy = m;
+        }
         plo = lf; phi = hf; hph = true;
       }
       if (fam & F_MOMH) {
@@ -297,9 +314,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     if (!(fam & F_OLS)) return;
     if (lpk) {  // bar m - 50 leaves the window
       const double dx = (double)llf - x0, dy = (double)lhf - y0;
-      Qx += dx; Qy += dy; Qxx += dx * dx; Qyy += dy * dy; Qxy += dx * dy; ++cQ;
+      Qx += dx; Qy += dy; Qxx += dx * dx; Qyy += dy * dy; Qxy += dx * dy;
+      if (!ALLP) ++cQ;
     }
-    if (m >= 49 && cR - cQ == 50) {  // window m-49..m, all 50 bars present (CM:129)
+    if (m >= 49 && (ALLP || cR - cQ == 50)) {  // window m-49..m, all 50 bars present (CM:129)
       const double Sx = Rx - Qx, Sy = Ry - Qy, Sxx = Rxx - Qxx, Syy = Ryy - Qyy, Sxy = Rxy - Qxy;
       const bool cx = lcx <= m - 49, cy = lcy <= m - 49;  // constant low / high
       // 50 x the population (co)variances: the factor 1/50 cancels in beta, cov^2/(vx vy)
@@ -455,10 +473,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
                   const float4& lh1, const float4& ll1) {
     // lagged bars: m0-50, m0-49 = (lh0, ll0).z .w; m0-48, m0-47 = (lh1, ll1).x .y
     if (fam & kSerH) {
-      olsbar(m0 + 0, pm & 1u, x.h.x, x.l.x, lm & 1u, lh0.z, ll0.z);
-      olsbar(m0 + 1, (pm >> 1) & 1u, x.h.y, x.l.y, (lm >> 1) & 1u, lh0.w, ll0.w);
-      olsbar(m0 + 2, (pm >> 2) & 1u, x.h.z, x.l.z, (lm >> 2) & 1u, lh1.x, ll1.x);
-      olsbar(m0 + 3, (pm >> 3) & 1u, x.h.w, x.l.w, (lm >> 3) & 1u, lh1.y, ll1.y);
+      olsbar(m0 + 0, pm & 1u, x.h.x, x.l.x, lm & 1u, lh0.z, ll0.z, full);
+      olsbar(m0 + 1, (pm >> 1) & 1u, x.h.y, x.l.y, (lm >> 1) & 1u, lh0.w, ll0.w, full);
+      olsbar(m0 + 2, (pm >> 2) & 1u, x.h.z, x.l.z, (lm >> 2) & 1u, lh1.x, ll1.x, full);
+      olsbar(m0 + 3, (pm >> 3) & 1u, x.h.w, x.l.w, (lm >> 3) & 1u, lh1.y, ll1.y, full);
     }
     if (fam & (kSerA | kSerB)) {
       // every lane has all four bars (the usual case): the presence selects fold away.
@@ -659,7 +677,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     };
     // the pair's two waves walk the same stock-days, so they take the same branch (and
     // pass the same barriers either way)
-    if (kAllpSet && __builtin_amdgcn_ballot_w64(n > 0 && n != NBAR) == 0ull) walk(std::true_type());
+    // (set H: the full-wave walk of olsbar; its own kernel, no barriers, so any wave may)
+    if ((kAllpSet || (!PAIR && SET == kSerH && MFF_SERH_FAST)) &&
+        __builtin_amdgcn_ballot_w64(n > 0 && n != NBAR) == 0ull)
+      walk(std::true_type());
     else walk(std::false_type());
   }
 
