@@ -316,23 +316,43 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
     const int n = (int)a.lvl_count[d];
     const uint64_t* K = a.lvl_key + (size_t)d * a.cap;
     const uint8_t* Wt = a.lvl_w + (size_t)d * a.cap;
-    const int step = (int)blockDim.x * UNR;
     const int steps = sl.steps;
     const bool shallow = steps <= 6;
-    // software-pipelined: the next UNR entries are loaded before this UNR's searches
+    // software-pipelined: the next UNR entries are loaded before this UNR's searches.
+    // A thread takes UNR consecutive entries (chunk c = entries [UNR c, UNR c + UNR)): the
+    // keys as four 16-B loads and the bars as one 8-B load (a wave reads 4 KB of keys
+    // contiguously) instead of UNR strided key and byte loads.  Every day's list starts
+    // 64-B aligned (pdf_levels_split: S x 240 entries per day), so the vector loads are
+    // aligned; the last partial chunk loads entry by entry.
+    static_assert(UNR == 8, "chunk loads assume 8 entries");
     uint64_t nkey[UNR];
     uint32_t nw[UNR];
-    auto fetch = [&](int i0) {
+    auto fetch = [&](int c) {
+      const int i0 = c * UNR;
+      if (i0 + UNR <= n) {
+        const uint4* kp = reinterpret_cast<const uint4*>(K + i0);
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        const int i = i0 + u * (int)blockDim.x;
-        const bool v = i < n;
-        nkey[u] = v ? K[i] : 0ull;
-        nw[u] = v ? (uint32_t)Wt[i] : 0u;
+        for (int q = 0; q < UNR / 2; ++q) {
+          const uint4 t = kp[q];
+          nkey[2 * q] = (uint64_t)t.x | ((uint64_t)t.y << 32);
+          nkey[2 * q + 1] = (uint64_t)t.z | ((uint64_t)t.w << 32);
+        }
+        const uint2 w2 = *reinterpret_cast<const uint2*>(Wt + i0);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) nw[u] = ((u < 4 ? w2.x : w2.y) >> (8 * (u & 3))) & 0xFFu;
+      } else {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const int i = i0 + u;
+          const bool v = i < n;
+          nkey[u] = v ? K[i] : 0ull;
+          nw[u] = v ? (uint32_t)Wt[i] : 0u;
+        }
       }
     };
+    const int nch = (n + UNR - 1) / UNR;
     fetch((int)threadIdx.x);
-    for (int i0 = (int)threadIdx.x; i0 < n; i0 += step) {
+    for (int c0 = (int)threadIdx.x; c0 < nch; c0 += (int)blockDim.x) {
       uint64_t key[UNR];
       uint32_t w[UNR];
       int j[UNR];  // byte offset of the probe base into L1 (shallow) or index (deep)
@@ -342,7 +362,7 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
         key[u] = nkey[u];
         w[u] = nw[u];
       }
-      fetch(i0 + step);
+      fetch(c0 + (int)blockDim.x);
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const bool bl = key[u] <= sl.L0;  // (padding entries have weight 0)
