@@ -353,15 +353,21 @@ __global__ __launch_bounds__(64) void k_stage2_ring(const double* val, const uin
 // 4.74 -> 4.27 ms at c4); a constant window still gives d = 0, sums exactly 0: std 0,
 // z NaN (C6); NaN / inf propagate to mean and std as in the two-pass form.
 constexpr int S2_U = 4;  // 4 in flight + 4 processed: <= 96 VGPRs at N = 20 (5 waves/SIMD)
+static_assert(S2_U == 4, "the chunk fast path's window offsets assume 4 days per chunk");
+#ifndef MFF_S2_CHUNK
+#define MFF_S2_CHUNK 1
+#endif
 constexpr int S2_THREADS = 256;
 
-template <int N>
-__device__ __forceinline__ void window_stats(const double (&w)[N], double& mean, double& sd) {
-  const double x0 = __builtin_isfinite(w[0]) ? w[0] : 0.0;
+// window w[B .. B + N) of an array of at least B + N registers (B a compile-time offset)
+template <int N, int B = 0, int L>
+__device__ __forceinline__ void window_stats(const double (&w)[L], double& mean, double& sd) {
+  static_assert(B + N <= L, "window past the array");
+  const double x0 = __builtin_isfinite(w[B]) ? w[B] : 0.0;
   double s1 = 0.0, s2 = 0.0;
 #pragma unroll
   for (int k = 0; k < N; ++k) {
-    const double dk = w[k] - x0;
+    const double dk = w[B + k] - x0;
     s1 += dk;
     s2 = fma(dk, dk, s2);
   }
@@ -385,9 +391,13 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
   double* ov = out_val + row * plane + s;
   uint8_t* os = out_state + row * plane + s;
 
-  double w[N];
+  // w[0 .. N): the window (oldest first); w[N .. N + S2_U): room for a chunk's days, so a
+  // chunk in which every lane has all S2_U days present takes them without shifting per
+  // day: day u enters at w[N + u], its window is w[u + 1 .. u + N], and the array shifts
+  // by S2_U once per chunk
+  double w[N + S2_U];
 #pragma unroll
-  for (int k = 0; k < N; ++k) w[k] = 0.0;
+  for (int k = 0; k < N + S2_U; ++k) w[k] = 0.0;
   uint64_t nullm = 0;  // bit k: w[k] is null
   int cnt = 0;
   // Stores are deferred by one chunk and issued together, before the next chunk's loads:
@@ -427,6 +437,49 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
       sb[u] = st[(size_t)d * S];
     }
     sp = 0u;
+    bool allp = false;
+    if constexpr (MFF_S2_CHUNK && N + S2_U <= 64) {
+     if (method != MFF_ROLL_O) {
+      bool mine = true;
+#pragma unroll
+      for (int u = 0; u < S2_U; ++u) mine = mine && sc[u] != MFF_STATE_ABSENT;
+      allp = __builtin_amdgcn_ballot_w64(!mine) == 0ull;  // wave-uniform
+     }
+    }
+    if constexpr (MFF_S2_CHUNK && N + S2_U <= 64) if (allp) {
+      // every lane has the chunk's S2_U days: they enter at w[N + u], window u is
+      // w[u + 1 .. u + N], its nulls bits u + 1 .. u + N of the extended mask
+      uint64_t nm = nullm;
+#pragma unroll
+      for (int u = 0; u < S2_U; ++u) {
+        const bool isnull = sc[u] == MFF_STATE_NULL;
+        w[N + u] = isnull ? 0.0 : xc[u];
+        nm |= (uint64_t)isnull << (N + u);
+      }
+#pragma unroll
+      for (int u = 0; u < S2_U; ++u) {
+        const int c = min(cnt + u + 1, N);
+        const uint64_t wm = (nm >> (u + 1)) & ((1ull << N) - 1ull);
+        rp[u] = 0.0;
+        if (c < N || wm != 0) {
+          sp |= (uint32_t)MFF_STATE_NULL << (8 * u);
+          continue;
+        }
+        double mean, sd;
+        if (u == 0) window_stats<N, 1>(w, mean, sd);
+        else if (u == 1) window_stats<N, 2>(w, mean, sd);
+        else if (u == 2) window_stats<N, 3>(w, mean, sd);
+        else window_stats<N, 4>(w, mean, sd);
+        const double x = xc[u];
+        rp[u] = method == MFF_ROLL_M ? mean : method == MFF_ROLL_STD ? sd : (x - mean) / sd;
+        sp |= (uint32_t)MFF_STATE_VALUE << (8 * u);
+      }
+#pragma unroll
+      for (int k = 0; k < N; ++k) w[k] = w[k + S2_U];
+      nullm = (nm >> S2_U) & ((1ull << N) - 1ull);
+      cnt = min(cnt + S2_U, N);
+      continue;
+    }
 #pragma unroll
     for (int u = 0; u < S2_U; ++u) {
       const double x = xc[u];

@@ -243,6 +243,32 @@ def test_stage2_live(dev, N, D):
     assert not bad, "\n".join(bad[:20])
 
 
+@pytest.mark.parametrize("N,D", [(1, 70), (2, 70), (3, 70), (20, 70), (20, 3), (5, 4), (7, 8), (59, 150),
+                                  (60, 150), (61, 150), (64, 150)])
+def test_stage2_chunk_fast_path(dev, N, D):
+    """k_stage2_reg's chunk fast path: where every lane of the wave has all four days of a
+    chunk (no ABSENT state), the days enter an extended register window without a shift
+    per day.  Panels without ABSENT days (NULL / NaN / inf / ties / constant column kept),
+    one stock absent over days 30..37 (the wave leaves and re-enters the fast path), and
+    N = 61, 64 (the extended window would pass 64 null-mask bits: the per-day path only)."""
+    import mff_oracle as O
+    from mff import engine
+    val, state = _random_long_panel(D, 130, 7 * N + D)
+    state[state == 0] = 2
+    if D > 40:
+        state[30:38, 9] = 0
+        val[20, 6] = 1e15
+    v = np.ascontiguousarray(val[None])
+    st = np.ascontiguousarray(state[None])
+    bad = []
+    for meth in ("m", "z", "std"):
+        rv, rs = engine.rolling(torch.from_numpy(v).to(dev), torch.from_numpy(st).to(dev), N, meth)
+        torch.cuda.synchronize()
+        ov, os_ = O.oracle_stage2(v[0], st[0], N, meth)
+        bad += compare(rv[0].cpu().numpy(), rs[0].cpu().numpy(), ov, os_, f"N{N}/D{D}/{meth}", atol=1e-9)
+    assert not bad, "\n".join(bad[:20])
+
+
 @pytest.mark.parametrize("impl,N", [("ring", 7), ("ring", 20), ("slide", 7), ("slide", 20), ("slide", 64)])
 def test_stage2_sliding_kernels_forced(dev, impl, N, monkeypatch):
     """The sliding kernels for windows the register kernel also covers (MFF_STAGE2_IMPL:
