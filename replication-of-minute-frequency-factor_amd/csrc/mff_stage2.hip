@@ -456,6 +456,24 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
         w[N + u] = isnull ? 0.0 : xc[u];
         nm |= (uint64_t)isnull << (N + u);
       }
+      // N >= S2_U: the four windows w[u + 1 .. u + N] all hold w[S2_U], so they share its
+      // shift (a member: a constant window still sums exact zeros, C6) and the sums over
+      // w[S2_U .. N]; each window adds its own 3 head / tail terms (N = 20: 81 instead of
+      // 240 flops per chunk).  Smaller N: one pass per window.
+      double cs1 = 0.0, cs2 = 0.0, dd[2 * S2_U];
+      const double cx = __builtin_isfinite(w[S2_U]) ? w[S2_U] : 0.0;
+      if constexpr (N >= S2_U) {
+#pragma unroll
+        for (int k = S2_U; k <= N; ++k) {
+          const double dk = w[k] - cx;
+          cs1 += dk;
+          cs2 = fma(dk, dk, cs2);
+        }
+#pragma unroll
+        for (int k = 1; k < S2_U; ++k) dd[k] = w[k] - cx;            // heads w[1 .. 3]
+#pragma unroll
+        for (int k = 1; k < S2_U; ++k) dd[S2_U + k] = w[N + k] - cx;  // tails w[N+1 .. N+3]
+      }
 #pragma unroll
       for (int u = 0; u < S2_U; ++u) {
         const int c = min(cnt + u + 1, N);
@@ -466,10 +484,22 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
           continue;
         }
         double mean, sd;
-        if (u == 0) window_stats<N, 1>(w, mean, sd);
-        else if (u == 1) window_stats<N, 2>(w, mean, sd);
-        else if (u == 2) window_stats<N, 3>(w, mean, sd);
-        else window_stats<N, 4>(w, mean, sd);
+        if constexpr (N >= S2_U) {
+          double s1 = cs1, s2 = cs2;
+#pragma unroll
+          for (int k = u + 1; k < S2_U; ++k) { s1 += dd[k]; s2 = fma(dd[k], dd[k], s2); }
+#pragma unroll
+          for (int k = 1; k <= u; ++k) { s1 += dd[S2_U + k]; s2 = fma(dd[S2_U + k], dd[S2_U + k], s2); }
+          constexpr double inv_n = 1.0 / (double)N;
+          const double m1 = s1 * inv_n;
+          mean = cx + m1;
+          sd = sqrt(fma(-s1, m1, s2) * inv_n);
+        } else {
+          if (u == 0) window_stats<N, 1>(w, mean, sd);
+          else if (u == 1) window_stats<N, 2>(w, mean, sd);
+          else if (u == 2) window_stats<N, 3>(w, mean, sd);
+          else window_stats<N, 4>(w, mean, sd);
+        }
         const double x = xc[u];
         rp[u] = method == MFF_ROLL_M ? mean : method == MFF_ROLL_STD ? sd : (x - mean) / sd;
         sp |= (uint32_t)MFF_STATE_VALUE << (8 * u);
