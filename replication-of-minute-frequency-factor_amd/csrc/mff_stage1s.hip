@@ -445,8 +445,12 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         if (hz) {
           const double pcz = fdivr(c - (double)czp, (double)czp, rcz);
           const double pvz = fdivr(v - (double)vzp, (double)vzp, rvz);
-          // first pair: the shifts (a wave-uniform branch, as for set A's captures)
-          if (MFF_CAPTURE_BRANCH ? __builtin_amdgcn_ballot_w64(nzc == 1) != 0ull : true) {
+          // first pair: the shifts, behind a wave-uniform branch taken only while some
+          // lane meets its second non-zero-volume row (set B bounds the wave pair: its
+          // walk 16.9 ms vs set A's 15.6 with both waves on one set; the branch instead of
+          // six selects per bar: pair 16.2 -> 15.8 ms.  Set A's capture stays select-based,
+          // MFF_CAPTURE_BRANCH: its branch form measured much slower)
+          if (__builtin_amdgcn_ballot_w64(nzc == 1) != 0ull) {
             if (nzc == 1) { x5 = pcz; y5 = pvz; x6 = c; }
           }
           const double dy = pvz - y5, e5 = pcz - x5, e6 = c - x6;
