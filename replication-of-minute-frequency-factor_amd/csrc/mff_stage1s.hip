@@ -257,14 +257,17 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   //  prv (pct_b, v_b) b = 1..n-1       E1 E2 (pct shifted by pct_1), B1 B2, EX
   // (dc = dv = 0 on row 0).  A subset that does not contain row 0 is not shifted by a
   // member, so its exact constancy (C3: Pearson NaN) comes from the change indices:
-  // kcf / kcl = first / last row whose close differs from the row before (kvf / kvl for
-  // volume), -1 when none.
+  // nchc = rows k >= 1 whose close differs from the row before, ch1c / chlc: whether row 1
+  // / the last row does (nchv, ch1v, chlv for volume): rows 1..n-1 are constant iff every
+  // change is at row 1, rows 0..n-2 iff every change is at the last row.  (Counts and
+  // lane masks: fewer VALU per bar than first / last change indices.)
   //  prvr (pct_c, pct_v) and pvr (c, pct_v) over the non-zero-volume rows after their
   //  first: shared pct_v sums Z1 Z2, shifted by the first pair (members).
   double A1 = 0, A2 = 0, B1 = 0, B2 = 0, X0 = 0, X1 = 0, X2 = 0, E1 = 0, E2 = 0, EX = 0;
   double Z1 = 0, Z2 = 0, F1 = 0, F2 = 0, FX = 0, G1 = 0, G2 = 0, GX = 0;
   double dcp = 0, dvp = 0;
-  int kr = 0, kcf = -1, kcl = -1, kvf = -1, kvl = -1;
+  int kr = 0, nchc = 0, nchv = 0;
+  bool ch1c = false, ch1v = false, chlc = false, chlv = false;
   double x5 = 0, y5 = 0, x6 = 0;
   int nzc = 0;
   // carries: previous present bar, previous present non-zero-volume bar
@@ -434,10 +437,13 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         const double ex = fdivr(c - (double)cp, (double)cp, rcp_) - x1;  // prv
         E1 += ex; E2 = fma(ex, ex, E2); EX = fma(ex, dv, EX);
         const bool chc = cf != cp, chv = vf != vp;
-        kcl = chc ? kr : kcl;
-        kcf = (chc && kcf < 0) ? kr : kcf;
-        kvl = chv ? kr : kvl;
-        kvf = (chv && kvf < 0) ? kr : kvf;
+        nchc += chc ? 1 : 0;
+        nchv += chv ? 1 : 0;
+        chlc = chc;
+        chlv = chv;
+        const bool r1 = kr == 1;
+        ch1c = r1 ? chc : ch1c;
+        ch1v = r1 ? chv : ch1v;
       }
       dcp = dc;
       dvp = dv;
@@ -803,8 +809,9 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   }
   if (fam & F_CORR) {
     const double dcl = dcp, dvl = dvp;  // the last row's shifted close / volume
-    const bool c_tail = kcl <= 1, c_head = kcf < 0 || kcf >= n - 1;  // rows 1..n-1 / 0..n-2 constant
-    const bool v_tail = kvl <= 1, v_head = kvf < 0 || kvf >= n - 1;
+    // rows 1..n-1 / 0..n-2 constant
+    const bool c_tail = nchc == (ch1c ? 1 : 0), c_head = nchc == (chlc ? 1 : 0);
+    const bool v_tail = nchv == (ch1v ? 1 : 0), v_head = nchv == (chlv ? 1 : 0);
     auto fin = [&](int f, bool cst, int np, double sx, double sy, double sxx, double syy, double sxy) {
       val(f, cst ? qnan() : pearson_raw(np, sx, sy, sxx, syy, sxy));
     };
