@@ -198,8 +198,12 @@ HL_AT = os.environ.get("MFF_HL_AT", "start")
 
 # Stream priorities of the side streams (torch / HIP: lower = higher priority; 0 is the
 # default): MFF_PDF_PRIO for the doc_pdf rank phases, MFF_HL_PRIO for the high / low kernel.
+# The high / low stream runs at high priority (-1) by default since round 3: its blocks
+# are then dispatched ahead of the doc_pdf and pair blocks, so its long walk no longer
+# ends last, and the doc_pdf sort / count fill the gaps around it (+1.8 % pass, c4,
+# profiles/r03e/ab_stream_priority.log; doc_pdf high instead: +0.1 %, both: +1.4 %).
 PDF_PRIO = int(os.environ.get("MFF_PDF_PRIO", "0"))
-HL_PRIO = int(os.environ.get("MFF_HL_PRIO", "0"))
+HL_PRIO = int(os.environ.get("MFF_HL_PRIO", "-1"))
 
 _SIDE = {}
 
