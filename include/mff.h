@@ -126,6 +126,30 @@ int mff_stage1(const float* open, const float* high, const float* low,
                void* workspace, void* stream);
 
 /*
+ * Stage 1 for the stock-days that hold polars nulls (a row that exists with a null open /
+ * high / low / close / volume).  Replaces the same `cal_*` calls (CM:12-1406) on those
+ * rows, with polars' null rules: only cal_liq_amihud_1min fills a null volume with 0
+ * (CM:743-744); first()/last() return the null (CM:799, 829), sums / moments skip it,
+ * pl.corr drops the pair (CM:841-931), pct_change forward-fills (CM:745, 861-866),
+ * top_k prefers non-null values (CM:393-471), rank() leaves a null key unranked
+ * (CM:1016) — the rules N1-N11 / C8 of oracle/mff_oracle.py.
+ * The K stock-days null_sd[K] (d*S + s, device int32) carry their own presence words
+ * null_mask uint32 [K][8] and per-field null bits null_bits uint32 [K][5][8] (field order
+ * open, high, low, close, volume; same bit layout as `valid`); the panel's `valid` mask
+ * must hold zeros for them, so the other stage-1 calls see them ABSENT.  Field values under
+ * a null bit are don't-care.
+ * phase 1: doc_pdf queries + the stock-days' price levels appended to pdf_levels (call
+ *          after mff_stage1_part 1 / 17 and before mff_pdf_sort);
+ * phase 2: every other requested row (call after the stage-1 calls that write those rows);
+ * phase 3: both (e.g. after mff_stage1 when no doc_pdf row is requested).
+ */
+int mff_stage1_nulls(const float* open, const float* high, const float* low, const float* close,
+                     const uint32_t* volume, int S, int D, const int32_t* null_sd,
+                     const uint32_t* null_mask, const uint32_t* null_bits, int K,
+                     const int32_t* factor_ids /* host */, int nf, double* val, uint8_t* state,
+                     double* pdf_query, void* pdf_levels, int phase, void* stream);
+
+/*
  * Multi-day frame semantics of the four factors whose reference windows run over('code')
  * only: liq_amihud_1min (CM:745-746 pct_change over code), corr_prvr (CM:855-867),
  * trade_bottom20retRatio (CM:1212-1216 volume.sum().over('code')) and
@@ -136,11 +160,17 @@ int mff_stage1(const float* open, const float* high, const float* low,
  * overwrites the rows of those four factors (when present in factor_ids) with the frame
  * semantics: the first bar of a day compares with the code's last close of the previous
  * day, and the 14:40+ / 14:10+ volume share uses the code's total over the whole frame.
- * open may be NULL unless a trade_bottom* row is requested.
+ * open may be NULL unless a trade_bottom* row is requested.  null_sd / null_mask / null_bits
+ * (K entries, the layout of mff_stage1_nulls; K = 0 and NULLs when the frame holds no
+ * null) give the null-holding stock-days' presence and null bits: a null volume is 0 for
+ * the Amihud sum (CM:743-744) and filtered out by volume != 0 (CM:855), a null close is
+ * forward-filled by pct_change (CM:745, 861).
  */
 int mff_stage1_frame(const float* open, const float* close, const uint32_t* volume,
-                     const uint32_t* valid, int S, int D, const int32_t* factor_ids /* host */,
-                     int nf, double* val, uint8_t* state, void* stream);
+                     const uint32_t* valid, int S, int D, const int32_t* null_sd,
+                     const uint32_t* null_mask, const uint32_t* null_bits, int K,
+                     const int32_t* factor_ids /* host */, int nf, double* val, uint8_t* state,
+                     void* stream);
 
 /*
  * doc_pdf60..95 frame-wide rank (CM:1015-1017: `.rank()` over ALL rows of the day

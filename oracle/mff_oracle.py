@@ -40,6 +40,34 @@ plus C6 below) and implemented in one helper each.
 
 C6 (stage 2, this build): a rolling window whose N values are identical has std
 exactly 0 and mean exactly the value, so ``z`` is 0/0 = NaN there.
+
+Null inputs (a row that exists with a null open / high / low / close / volume) follow
+polars' null rules, each applied where the reference expression puts it.  Only
+``cal_liq_amihud_1min`` fills a null volume with 0 (CM:743-744); everywhere else the
+null propagates or is skipped:
+
+* N1 arithmetic and comparisons with a null operand are null; ``filter(null)`` drops the
+  row, ``when(null)`` takes ``otherwise``.
+* N2 ``first()`` / ``last()`` return the row's value, null included (CM:22, 54, 799,
+  829, 946, 1015).
+* N3 ``sum`` / ``mean`` / ``std`` / ``var`` / ``skew`` / ``kurtosis`` / ``product`` skip
+  nulls (an all-null sum is 0, mean / std null).
+* N4 ``pl.corr`` drops a pair with a null side (CM:841-931).
+* N5 ``pct_change`` forward-fills nulls, then diff / shift of the filled series
+  (CM:745, 843, 861-866, 929).
+* N6 ``shift(±1)`` moves nulls with their rows (CM:899, 913).
+* N7 ``top_k`` / ``bottom_k`` prefer non-null values; the ``min`` / ``max`` / ``sum``
+  after them skip nulls (CM:393-419, 1154-1196).
+* N8 ``rank()`` keeps a null key null and ranks non-null keys among themselves
+  (CM:1016).
+* N10 ``group_by`` on a key with nulls makes one null group (CM:948, 1018).
+* N11 ``pl.len()`` counts rows, nulls included; the rolling ``var`` / ``mean`` skip
+  nulls and ``pl.cov`` drops a pair with a null side (CM:114-129).
+* C8 the doc_pdf null-rank level (N10) is cum-summed first, where ``sort()`` puts
+  nulls (C2 leaves group order to the build); if it passes the ``> p`` filter the value
+  is null (``sort()`` then ``first()``).
+None of these is pinned by a polars run (parity unpinned); each is the documented
+behaviour of the polars expression the reference uses.
 """
 from __future__ import annotations
 
@@ -197,21 +225,41 @@ def pl_corr(x: Sequence, y: Sequence) -> float:
         return float(np.sum(dx * dy) / den)
 
 
-def pl_pct_change(x: Sequence) -> List[Optional[float]]:
-    """S4: (x_i - x_{i-1}) / x_{i-1}; first element null."""
-    out: List[Optional[float]] = [None]
-    for i in range(1, len(x)):
-        out.append(_div(float(x[i]) - float(x[i - 1]), float(x[i - 1])))
+def _opt(x: Sequence, null=None) -> List[Optional[float]]:
+    """Values as Optional floats: None where ``null`` is set (a polars null) or where
+    the value already is None."""
+    if null is None:
+        return [None if v is None else float(v) for v in x]
+    return [None if (n or v is None) else float(v) for v, n in zip(x, null)]
+
+
+def pl_pct_change(x: Sequence, null=None) -> List[Optional[float]]:
+    """S4 + N5: polars ``pct_change(1)`` forward-fills nulls first, then
+    diff(1) / shift(1) of the filled series: (f_i - f_{i-1}) / f_{i-1}.  The first
+    element (and any element before the first non-null value) is null; at a null
+    position after a value the filled series repeats it, so the change is 0."""
+    vals = _opt(x, null)
+    ff: List[Optional[float]] = []
+    last = None
+    for v in vals:
+        if v is not None:
+            last = v
+        ff.append(last)
+    out: List[Optional[float]] = [None] if ff else []
+    for i in range(1, len(ff)):
+        a, b = ff[i], ff[i - 1]
+        out.append(None if a is None or b is None else _div(a - b, b))
     return out
 
 
-def pl_shift(x: Sequence, n: int) -> List[Optional[float]]:
-    """S5: shift within the group, null at the edge."""
-    L = len(x)
+def pl_shift(x: Sequence, n: int, null=None) -> List[Optional[float]]:
+    """S5: shift within the group, null at the edge; nulls move with their rows."""
+    v = _opt(x, null)
+    L = len(v)
     if n >= 0:
-        return [None] * min(n, L) + [float(v) for v in x[: max(L - n, 0)]]
+        return [None] * min(n, L) + v[: max(L - n, 0)]
     n = -n
-    return [float(v) for v in x[n:]] + [None] * min(n, L)
+    return v[n:] + [None] * min(n, L)
 
 
 def pl_sum(x) -> float:
@@ -222,9 +270,11 @@ def pl_sum(x) -> float:
 
 
 def pl_product(x) -> float:
+    """N3: product of the non-null values (empty product 1)."""
     p = 1.0
     for v in x:
-        p *= float(v)
+        if v is not None:
+            p *= float(v)
     return p
 
 
@@ -249,10 +299,17 @@ def avg_rank(values: np.ndarray) -> np.ndarray:
 # ----------------------------------------------------------------------------
 
 
-class DayFrame:
-    """One trading day, long format, rows ordered by (code, time) (C4)."""
+FIELDS = ("open", "high", "low", "close", "volume")
 
-    def __init__(self, code, date, time, open_, high, low, close, volume):
+
+class DayFrame:
+    """One trading day, long format, rows ordered by (code, time) (C4).
+
+    ``null``: optional {field: bool array} marking polars nulls (a row that exists with
+    a null value); the value arrays hold don't-care numbers there.  Missing fields (or
+    ``null=None``) have no nulls."""
+
+    def __init__(self, code, date, time, open_, high, low, close, volume, null=None):
         self.code = np.asarray(code)
         self.date = date
         self.time = np.asarray(time, dtype=np.int64)
@@ -262,6 +319,10 @@ class DayFrame:
         self.close = np.asarray(close, dtype=np.float64)
         self.volume = np.asarray(volume, dtype=np.float64)
         n = self.code.size
+        null = null or {}
+        self.null = {k: (np.asarray(null[k], dtype=bool) if k in null else np.zeros(n, dtype=bool))
+                     for k in FIELDS}
+        self.has_null = any(bool(a.any()) for a in self.null.values())
         if n:
             cut = np.flatnonzero(self.code[1:] != self.code[:-1]) + 1
             starts = np.concatenate([[0], cut])
@@ -272,6 +333,21 @@ class DayFrame:
 
     def g(self, name, s, e):
         return getattr(self, name)[s:e]
+
+    def nul(self, name, s, e):
+        """Null mask of column ``name`` on rows s..e (N1)."""
+        return self.null[name][s:e]
+
+    def ok(self, s, e, *names):
+        """Rows s..e where every listed column is non-null."""
+        m = np.ones(e - s, dtype=bool)
+        for k in names:
+            m &= ~self.null[k][s:e]
+        return m
+
+    def col(self, name, s, e):
+        """Column ``name`` on rows s..e as Optional floats (None = null)."""
+        return _opt(getattr(self, name)[s:e], self.null[name][s:e])
 
 
 def minute_to_time(m: np.ndarray) -> np.ndarray:
@@ -296,7 +372,10 @@ def _seg_pair(df: DayFrame, times) -> Dict:
             continue
         idx = np.flatnonzero(sel)
         idx = idx[np.argsort(t[idx], kind="stable")]
-        out[code] = _div(df.close[s + idx[-1]], df.open[s + idx[0]])
+        # N2: last() / first() take the row's value, null included; N1: x / null = null
+        cl = None if df.null["close"][s + idx[-1]] else df.close[s + idx[-1]]
+        op = None if df.null["open"][s + idx[0]] else df.open[s + idx[0]]
+        out[code] = _div(cl, op)
     return out
 
 
@@ -326,9 +405,13 @@ def cal_mmt_paratio(df):  # CM:42-60
             idx = np.flatnonzero(sess == k)
             if idx.size == 0:
                 continue
-            # close.last() / open.first() - 1 in frame order (CM:54)
-            mmts.append(_div(df.close[s + idx[-1]], df.open[s + idx[0]]) - 1.0)
-        out[code] = mmts[-1] - mmts[0]  # mmt.last() - mmt.first() (CM:57)
+            # close.last() / open.first() - 1 in frame order (CM:54); null propagates (N1, N2)
+            cl = None if df.null["close"][s + idx[-1]] else df.close[s + idx[-1]]
+            op = None if df.null["open"][s + idx[0]] else df.open[s + idx[0]]
+            q = _div(cl, op)
+            mmts.append(None if q is None else q - 1.0)
+        # mmt.last() - mmt.first() (CM:57)
+        out[code] = None if mmts[-1] is None or mmts[0] is None else mmts[-1] - mmts[0]
     return out
 
 
@@ -345,33 +428,71 @@ def _minute_in_trade(time: np.ndarray) -> np.ndarray:
 
 def _ols_windows(df: DayFrame, s: int, e: int):
     """rolling(index_column='minute_in_trade', period='50i', group_by=[code, date])
-    (CM:114-118) then filter(n >= 50) (CM:129).  S12: window (t-50, t]."""
+    (CM:114-118) then filter(n >= 50) (CM:129).  S12: window (t-50, t].  The five OLS
+    functions share one computation per (frame, group)."""
+    cache = df.__dict__.setdefault("_ols_cache", {})
+    if (s, e) not in cache:
+        cache[(s, e)] = _ols_windows_calc(df, s, e)
+    return cache[(s, e)]
+
+
+def _ols_windows_calc(df: DayFrame, s: int, e: int):
     mins = _minute_in_trade(df.time[s:e])
     x = df.low[s:e]
     y = df.high[s:e]
+    xok = ~df.null["low"][s:e]
+    yok = ~df.null["high"][s:e]
     wins = []
     for i in range(mins.size):
         t = mins[i]
         lo = np.searchsorted(mins, t - 50, side="right")
         hi = i + 1
-        n = hi - lo
+        n = hi - lo  # pl.len(): rows, nulls included (N11)
         if n < 50:
             continue
-        wx, wy = x[lo:hi], y[lo:hi]
-        cx, cy = _constant(wx), _constant(wy)
-        mx, my = _mean_exact(wx), _mean_exact(wy)
         with np.errstate(all="ignore"):
-            var_x = 0.0 if cx else float(np.mean((wx - mx) ** 2))  # ddof=0 (CM:120)
-            var_y = 0.0 if cy else float(np.mean((wy - my) ** 2))  # ddof=0 (CM:121)
-            cov = 0.0 if (cx or cy) else float(np.mean((wx - mx) * (wy - my)))  # CM:119
+            if xok[lo:hi].all() and yok[lo:hi].all():
+                wx, wy = x[lo:hi], y[lo:hi]
+                cx, cy = _constant(wx), _constant(wy)
+                mx, my = _mean_exact(wx), _mean_exact(wy)
+                var_x = 0.0 if cx else float(np.mean((wx - mx) ** 2))  # ddof=0 (CM:120)
+                var_y = 0.0 if cy else float(np.mean((wy - my) ** 2))  # ddof=0 (CM:121)
+                cov = 0.0 if (cx or cy) else float(np.mean((wx - mx) * (wy - my)))  # CM:119
+                wins.append((cov, var_x, var_y, mx, my))
+                continue
+            # N11: var / mean skip nulls, cov drops a pair with a null side; an empty set
+            # is null
+            wx, wy = x[lo:hi][xok[lo:hi]], y[lo:hi][yok[lo:hi]]
+            pr = xok[lo:hi] & yok[lo:hi]
+            px, py = x[lo:hi][pr], y[lo:hi][pr]
+            mx = _mean_exact(wx) if wx.size else None
+            my = _mean_exact(wy) if wy.size else None
+            # ddof=0 (CM:119-121); C3: exactly 0 for identical values
+            var_x = None if not wx.size else 0.0 if _constant(wx) else float(np.mean((wx - mx) ** 2))
+            var_y = None if not wy.size else 0.0 if _constant(wy) else float(np.mean((wy - my) ** 2))
+            if not px.size:
+                cov = None
+            elif _constant(px) or _constant(py):
+                cov = 0.0
+            else:
+                cov = float(np.mean((px - _mean_exact(px)) * (py - _mean_exact(py))))
         wins.append((cov, var_x, var_y, mx, my))
     return wins
 
 
+def _ne0(x) -> Optional[bool]:
+    """polars ``x != 0`` with null propagation (N1)."""
+    return None if x is None else tot_ne(x, 0.0)
+
+
+def _mul(a, b):
+    return None if a is None or b is None else a * b
+
+
 def _beta(w):
     cov, vx, vy, mx, my = w
-    # CM:131-134
-    return _div(cov, vx) if vx != 0 else _div(my, mx)
+    # CM:131-134: when(var_x != 0) -- a null condition takes otherwise (N1)
+    return _div(cov, vx) if _ne0(vx) is True else _div(my, mx)
 
 
 def _pow(a, p):
@@ -389,18 +510,19 @@ def cal_mmt_ols_qrs(df):  # CM:93-173
         for w in wins:
             cov, vx, vy, mx, my = w
             betas.append(_beta(w))
-            # CM:135-140: cov**0.5 / (var_x * var_y), null when the product is 0
-            qs.append(_div(_pow(cov, 0.5), vx * vy) if vy * vx != 0 else None)
-        b = np.array(betas)
-        beta_mean = pl_mean(b)
-        beta_std = pl_std(b)
-        beta_last = betas[-1]
+            # CM:135-140: cov**0.5 / (var_x * var_y), null when the product is 0 or null
+            qs.append(_div(None if cov is None else _pow(cov, 0.5), vx * vy)
+                      if _ne0(_mul(vy, vx)) is True else None)
+        beta_mean = pl_mean(betas)  # N3: nulls skipped
+        beta_std = pl_std(betas)
+        beta_last = betas[-1]  # N2: the last window's beta, null included
         csm = pl_mean(qs)
         cond_a = tot_ne(beta_std, 0.0)
         cond_b = csm is not None
-        # CM:159-171: when(...).then(csm * (last - mean) / std).otherwise(0)
+        # CM:159-171: when(...).then(csm * (last - mean) / std).otherwise(0); a null
+        # condition takes otherwise (N1), a null operand nulls the then-branch
         if cond_a is True and cond_b:
-            out[code] = _div(csm * (beta_last - beta_mean), beta_std)
+            out[code] = None if beta_last is None else _div(csm * (beta_last - beta_mean), beta_std)
         else:
             out[code] = 0.0
     return out
@@ -414,7 +536,7 @@ def _ols_mean_of(df, fn):
             continue
         vals = []
         for cov, vx, vy, mx, my in wins:
-            vals.append(fn(cov, vx, vy) if vx * vy != 0 else None)
+            vals.append(fn(cov, vx, vy) if _ne0(_mul(vx, vy)) is True and cov is not None else None)
         m = pl_mean(vals)
         out[code] = 0.0 if m is None else m  # fill_null(0)
     return out
@@ -433,7 +555,7 @@ def cal_mmt_ols_beta_mean(df):  # CM:274-324
     for code, s, e in df.groups:
         wins = _ols_windows(df, s, e)
         if wins:
-            out[code] = pl_mean(np.array([_beta(w) for w in wins]))
+            out[code] = pl_mean([_beta(w) for w in wins])
     return out
 
 
@@ -443,11 +565,11 @@ def cal_mmt_ols_beta_zscore_last(df):  # CM:327-376
         wins = _ols_windows(df, s, e)
         if not wins:
             continue
-        b = np.array([_beta(w) for w in wins])
+        b = [_beta(w) for w in wins]
         sd = pl_std(b)
         mean = pl_mean(b)
         if tot_gt(sd, 0.0) is True:  # when(std > 0), null -> otherwise (CM:369-373)
-            out[code] = _div(b[-1] - mean, sd)
+            out[code] = None if b[-1] is None else _div(b[-1] - mean, sd)
         else:
             out[code] = mean
     return out
@@ -462,13 +584,20 @@ def _vol_rank_ret(df, k, top):
     out = {}
     for code, s, e in df.groups:
         v = df.volume[s:e]
-        sv = np.sort(v)
+        vok = ~df.null["volume"][s:e]
+        # N7: top_k / bottom_k prefer non-null values; min / max skip the nulls, so the
+        # threshold comes from the non-null volumes -- null when there are none, and then
+        # every row's predicate is null and the filter leaves the code no row (absent)
+        sv = np.sort(v[vok])
+        if sv.size == 0:
+            continue
         if top:  # volume >= volume.top_k(k).min()  (CM:391-396)
-            theta = sv[-k] if v.size >= k else sv[0]
-            sel = v >= theta
+            theta = sv[-k] if sv.size >= k else sv[0]
+            sel = vok & (v >= theta)  # a null volume compares null: filtered out (N1)
         else:  # volume <= volume.bottom_k(k).max()  (CM:417-422)
-            theta = sv[k - 1] if v.size >= k else sv[-1]
-            sel = v <= theta
+            theta = sv[k - 1] if sv.size >= k else sv[-1]
+            sel = vok & (v <= theta)
+        sel &= df.ok(s, e, "close", "open")  # a null ret is skipped by product() (N3)
         ret = [_div(c, o) for c, o in zip(df.close[s:e][sel], df.open[s:e][sel])]
         out[code] = pl_product(ret) - 1.0  # ret.product() - 1
     return out
@@ -496,8 +625,11 @@ def cal_mmt_bottom20VolumeRet(df):  # CM:457-480 — bottom_k(50) [sic, CM:471]
 
 
 def _returns(df, s, e):
+    """close / open - 1 of the rows where it is non-null (N1); every consumer (std, skew,
+    kurtosis, the up / down filters) skips nulls (N3)."""
+    ok = df.ok(s, e, "close", "open")
     with np.errstate(all="ignore"):
-        return df.close[s:e] / df.open[s:e] - 1.0  # close / open - 1
+        return df.close[s:e][ok] / df.open[s:e][ok] - 1.0
 
 
 def _per_group(df, fn):
@@ -505,13 +637,14 @@ def _per_group(df, fn):
 
 
 def cal_vol_volume1min(df):  # CM:485-496
-    return _per_group(df, lambda s, e: pl_std(df.volume[s:e]))
+    return _per_group(df, lambda s, e: pl_std(df.volume[s:e][df.ok(s, e, "volume")]))
 
 
 def cal_vol_range1min(df):  # CM:499-515
     def f(s, e):
+        ok = df.ok(s, e, "high", "low")
         with np.errstate(all="ignore"):
-            return pl_std(df.high[s:e] / df.low[s:e])
+            return pl_std(df.high[s:e][ok] / df.low[s:e][ok])
     return _per_group(df, f)
 
 
@@ -570,9 +703,11 @@ def cal_shape_skratio(df):  # CM:673-687 (output columns ordered date, code)
 
 
 def _vshare(df, s, e):
-    v = df.volume[s:e]
+    """volume / volume.sum() on the non-null volumes (a null share is skipped by skew /
+    kurtosis, N3; the sum skips nulls)."""
+    v = df.volume[s:e][df.ok(s, e, "volume")]
     with np.errstate(all="ignore"):
-        return v / np.sum(v)  # volume / volume.sum()
+        return v / np.sum(v)
 
 
 def cal_shape_skewVol(df):  # CM:690-700
@@ -597,9 +732,10 @@ def cal_shape_skratioVol(df):  # CM:716-729
 
 def cal_liq_amihud_1min(df):  # CM:734-761
     def f(s, e):
-        pc = pl_pct_change(df.close[s:e])  # pct_change().over('code')
+        pc = pl_pct_change(df.close[s:e], df.nul("close", s, e))  # pct_change().over('code')
+        vol = np.where(df.nul("volume", s, e), 0.0, df.volume[s:e])  # volume.fill_null(0)
         tot = []
-        for p, v in zip(pc, df.volume[s:e]):
+        for p, v in zip(pc, vol):
             pa = 0.0 if p is None else abs(p)  # .abs().fill_null(0)
             tot.append(_div(pa, v) if v > 0 else 0.0)
         return pl_sum(tot)
@@ -610,8 +746,8 @@ def _filtered_sum(df, pred):
     out = {}
     for code, s, e in df.groups:
         sel = pred(df.time[s:e])
-        if sel.any():
-            out[code] = pl_sum(df.volume[s:e][sel])
+        if sel.any():  # the row exists, whatever its volume
+            out[code] = pl_sum(df.volume[s:e][sel & df.ok(s, e, "volume")])
     return out
 
 
@@ -623,19 +759,26 @@ def cal_liq_closevol(df):  # CM:778-789
     return _filtered_sum(df, lambda t: t >= 145700000)
 
 
+def _first_volume(df, s):
+    """volume.first(): the first row's volume, null included (N2)."""
+    return None if df.null["volume"][s] else float(df.volume[s])
+
+
 def cal_liq_firstCallR(df):  # CM:792-802
-    return _per_group(df, lambda s, e: _div(df.volume[s], pl_sum(df.volume[s:e])))
+    return _per_group(df, lambda s, e: _div(_first_volume(df, s),
+                                            pl_sum(df.volume[s:e][df.ok(s, e, "volume")])))
 
 
 def cal_liq_lastCallR(df):  # CM:805-820
     def f(s, e):
+        ok = df.ok(s, e, "volume")
         v = df.volume[s:e]
-        return _div(pl_sum(v[df.time[s:e] >= 145700000]), pl_sum(v))
+        return _div(pl_sum(v[(df.time[s:e] >= 145700000) & ok]), pl_sum(v[ok]))
     return _per_group(df, f)
 
 
 def cal_liq_openvol(df):  # CM:823-831
-    return _per_group(df, lambda s, e: float(df.volume[s]))
+    return _per_group(df, lambda s, e: _first_volume(df, s))
 
 
 # ----------------------------------------------------------------------------
@@ -644,16 +787,18 @@ def cal_liq_openvol(df):  # CM:823-831
 
 
 def cal_corr_prv(df):  # CM:836-847
-    return _per_group(df, lambda s, e: pl_corr(pl_pct_change(df.close[s:e]),
-                                               list(df.volume[s:e])))
+    return _per_group(df, lambda s, e: pl_corr(pl_pct_change(df.close[s:e], df.nul("close", s, e)),
+                                               df.col("volume", s, e)))
 
 
 def _nonzero_groups(df):
-    """filter(volume != 0) then re-group (CM:855-857, CM:924-926)."""
+    """filter(volume != 0) then re-group (CM:855-857, CM:924-926): a null volume
+    compares null and is filtered out too (N1).  Yields (code, close as Optional
+    floats, volume)."""
     for code, s, e in df.groups:
-        sel = df.volume[s:e] != 0
+        sel = (df.volume[s:e] != 0) & df.ok(s, e, "volume")
         if sel.any():
-            yield code, df.close[s:e][sel], df.volume[s:e][sel]
+            yield code, _opt(df.close[s:e][sel], df.nul("close", s, e)[sel]), df.volume[s:e][sel]
 
 
 def cal_corr_prvr(df):  # CM:850-874
@@ -662,21 +807,21 @@ def cal_corr_prvr(df):  # CM:850-874
 
 
 def cal_corr_pv(df):  # CM:877-888
-    return _per_group(df, lambda s, e: pl_corr(list(df.close[s:e]), list(df.volume[s:e])))
+    return _per_group(df, lambda s, e: pl_corr(df.col("close", s, e), df.col("volume", s, e)))
 
 
 def cal_corr_pvd(df):  # CM:891-902
-    return _per_group(df, lambda s, e: pl_corr(list(df.close[s:e]),
-                                               pl_shift(df.volume[s:e], 1)))
+    return _per_group(df, lambda s, e: pl_corr(df.col("close", s, e),
+                                               pl_shift(df.volume[s:e], 1, df.nul("volume", s, e))))
 
 
 def cal_corr_pvl(df):  # CM:905-916
-    return _per_group(df, lambda s, e: pl_corr(list(df.close[s:e]),
-                                               pl_shift(df.volume[s:e], -1)))
+    return _per_group(df, lambda s, e: pl_corr(df.col("close", s, e),
+                                               pl_shift(df.volume[s:e], -1, df.nul("volume", s, e))))
 
 
 def cal_corr_pvr(df):  # CM:919-932
-    return {code: pl_corr(list(c), pl_pct_change(v)) for code, c, v in _nonzero_groups(df)}
+    return {code: pl_corr(c, pl_pct_change(v)) for code, c, v in _nonzero_groups(df)}
 
 
 # ----------------------------------------------------------------------------
@@ -693,14 +838,19 @@ def _doc_levels(df, s, e):
     moments below are NaN rather than a function of float summation order."""
     v = df.volume[s:e]
     c = df.close[s:e]
+    vok = df.ok(s, e, "volume")
     with np.errstate(all="ignore"):
-        vd = v / np.sum(v)
+        vd = v / np.sum(v[vok])
         key = c[-1] / c
-    levels: Dict[float, float] = {}
-    vol: Dict[float, float] = {}
-    for k, x, vv in zip(key.tolist(), vd.tolist(), v.tolist()):
-        levels[k] = levels.get(k, 0.0) + x
-        vol[k] = vol.get(k, 0.0) + vv
+    # N10: a null key (null close, or every row when close.last() is null, N2) is one
+    # more group; N3: volume_d.sum() skips null shares (a group of nulls sums to 0)
+    knull = df.nul("close", s, e) | bool(df.null["close"][e - 1])
+    levels: Dict[Optional[float], float] = {}
+    vol: Dict[Optional[float], float] = {}
+    for k, x, vv, ok, kn in zip(key.tolist(), vd.tolist(), v.tolist(), vok.tolist(), knull.tolist()):
+        k = None if kn else k
+        levels[k] = levels.get(k, 0.0) + (x if ok else 0.0)
+        vol[k] = vol.get(k, 0.0) + (vv if ok else 0.0)
     shares = np.array(list(levels.values()))
     V = np.array(list(vol.values()))
     if shares.size >= 2 and np.all(V == V[0]) and np.all(np.isfinite(shares)):
@@ -728,24 +878,38 @@ def _doc_pdf(df, p):
         return out
     with np.errstate(all="ignore"):
         last_close = np.empty_like(df.close)
+        knull = df.null["close"].copy()
         for code, s, e in df.groups:
             last_close[s:e] = df.close[e - 1]
+            if df.null["close"][e - 1]:  # close.last() is null: every key of the code (N2)
+                knull[s:e] = True
         key = last_close / df.close
-    rank = avg_rank(key)
+    # N8: rank() leaves a null key null and ranks the non-null keys among themselves
+    rank = np.full(key.size, np.nan)
+    rank[~knull] = avg_rank(key[~knull])
     for code, s, e in df.groups:
         v = df.volume[s:e]
+        vok = df.ok(s, e, "volume")
         with np.errstate(all="ignore"):
-            vd = v / np.sum(v)
-        levels: Dict[float, float] = {}
-        for rk, x in zip(rank[s:e].tolist(), vd.tolist()):
-            levels[rk] = levels.get(rk, 0.0) + x
+            vd = v / np.sum(v[vok])
+        levels: Dict[Optional[float], float] = {}
+        for rk, x, ok, kn in zip(rank[s:e].tolist(), vd.tolist(), vok.tolist(), knull[s:e].tolist()):
+            rk = None if kn else rk
+            levels[rk] = levels.get(rk, 0.0) + (x if ok else 0.0)  # N3, N10
         cum = 0.0
-        best = None
-        for rk in sorted(levels):  # C2
+        passing = []
+        # C2: cum-sum in ascending rank order; the null-rank level (N10) first, where
+        # sort() puts nulls (C8)
+        for rk in sorted(levels, key=lambda r: (r is not None, r if r is not None else 0.0)):
             cum = cum + levels[rk]
             if tot_gt(cum, p) is True:  # cum_sum() > p, S11
-                best = rk if best is None else min(best, rk)
-        out[code] = best  # .filter(...).sort().first(): null if none passes
+                passing.append(rk)
+        # .filter(...).sort().first(): null if none passes, or if the null rank passes
+        # (sort() puts nulls first)
+        if not passing or any(r is None for r in passing):
+            out[code] = None
+        else:
+            out[code] = min(passing)
     return out
 
 
@@ -771,7 +935,8 @@ def cal_doc_pdf95(df):  # CM:1114-1138
 
 def _doc_vol_topk(df, k):
     def f(s, e):
-        v = df.volume[s:e]
+        # N7: top_k prefers the non-null shares; the sum skips the nulls (0 if all null)
+        v = df.volume[s:e][df.ok(s, e, "volume")]
         with np.errstate(all="ignore"):
             vd = v / np.sum(v)
         # top_k(k) (S7, NaN is largest under total order) then sum
@@ -805,14 +970,17 @@ def _tail_ret_ratio(df, t0, plus_one):
         sel = df.time[s:e] >= t0
         if not sel.any():
             continue
+        vok = df.ok(s, e, "volume")[sel]
+        rok = df.ok(s, e, "close", "open")[sel]
         v = df.volume[s:e][sel]
         with np.errstate(all="ignore"):
             ret = df.close[s:e][sel] / df.open[s:e][sel] - 1.0
-        sv = pl_sum(v)  # volume.sum().over('code') on the filtered frame
+        sv = pl_sum(v[vok])  # volume.sum().over('code') on the filtered frame (N3)
         den = sv + 1.0 if plus_one else (1.0 if sv == 0 else sv)
         with np.errstate(all="ignore"):
             vd = v / den
-            out[code] = pl_sum(vd * ret)
+            both = vok & rok  # volume_d * ret is null unless both are non-null (N1)
+            out[code] = pl_sum(vd[both] * ret[both])
     return out
 
 
@@ -826,7 +994,7 @@ def cal_trade_bottom50retRatio(df):  # CM:1227-1248
 
 def _window_share(df, pred):
     def f(s, e):
-        v = df.volume[s:e]
+        v = np.where(df.nul("volume", s, e), 0.0, df.volume[s:e])  # both sums skip nulls (N3)
         part = pl_sum(np.where(pred(df.time[s:e]), v, 0.0))
         tot = pl_sum(v)
         return _div(part, tot) if tot > 0 else 0.125
@@ -847,17 +1015,21 @@ def _head_ret_ratio(df, t1, mode):
         sel = df.time[s:e] <= t1
         if not sel.any():
             continue
+        vok = df.ok(s, e, "volume")[sel]
+        rok = df.ok(s, e, "close", "open")[sel]
         v = df.volume[s:e][sel]
         with np.errstate(all="ignore"):
-            vd = v / np.sum(v)  # volume / volume.sum().over(code, date)
+            vd = v / np.sum(v[vok])  # volume / volume.sum().over(code, date), sum skips nulls
             pc = df.close[s:e][sel] / df.open[s:e][sel] - 1.0
             if mode == "all":
-                num = pc
-            elif mode == "neg":
-                num = np.where(pc < 0, np.abs(pc), 0.0)
+                num, nok = pc, rok
+            elif mode == "neg":  # when(pct < 0): a null pct takes otherwise(0) (N1)
+                num, nok = np.where(rok & (pc < 0), np.abs(pc), 0.0), np.ones_like(rok)
             else:
-                num = np.where(pc > 0, np.abs(pc), 0.0)
-            out[code] = pl_mean(num / vd)
+                num, nok = np.where(rok & (pc > 0), np.abs(pc), 0.0), np.ones_like(rok)
+            q = num / vd
+            # mean() over the non-null quotients (N3): null where either side is null
+            out[code] = pl_mean(q[nok & vok])
     return out
 
 
@@ -923,7 +1095,17 @@ def day_frame_from_panel(panel, d: int) -> DayFrame:
     codes = np.asarray(panel["codes"])[s_idx]
     f = lambda k: panel[k][d][s_idx, m_idx].astype(np.float64)
     return DayFrame(codes, d, minute_to_time(m_idx), f("open"), f("high"), f("low"),
-                    f("close"), f("volume"))
+                    f("close"), f("volume"), null=panel_nulls(panel, d, s_idx, m_idx))
+
+
+def panel_nulls(panel, d, s_idx, m_idx):
+    """{field: bool} null masks of the rows (s_idx, m_idx) of day d: panel["null"] is an
+    optional uint8 [D][S][240] whose bit i marks FIELDS[i] null on a present bar."""
+    nb = panel.get("null")
+    if nb is None:
+        return None
+    bits = nb[d][s_idx, m_idx]
+    return {k: (bits >> i) & 1 == 1 for i, k in enumerate(FIELDS)}
 
 
 def oracle_stage1(panel, names: Sequence[str] = None):
@@ -962,7 +1144,9 @@ def oracle_frame_doc_pdf(panel):
     parts = [day_frame_from_panel(panel, d) for d in range(D)]
     lab = np.concatenate([np.char.add(np.asarray(p.code, dtype=str), f"|{d}") for d, p in enumerate(parts)])
     cat = lambda k: np.concatenate([getattr(p, k) for p in parts])
-    frame = DayFrame(lab, None, cat("time"), cat("open"), cat("high"), cat("low"), cat("close"), cat("volume"))
+    null = {k: np.concatenate([p.null[k] for p in parts]) for k in FIELDS}
+    frame = DayFrame(lab, None, cat("time"), cat("open"), cat("high"), cat("low"), cat("close"), cat("volume"),
+                     null=null)
     code_index = {c: i for i, c in enumerate(panel["codes"])}
     out = {}
     for name, p in zip(FRAME_RANK_NAMES, (0.6, 0.7, 0.8, 0.9, 0.95)):
@@ -1000,15 +1184,20 @@ def oracle_frame_xday(panel):
             continue
         g = lambda k: panel[k][dd, s, mm].astype(np.float64)
         o, c, v = g("open"), g("close"), g("volume")
-        # liq_amihud_1min: pct_change().over('code').abs().fill_null(0); v > 0 ? pct / v : 0
-        pc = pl_pct_change(c)
-        am = [(_div(0.0 if p is None else abs(p), vv) if vv > 0 else 0.0) for p, vv in zip(pc, v)]
+        nb = panel.get("null")
+        nbits = nb[dd, s, mm] if nb is not None else np.zeros(dd.size, np.uint8)
+        nO, nC, nV = (nbits & 1) != 0, (nbits & 8) != 0, (nbits & 16) != 0
+        # liq_amihud_1min: volume.fill_null(0); pct_change().over('code') (N5: nulls
+        # forward-filled) .abs().fill_null(0); v > 0 ? pct / v : 0
+        pc = pl_pct_change(c, nC)
+        v0 = np.where(nV, 0.0, v)
+        am = [(_div(0.0 if p is None else abs(p), vv) if vv > 0 else 0.0) for p, vv in zip(pc, v0)]
         for d in np.unique(dd):
             put("liq_amihud_1min", d, s, pl_sum([a for a, e in zip(am, dd) if e == d]))
-        # corr_prvr: filter(volume != 0), pct_change of close and volume over('code'),
-        # then pl.corr per (code, date)
-        nz = v != 0
-        cc, vc = pl_pct_change(c[nz]), pl_pct_change(v[nz])
+        # corr_prvr: filter(volume != 0) (a null volume is filtered out, N1), pct_change of
+        # close and volume over('code'), then pl.corr per (code, date)
+        nz = (v != 0) & ~nV
+        cc, vc = pl_pct_change(c[nz], nC[nz]), pl_pct_change(v[nz])
         dz = dd[nz]
         for d in np.unique(dz):
             sel = [i for i in range(dz.size) if dz[i] == d]
@@ -1018,13 +1207,14 @@ def oracle_frame_xday(panel):
             t = mm >= m0
             if not t.any():
                 continue
-            tot = pl_sum(v[t])
+            tot = pl_sum(v[t & ~nV])
             den = tot + 1.0 if plus_one else (1.0 if tot == 0 else tot)
             with np.errstate(all="ignore"):
                 ret = c[t] / o[t] - 1.0
                 vd = v[t] / den
+            both = ~(nV | nC | nO)[t]
             for d in np.unique(dd[t]):
-                k = dd[t] == d
+                k = (dd[t] == d) & both
                 put(name, d, s, pl_sum(vd[k] * ret[k]))
     return out
 

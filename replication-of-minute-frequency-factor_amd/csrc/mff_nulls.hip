@@ -1,0 +1,872 @@
+// mff_nulls.hip — stage 1 for the stock-days that hold polars nulls.
+//
+// A day file row may exist with a null open / high / low / close / volume.  That is not a
+// missing bar: the reference's expressions decide what a null does (SURVEY §8(c) S1-S13
+// plus the null rules N1-N11 / C8 of oracle/mff_oracle.py), and only cal_liq_amihud_1min
+// fills a null volume with 0 (CM:743-744):
+//   N1 x op null = null, a null comparison drops the row (filter) or takes otherwise (when)
+//   N2 first() / last() return the row's value, null included (CM:22, 54, 799, 829, 946)
+//   N3 sum / mean / std / skew / kurtosis / product skip nulls (all-null sum 0, mean null)
+//   N4 pl.corr drops a pair with a null side                        (CM:841-931)
+//   N5 pct_change forward-fills, then diff / shift                  (CM:745, 843, 861-866, 929)
+//   N6 shift moves a null with its row                              (CM:899, 913)
+//   N7 top_k / bottom_k prefer non-null values                      (CM:393-471, 1154-1196)
+//   N8 rank() keeps a null key null                                 (CM:1016)
+//   N10 group_by makes one null-key group; C8 it is cum-summed first (CM:948, 1018-1026)
+//   N11 pl.len() counts rows, the rolling var / mean / cov skip nulls (CM:114-129)
+// The ingest (mff/ingest.py) lists those stock-days with their real presence mask and
+// per-field null bits and clears them from the panel's mask, so the fast kernels see
+// them ABSENT (no outputs, no doc_pdf levels); this kernel then computes every requested
+// factor of the listed stock-days.  Null rows are rare (vendor gaps), so the layout is
+// the plain one of the exact kernel (mff_stage1.hip): one wavefront per stock-day, lane l
+// = bars 4l..4l+3, direct stores.
+//
+// phase 1: the doc_pdf queries, the stock-day's levels appended to the day's flat list
+//          (non-null keys only, N8) and the NULL placeholders of the doc_pdf rows — after
+//          the sorted-group kernel (which zeroes the list counts), before mff_pdf_sort;
+// phase 2: every other requested row — after the kernels that write the same rows
+//          (they store ABSENT for the listed stock-days);
+// phase 3: both.
+#include <string.h>
+
+#include "../../include/mff.h"
+#include "mff_internal.h"
+#include "mff_w64.h"
+#include "mff_wave.h"
+
+namespace mff {
+namespace nul {
+
+constexpr int WPB = 4;  // waves per block
+
+struct Args {
+  const float* fld[5];      // open, high, low, close (fp32), volume (u32) planes [D][S][240]
+  const int32_t* sd_list;   // [K] stock-day indices d*S + s
+  const uint32_t* nmask;    // [K][8] presence words (the panel's own mask is cleared there)
+  const uint32_t* nbits;    // [K][5][8] null bits per field (open, high, low, close, volume)
+  int K;
+  double* val;
+  uint8_t* state;
+  double* pdfq;             // [5][D][S]
+  uint32_t* lvl_count;      // doc_pdf level side channel (mff_pdf_levels_bytes)
+  uint64_t* lvl_key;
+  uint8_t* lvl_w;
+  int S, D;
+  uint32_t fam;
+  int8_t row[NF];
+};
+
+struct Out {
+  double* val;
+  uint8_t* state;
+  const int8_t* row;
+  size_t sd, plane;
+  __device__ __forceinline__ void put(int f, double v, uint8_t st) const {
+    const int r = row[f];
+    if (r >= 0 && lane_id() == 0) {
+      val[(size_t)r * plane + sd] = v;
+      state[(size_t)r * plane + sd] = st;
+    }
+  }
+  __device__ __forceinline__ void val1(int f, double v) const { put(f, v, MFF_STATE_VALUE); }
+  __device__ __forceinline__ void null(int f) const { put(f, 0.0, MFF_STATE_NULL); }
+};
+
+__device__ __forceinline__ Bits bits_of(const uint32_t* w) {
+  const int lane = lane_id();
+  const uint32_t mw = lane < 60 ? w[lane >> 3] : 0u;
+  const uint32_t b = (mw >> ((lane & 7) * 4)) & 0xFu;
+  bool f[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) f[k] = (b >> k) & 1u;
+  return ballot4(f);
+}
+
+// the previous present row's value and flag of x (the row order of a day frame, C4)
+template <typename T>
+__device__ __forceinline__ void prev_row(const T (&x)[4], const bool (&xf)[4], const bool (&p)[4], T (&xp)[4],
+                                         bool (&xfp)[4], bool (&has)[4]) {
+  uint32_t fw[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) fw[k] = xf[k] ? 1u : 0u;
+  uint32_t fwp[4];
+  prev_valid(x, p, xp, has);
+  prev_valid(fw, p, fwp, has);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) xfp[k] = has[k] && fwp[k] != 0u;
+}
+
+// pct_change over the rows flagged `rows` of a series x with nulls (N5): the series is
+// forward-filled over those rows, then (f - f_prev) / f_prev, f_prev = the previous
+// row's filled value; ok[k] = the change is non-null
+__device__ __forceinline__ void pct_ffill(const float (&x)[4], const bool (&xok)[4], const bool (&rows)[4],
+                                          double (&pc)[4], bool (&ok)[4]) {
+  bool fl[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) fl[k] = rows[k] && xok[k];
+  float xv[4];
+  bool hv[4];
+  prev_valid(x, fl, xv, hv);  // the latest non-null value strictly before, over the rows
+  double f[4];
+  bool hf[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[k] = fl[k] ? (double)x[k] : (double)xv[k];
+    hf[k] = fl[k] || hv[k];
+  }
+  double fp[4];
+  bool hfp[4], hrow[4];
+  prev_row(f, hf, rows, fp, hfp, hrow);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    ok[k] = rows[k] && hf[k] && hfp[k];
+    pc[k] = ok[k] ? (f[k] - fp[k]) / fp[k] : 0.0;
+  }
+}
+
+struct Win {  // one OLS window's statistics (ddof = 0), null flags per N11
+  double vx, vy, cov, mx, my;
+  bool vxn, vyn, covn;
+};
+
+// CM:114-129: the window (t-50, t] of 50 present minutes; var / mean over the non-null
+// lows / highs, cov over the pairs with both; exact zero for identical values (C3)
+__device__ Win ols_window(const float* lo, const float* hi, const uint8_t* fl, int t) {
+  Win w;
+  int nx = 0, ny = 0, np_ = 0;
+  double x0 = 0.0, y0 = 0.0, px0 = 0.0, py0 = 0.0, sx = 0.0, sy = 0.0, spx = 0.0, spy = 0.0;
+  bool cx = true, cy = true, cpx = true, cpy = true;
+  for (int m = t - 49; m <= t; ++m) {
+    const bool xo = fl[m] & 1u, yo = fl[m] & 2u;
+    const double x = (double)lo[m], y = (double)hi[m];
+    if (xo) {
+      if (nx == 0) x0 = x;
+      cx = cx && x == x0;
+      sx += x - x0;
+      ++nx;
+    }
+    if (yo) {
+      if (ny == 0) y0 = y;
+      cy = cy && y == y0;
+      sy += y - y0;
+      ++ny;
+    }
+    if (xo && yo) {
+      if (np_ == 0) { px0 = x; py0 = y; }
+      cpx = cpx && x == px0;
+      cpy = cpy && y == py0;
+      spx += x - px0;
+      spy += y - py0;
+      ++np_;
+    }
+  }
+  w.vxn = nx == 0;
+  w.vyn = ny == 0;
+  w.covn = np_ == 0;
+  w.mx = nx ? x0 + sx / (double)nx : 0.0;
+  w.my = ny ? y0 + sy / (double)ny : 0.0;
+  const double mpx = np_ ? px0 + spx / (double)np_ : 0.0, mpy = np_ ? py0 + spy / (double)np_ : 0.0;
+  double axx = 0.0, ayy = 0.0, axy = 0.0;
+  for (int m = t - 49; m <= t; ++m) {
+    const bool xo = fl[m] & 1u, yo = fl[m] & 2u;
+    const double x = (double)lo[m], y = (double)hi[m];
+    if (xo) axx += (x - w.mx) * (x - w.mx);
+    if (yo) ayy += (y - w.my) * (y - w.my);
+    if (xo && yo) axy += (x - mpx) * (y - mpy);
+  }
+  w.vx = (w.vxn || cx) ? 0.0 : axx / (double)nx;
+  w.vy = (w.vyn || cy) ? 0.0 : ayy / (double)ny;
+  w.cov = (w.covn || cpx || cpy) ? 0.0 : axy / (double)np_;
+  return w;
+}
+
+struct Lds {  // per wave
+  uint32_t vw[256];   // volume per bar; 0xffffffff = null
+  float lo[NBAR], hi[NBAR];
+  uint8_t fl[NBAR];   // bit 0 low non-null, bit 1 high non-null (present bars)
+};
+
+__device__ void stock_day(const Args& a, int i, Lds& L) {
+  const int lane = lane_id();
+  const bool lv = lane < 60;
+  const uint32_t fam = a.fam;
+  const int sdi = __builtin_amdgcn_readfirstlane(a.sd_list[i]);
+  const int d = sdi / a.S;
+  const size_t sd = (size_t)sdi;
+  const Out out{a.val, a.state, a.row, sd, (size_t)a.D * a.S};
+
+  // ---- presence and null bits (N*: per field)
+  const Bits B = bits_of(a.nmask + (size_t)i * 8);
+  Bits NB[5];
+#pragma unroll
+  for (int f = 0; f < 5; ++f) NB[f] = band(bits_of(a.nbits + ((size_t)i * 5 + f) * 8), B);
+  bool p[4], okO[4], okH[4], okL[4], okC[4], okV[4], okR[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    p[k] = mine(B, k);
+    okO[k] = p[k] && !mine(NB[0], k);
+    okH[k] = p[k] && !mine(NB[1], k);
+    okL[k] = p[k] && !mine(NB[2], k);
+    okC[k] = p[k] && !mine(NB[3], k);
+    okV[k] = p[k] && !mine(NB[4], k);
+    okR[k] = okO[k] && okC[k];
+  }
+  const int n = count(B);
+  if (n == 0) {  // nothing to compute: every output stays ABSENT
+    if ((fam & F_PDF) && a.pdfq && lane < 5) a.pdfq[(size_t)lane * a.D * a.S + sd] = qnan();
+    return;
+  }
+  const int mf = first_of(B), ml = last_of(B);
+
+  float o[4], h[4], lo[4], c[4];
+  uint32_t v[4] = {0u, 0u, 0u, 0u};
+  auto load = [&](int f, float (&x)[4]) {
+    float4 t = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (lv) t = reinterpret_cast<const float4*>(a.fld[f] + sd * NBAR)[lane];
+    x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
+  };
+  load(0, o);
+  load(1, h);
+  load(2, lo);
+  load(3, c);
+  if (lv) {
+    const uint4 t = reinterpret_cast<const uint4*>(a.fld[4] + sd * NBAR)[lane];
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+  double vd_[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) vd_[k] = okV[k] ? (double)v[k] : 0.0;
+  const double sumv = msum(vd_, okV);         // volume.sum(): nulls skipped (N3)
+  const int nvok = count(ballot4(okV));
+  const Bits NO = NB[0], NC = NB[3], NV = NB[4];
+
+  // ================================================================ SEG CM:10-90
+  if (fam & F_SEG) {
+    auto seg = [&](int f, int ma, int mb) {
+      const bool pa = test(B, ma), pbb = test(B, mb);
+      if (!pa && !pbb) return;  // filtered set empty -> absent row
+      const int m0 = pa ? ma : mb, m1 = pbb ? mb : ma;
+      if (test(NC, m1) || test(NO, m0)) out.null(f);  // close.last() / open.first() (N1, N2)
+      else out.val1(f, (double)elem(c, m1) / (double)elem(o, m0));
+    };
+    seg(0, 120, 239);  // mmt_pm
+    seg(1, 210, 239);  // mmt_last30
+    seg(3, 0, 119);    // mmt_am
+    seg(4, 30, 209);   // mmt_between
+    // mmt_paratio CM:42-60 (C1: PM - AM); a null mmt nulls the difference
+    const Bits am = band(B, range_bits(0, 119)), pm = band(B, range_bits(120, 239));
+    double g[2];
+    bool gn[2];
+    int ng = 0;
+    if (any(am)) {
+      gn[ng] = test(NC, last_of(am)) || test(NO, first_of(am));
+      g[ng++] = (double)elem(c, last_of(am)) / (double)elem(o, first_of(am)) - 1.0;
+    }
+    if (any(pm)) {
+      gn[ng] = test(NC, last_of(pm)) || test(NO, first_of(pm));
+      g[ng++] = (double)elem(c, last_of(pm)) / (double)elem(o, first_of(pm)) - 1.0;
+    }
+    if (gn[ng - 1] || gn[0]) out.null(2);
+    else out.val1(2, g[ng - 1] - g[0]);
+  }
+
+  // ================================================================ MOMR / TRD returns
+  double r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r[k] = okR[k] ? (double)c[k] / (double)o[k] - 1.0 : 0.0;
+  if (fam & F_MOMR) {
+    const Mom mr = moments<4>(r, okR);  // the non-null returns (N3)
+    double sdr;
+    const bool has_sdr = std1(mr, sdr);
+    if (has_sdr) out.val1(16, sdr); else out.null(16);  // vol_return1min
+    bool up[4], dn[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      up[k] = okR[k] && tot_gt(r[k], 0.0);  // when(return > 0): a null takes otherwise(None)
+      dn[k] = okR[k] && tot_lt(r[k], 0.0);
+    }
+    double sup = 0.0, sdn = 0.0;
+    std1(moments<2>(r, up), sup);
+    std1(moments<2>(r, dn), sdn);
+    out.val1(17, sup);  // vol_upVol (fill_null(0))
+    out.val1(19, sdn);  // vol_downVol
+    if (has_sdr) {
+      out.val1(18, sup / sdr);
+      out.val1(20, sdn / sdr);
+    } else {
+      out.null(18);
+      out.null(20);
+    }
+    if (mr.n == 0) {  // skew / kurtosis of no value: null (S2 n = 0)
+      out.null(21);
+      out.null(22);
+      out.null(23);
+    } else {
+      const double sk = skew_b(mr), ku = kurt_b(mr);
+      out.val1(21, sk);
+      out.val1(22, ku);
+      out.val1(23, sk / ku);
+    }
+  }
+
+  // ================================================================ MOMV / MOMH
+  if (fam & F_MOMV) {
+    double sdv;
+    if (std1(moments<2>(vd_, okV), sdv)) out.val1(14, sdv); else out.null(14);  // vol_volume1min
+    if (nvok == 0) {  // volume / volume.sum() is all null
+      out.null(24);
+      out.null(25);
+      out.null(26);
+    } else {
+      double sh[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sh[k] = vd_[k] / sumv;
+      const Mom ms = moments<4>(sh, okV);
+      const double sk = skew_b(ms), ku = kurt_b(ms);
+      out.val1(24, sk);
+      out.val1(25, ku);
+      out.val1(26, sk / ku);
+    }
+  }
+  if (fam & F_MOMH) {
+    double hl[4];
+    bool okHL[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      okHL[k] = okH[k] && okL[k];
+      hl[k] = okHL[k] ? (double)h[k] / (double)lo[k] : 0.0;
+    }
+    double sdh;
+    if (std1(moments<2>(hl, okHL), sdh)) out.val1(15, sdh); else out.null(15);  // vol_range1min
+  }
+
+  // ================================================================ SUMV CM:764-831, 1251-1306
+  if (fam & F_SUMV) {
+    const int l4 = 4 * lane;
+    bool pre[4], cls[4], head[4], tail[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int m = l4 + k;
+      pre[k] = okV[k] && m <= 236;
+      cls[k] = okV[k] && m >= 237;
+      head[k] = okV[k] && m <= 30;
+      tail[k] = okV[k] && m >= 210;
+    }
+    const double spre = msum(vd_, pre), scls = msum(vd_, cls);
+    const double shead = msum(vd_, head), stail = msum(vd_, tail);
+    if (any(band(B, range_bits(0, 236)))) out.val1(28, spre);    // liq_closeprevol
+    if (any(band(B, range_bits(237, 239)))) out.val1(29, scls);  // liq_closevol
+    if (test(NV, mf)) {  // volume.first() is null (N2)
+      out.null(30);
+      out.null(32);
+    } else {
+      const double vfirst = (double)elem(v, mf);
+      out.val1(30, vfirst / sumv);  // liq_firstCallR
+      out.val1(32, vfirst);         // liq_openvol
+    }
+    out.val1(31, scls / sumv);  // liq_lastCallR
+    out.val1(52, sumv > 0.0 ? shead / sumv : 0.125);  // trade_headRatio
+    out.val1(53, sumv > 0.0 ? stail / sumv : 0.125);  // trade_tailRatio
+  }
+
+  // ================================================================ SUMC / CORR
+  double pcc[4];
+  bool pcok[4];
+  if (fam & (F_SUMC | F_CORR)) pct_ffill(c, okC, p, pcc, pcok);  // close.pct_change() (N5)
+  if (fam & F_SUMC) {
+    // liq_amihud_1min CM:739-760: volume.fill_null(0), |pct_change| fill_null(0)
+    double am[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) am[k] = (okV[k] && v[k] != 0u && pcok[k]) ? fabs(pcc[k]) / (double)v[k] : 0.0;
+    out.val1(27, msum(am, p));
+  }
+  if (fam & F_CORR) {
+    double cd[4], y[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cd[k] = (double)c[k];
+    // corr_prv CM:836-847: corr(close.pct_change(), volume), pairs without nulls (N4)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ok[k] = pcok[k] && okV[k];
+    out.val1(33, pearson(pcc, vd_, ok));
+    // corr_pv CM:877-888
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ok[k] = okC[k] && okV[k];
+    out.val1(35, pearson(cd, vd_, ok));
+    // corr_pvd CM:891-902: volume.shift(1) = the previous row's volume, null included (N6)
+    {
+      double vp[4];
+      bool vpok[4], hp[4];
+      prev_row(vd_, okV, p, vp, vpok, hp);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        ok[k] = okC[k] && vpok[k];
+        y[k] = ok[k] ? vp[k] : 0.0;
+      }
+      out.val1(36, pearson(cd, y, ok));
+    }
+    // corr_pvl CM:905-916: volume.shift(-1)
+    {
+      double vn[4];
+      uint32_t fw[4], fwn[4];
+      bool hn[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) fw[k] = okV[k] ? 1u : 0u;
+      next_valid(vd_, p, vn, hn);
+      next_valid(fw, p, fwn, hn);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        ok[k] = okC[k] && hn[k] && fwn[k] != 0u;
+        y[k] = ok[k] ? vn[k] : 0.0;
+      }
+      out.val1(37, pearson(cd, y, ok));
+    }
+    // corr_prvr CM:850-874 / corr_pvr CM:919-932: filter(volume != 0) -- a null volume
+    // compares null and is filtered out (N1) -- then pct_change over the kept rows
+    bool z[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) z[k] = okV[k] && v[k] != 0u;
+    if (any(ballot4(z))) {
+      double pcz[4], pvz[4];
+      bool pczok[4], pvzok[4];
+      pct_ffill(c, okC, z, pcz, pczok);
+      {  // volume pct_change over the kept rows (no null among them): exact u32 values
+        double vz[4], vzp[4];
+        bool vzf[4], vzpf[4], hz[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          vz[k] = (double)v[k];
+          vzf[k] = true;
+        }
+        prev_row(vz, vzf, z, vzp, vzpf, hz);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          pvzok[k] = z[k] && hz[k];
+          pvz[k] = pvzok[k] ? (vz[k] - vzp[k]) / vzp[k] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ok[k] = pczok[k] && pvzok[k];
+      out.val1(34, pearson(pcz, pvz, ok));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ok[k] = z[k] && okC[k] && pvzok[k];
+      out.val1(38, pearson(cd, pvz, ok));
+    }
+  }
+
+  // ================================================================ TRD CM:1206-1406
+  if (fam & F_TRD) {
+    const int l4 = 4 * lane;
+    bool t20[4], t50[4], h20[4], h50[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int m = l4 + k;
+      t20[k] = p[k] && m >= 220;
+      t50[k] = p[k] && m >= 190;
+      h20[k] = p[k] && m <= 20;
+      h50[k] = p[k] && m <= 50;
+    }
+    auto tail = [&](const bool (&tm)[4], int f, bool plus_one) {
+      bool tv[4], tb[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        tv[k] = tm[k] && okV[k];
+        tb[k] = tv[k] && okR[k];  // volume_d * ret is null unless both are (N1)
+      }
+      double den = msum(vd_, tv);
+      den = plus_one ? den + 1.0 : (den == 0.0 ? 1.0 : den);
+      double tmp[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) tmp[k] = (vd_[k] / den) * r[k];
+      out.val1(f, msum(tmp, tb));
+    };
+    if (any(band(B, range_bits(220, 239)))) tail(t20, 50, true);   // trade_bottom20retRatio
+    if (any(band(B, range_bits(190, 239)))) tail(t50, 51, false);  // trade_bottom50retRatio
+    // trade_top{20,50}retRatio, topNeg20, topPos20: mean over the non-null quotients (N3)
+    auto headf = [&](const bool (&hm)[4], int lo_, int hi_, int f_all, int f_neg, int f_pos) {
+      if (!any(band(B, range_bits(lo_, hi_)))) return;
+      bool hv[4], ha[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        hv[k] = hm[k] && okV[k];
+        ha[k] = hv[k] && okR[k];
+      }
+      const double sh = msum(vd_, hv);
+      double ta[4], tn[4], tp[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double vdk = vd_[k] / sh;
+        ta[k] = r[k] / vdk;
+        // when(pct < 0 / > 0): a null pct takes otherwise(0) (N1)
+        tn[k] = ((okR[k] && r[k] < 0.0) ? fabs(r[k]) : 0.0) / vdk;
+        tp[k] = ((okR[k] && r[k] > 0.0) ? fabs(r[k]) : 0.0) / vdk;
+      }
+      const int na = count(ballot4(ha)), nv = count(ballot4(hv));
+      if (na > 0) out.val1(f_all, msum(ta, ha) / (double)na); else out.null(f_all);
+      if (f_neg >= 0) {
+        if (nv > 0) {
+          out.val1(f_neg, msum(tn, hv) / (double)nv);
+          out.val1(f_pos, msum(tp, hv) / (double)nv);
+        } else {
+          out.null(f_neg);
+          out.null(f_pos);
+        }
+      }
+    };
+    headf(h20, 0, 20, 54, 56, 57);
+    headf(h50, 0, 50, 55, -1, -1);
+  }
+
+  // ================================================================ ORD / ORDV (N7)
+  if (fam & (F_ORD | F_ORDV)) {
+    uint32_t key[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) key[k] = okV[k] ? v[k] : 0xffffffffu;  // nulls sort last
+    bitonic256(key);
+    const int nn = nvok;
+    if ((fam & F_ORD) && nn > 0) {  // no non-null volume: the filter keeps no row (absent)
+      const uint32_t th50 = elem(key, nn >= 50 ? nn - 50 : 0);
+      const uint32_t th20 = elem(key, nn >= 20 ? nn - 20 : 0);
+      const uint32_t tb50 = elem(key, nn >= 50 ? 49 : nn - 1);
+      double q50[4], q20[4], qb50[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double ret = (double)c[k] / (double)o[k];
+        const bool use = okV[k] && okR[k];  // a null ret is skipped by product() (N3)
+        q50[k] = (use && v[k] >= th50) ? ret : 1.0;
+        q20[k] = (use && v[k] >= th20) ? ret : 1.0;
+        qb50[k] = (use && v[k] <= tb50) ? ret : 1.0;
+      }
+      const double pb50 = 0.0 + (wprod(qb50[0] * qb50[1] * qb50[2] * qb50[3]) - 1.0);
+      out.val1(10, wprod(q50[0] * q50[1] * q50[2] * q50[3]) - 1.0);
+      out.val1(11, pb50);
+      out.val1(12, wprod(q20[0] * q20[1] * q20[2] * q20[3]) - 1.0);
+      out.val1(13, pb50);  // bottom_k(50) [sic CM:471]
+    }
+    if (fam & F_ORDV) {
+      if (nn == 0) {  // top_k of null shares sums to 0
+        out.val1(47, 0.0);
+        out.val1(48, 0.0);
+        out.val1(49, 0.0);
+      } else {
+        const int l4 = 4 * lane;
+        double t10 = 0.0, t5 = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int e = l4 + k;
+          const double x = (double)key[k];
+          if (e < nn && e >= nn - 10) t10 += x;
+          if (e < nn && e >= nn - 5) t5 += x;
+        }
+        t10 = wsum(t10);
+        t5 = wsum(t5);
+        out.val1(47, t10 / sumv);
+        out.val1(48, t5 / sumv);
+        out.val1(49, t5 / sumv);  // top_k(5) [sic CM:1196]
+      }
+    }
+  }
+
+  // ================================================================ LVL / PDF (N2, N8, N10, C8)
+  if (fam & (F_LVL | F_PDF)) {
+    // key = close.last() / close: null when the close is null or close.last() is (N2);
+    // the null group sorts first (high word 0: C8), then ascending key = descending close
+    const bool lastnull = test(NC, ml);
+    if (lv) {
+      uint4 w;
+      w.x = okV[0] ? v[0] : 0xffffffffu;
+      w.y = okV[1] ? v[1] : 0xffffffffu;
+      w.z = okV[2] ? v[2] : 0xffffffffu;
+      w.w = okV[3] ? v[3] : 0xffffffffu;
+      *reinterpret_cast<uint4*>(L.vw + 4 * lane) = w;
+    }
+    uint64_t key[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t hiw = (lastnull || !okC[k]) ? 0u : ~fbits(c[k]);
+      key[k] = p[k] ? (((uint64_t)hiw << 32) | (uint32_t)(4 * lane + k)) : ~0ull;
+    }
+    bitonic256(key);
+    __builtin_amdgcn_wave_barrier();
+    const int l4 = 4 * lane;
+    uint32_t hi[4];
+    double vs[4];
+    uint32_t hvn[4];
+    bool valid[4], lend[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hi[k] = (uint32_t)(key[k] >> 32);
+      valid[k] = (l4 + k) < n;
+      const uint32_t w = valid[k] ? L.vw[(uint32_t)key[k] & 0xffu] : 0xffffffffu;
+      vs[k] = (valid[k] && w != 0xffffffffu) ? (double)w : 0.0;
+      hvn[k] = (valid[k] && w != 0xffffffffu) ? 1u : 0u;
+    }
+    const uint32_t hnext0 = (uint32_t)__shfl_down((int)hi[0], 1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t hn = (k < 3) ? hi[k + 1] : hnext0;
+      lend[k] = valid[k] && ((l4 + k) == n - 1 || hn != hi[k]);
+    }
+    double cum[4] = {vs[0], vs[1], vs[2], vs[3]};
+    scan4(cum);       // exact: integer volumes
+    scan4_u32(hvn);   // non-null volumes so far
+    double pcum[4];
+    uint32_t phv[4];
+    bool hpc[4];
+    prev_valid(cum, lend, pcum, hpc);
+    prev_valid(hvn, lend, phv, hpc);
+    bool lhas[4];  // the level holds a non-null volume (its share sum is V / sum(v), else 0)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lhas[k] = lend[k] && (hvn[k] - (hpc[k] ? phv[k] : 0u)) != 0u;
+
+    if ((fam & F_PDF) && a.pdfq) {
+      const double cl = (double)elem(c, ml);
+      // the stock-day's non-null levels (N8: a null key is not ranked), one reservation
+      bool emit[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) emit[k] = lend[k] && hi[k] != 0u;
+      const Bits LE = ballot4(emit);
+      const int Lc = count(LE);
+      if (Lc > 0) {
+        const uint64_t lt = (1ull << lane) - 1ull;
+        uint32_t idx = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) idx += (uint32_t)__popcll(LE.b[k] & lt);
+        uint32_t base = 0u;
+        if (lane == 0) base = atomicAdd(a.lvl_count + d, (uint32_t)Lc);
+        idx += (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        double pos[4] = {(double)l4, (double)(l4 + 1), (double)(l4 + 2), (double)(l4 + 3)};
+        double ppos[4];
+        bool hpp[4];
+        prev_valid(pos, lend, ppos, hpp);
+        const size_t cap = (size_t)a.S * NBAR;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (emit[k]) {
+            a.lvl_key[(size_t)d * cap + idx] = ord64(cl / (double)bitsf(~hi[k]));
+            a.lvl_w[(size_t)d * cap + idx] = (uint8_t)(l4 + k - (hpp[k] ? (int)ppos[k] : -1));
+            ++idx;
+          }
+      }
+      // threshold level for p = k/20 (CM:1022-1026, C2 / C8): the first level whose
+      // cumulative share passes p; exact comparison 20 cum > k sum(v) of the integer sums
+      const double kk[5] = {12.0, 14.0, 16.0, 18.0, 19.0};
+      const double pp[5] = {0.6, 0.7, 0.8, 0.9, 0.95};
+      int est[5];
+      bool need_seq = false;
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        if (nvok == 0) {  // every share null: level sums 0, no level passes
+          est[t] = -1;
+          continue;
+        }
+        if (sumv == 0.0) {  // shares NaN on levels with a non-null volume; NaN > p (S11)
+          est[t] = first_of(ballot4(lhas));
+          continue;
+        }
+        bool ps[4], ts[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const double lhs = 20.0 * cum[k], rhs = kk[t] * sumv;
+          ps[k] = lend[k] && lhs > rhs;
+          ts[k] = lend[k] && lhs == rhs;
+        }
+        const int ep = first_of(ballot4(ps));
+        const int et = first_of(ballot4(ts));
+        est[t] = ep;
+        if (et >= 0 && (ep < 0 || et < ep)) need_seq = true;
+      }
+      if (need_seq) {
+        // an exact tie: the reference's float sequence (level sums of the non-null shares
+        // in bar order, cum-summed in level order, compared with p as f64)
+        double VD = 0.0, cs = 0.0;
+        int done = 0;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) est[t] = -1;
+        for (int e = 0; e < n; ++e) {
+          const uint64_t ke = elem(key, e);
+          const uint32_t w = L.vw[(uint32_t)ke & 0xffu];
+          if (w != 0xffffffffu) VD = VD + (double)w / sumv;
+          const bool is_end = (e == n - 1) || ((uint32_t)(elem(key, e + 1) >> 32) != (uint32_t)(ke >> 32));
+          if (is_end) {
+            cs = cs + VD;
+            VD = 0.0;
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+              if (est[t] < 0 && tot_gt(cs, pp[t])) {
+                est[t] = e;
+                ++done;
+              }
+            if (done == 5) break;
+          }
+        }
+      }
+      double qv = qnan();
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        double q = qnan();  // no level passes, or the null level does (sort() puts it first)
+        if (est[t] >= 0) {
+          const uint32_t hk = (uint32_t)(elem(key, est[t]) >> 32);
+          if (hk != 0u) q = cl / (double)bitsf(~hk);
+        }
+        if (lane == t) qv = q;
+      }
+      if (lane < 5) a.pdfq[(size_t)lane * a.D * a.S + sd] = qv;
+#pragma unroll
+      for (int t = 0; t < 5; ++t) out.null(PDF0 + t);  // filled by the doc_pdf finalize
+    }
+    if (fam & F_LVL) {
+      double xl[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double Vl = lend[k] ? cum[k] - (hpc[k] ? pcum[k] : 0.0) : 0.0;
+        xl[k] = lhas[k] ? Vl / sumv : 0.0;  // a level of null volumes sums to 0 (N3)
+      }
+      const Mom mlv = moments<4>(xl, lend);
+      const double sk = skew_b(mlv), ku = kurt_b(mlv);
+      out.val1(39, ku);  // doc_kurt
+      out.val1(40, sk);  // doc_skew
+      out.val1(41, sk);  // doc_std: .skew() [sic CM:999]
+    }
+  }
+
+  // ================================================================ OLS CM:93-376 (N11)
+  if (fam & F_OLS) {
+    if (lv) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        L.lo[4 * lane + k] = lo[k];
+        L.hi[4 * lane + k] = h[k];
+        L.fl[4 * lane + k] = (uint8_t)((okL[k] ? 1u : 0u) | (okH[k] ? 2u : 0u));
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // window t: a row at t and all of t-49..t present (pl.len() = 50 rows, CM:129)
+    uint32_t pc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pc[k] = p[k] ? 1u : 0u;
+    scan4_u32(pc);
+    double beta[4], q[4], cs[4], cr[4];
+    bool okw[4], okb[4], okq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = 4 * lane + k;
+      const int src = (k < 2) ? lane - 13 : lane - 12;  // element t-50 at (src, k +- 2)
+      const int ks = (k < 2) ? k + 2 : k - 2;
+      uint32_t b = bperm(src < 0 ? 0 : src, ks == 0 ? pc[0] : ks == 1 ? pc[1] : ks == 2 ? pc[2] : pc[3]);
+      if (t - 50 < 0) b = 0u;
+      okw[k] = lv && p[k] && t >= 49 && pc[k] - b == 50u;
+      beta[k] = q[k] = cs[k] = cr[k] = 0.0;
+      okb[k] = okq[k] = false;
+      if (okw[k]) {
+        const Win w = ols_window(L.lo, L.hi, L.fl, t);
+        // CM:131-134: when(var_x != 0) cov / var_x, otherwise mean_y / mean_x (null cond
+        // or null operand: N1)
+        if (!w.vxn && w.vx != 0.0) {
+          okb[k] = !w.covn;
+          beta[k] = w.cov / w.vx;
+        } else {
+          okb[k] = !w.vxn && !w.vyn;
+          beta[k] = w.my / w.mx;
+        }
+        const double prod = w.vx * w.vy;
+        okq[k] = !w.vxn && !w.vyn && prod != 0.0 && !w.covn;
+        if (okq[k]) {
+          q[k] = sqrt(w.cov) / prod;      // cov**0.5 / (vx*vy)   CM:137
+          cs[k] = (w.cov * w.cov) / prod;  // cov**2 / (vx*vy)     CM:212
+          cr[k] = w.cov / sqrt(prod);      // cov / (vx*vy)**0.5   CM:261
+        }
+        if (!okb[k]) beta[k] = 0.0;
+      }
+    }
+    const Bits WB = ballot4(okw);
+    const int W = count(WB);
+    if (W > 0) {
+      const Mom mb = moments<2>(beta, okb);  // the non-null betas (N3)
+      const double bmean = mb.mean;
+      double bstd = 0.0;
+      const bool has_std = std1(mb, bstd);
+      const int lw = last_of(WB);
+      const bool blast_ok = test(ballot4(okb), lw);  // beta.last(): null included (N2)
+      const double blast = elem(beta, lw);
+      const int Wq = count(ballot4(okq));
+      const double sq = msum(q, okq), scs = msum(cs, okq), scr = msum(cr, okq);
+      if (has_std && tot_ne(bstd, 0.0) && Wq > 0) {  // mmt_ols_qrs CM:156-171
+        if (blast_ok) out.val1(5, (sq / (double)Wq) * (blast - bmean) / bstd); else out.null(5);
+      } else {
+        out.val1(5, 0.0);
+      }
+      out.val1(6, Wq > 0 ? scs / (double)Wq : 0.0);  // corr_square_mean, fill_null(0)
+      out.val1(7, Wq > 0 ? scr / (double)Wq : 0.0);  // corr_mean, fill_null(0)
+      if (mb.n > 0) out.val1(8, bmean); else out.null(8);  // beta_mean
+      if (has_std && tot_gt(bstd, 0.0)) {  // beta_zscore_last CM:369-373
+        if (blast_ok) out.val1(9, (blast - bmean) / bstd); else out.null(9);
+      } else if (mb.n > 0) {
+        out.val1(9, bmean);
+      } else {
+        out.null(9);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_stage1_nulls(Args a) {
+  __shared__ Lds lds[WPB];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = gridDim.x * WPB;
+  for (int i = blockIdx.x * WPB + wave; i < a.K; i += nw) stock_day(a, i, lds[wave]);
+}
+
+}  // namespace nul
+
+size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w);
+
+}  // namespace mff
+
+using namespace mff;
+
+extern "C" int mff_stage1_nulls(const float* open, const float* high, const float* low, const float* close,
+                                const uint32_t* volume, int S, int D, const int32_t* null_sd,
+                                const uint32_t* null_mask, const uint32_t* null_bits, int K,
+                                const int32_t* factor_ids, int nf, double* val, uint8_t* state,
+                                double* pdf_query, void* pdf_levels, int phase, void* stream) {
+  clear_error();
+  MFF_REQUIRE(S > 0 && D > 0 && (long long)S * D < (1ll << 31), "mff_stage1_nulls: bad sizes S=%d D=%d", S, D);
+  MFF_REQUIRE(K >= 0, "mff_stage1_nulls: K=%d", K);
+  MFF_REQUIRE(phase >= 1 && phase <= 3, "mff_stage1_nulls: phase=%d must be 1, 2 or 3", phase);
+  MFF_REQUIRE(nf > 0 && nf <= NF && factor_ids, "mff_stage1_nulls: bad factor list");
+  if (K == 0) return 0;
+  MFF_REQUIRE(open && high && low && close && volume && null_sd && null_mask && null_bits && val && state,
+              "mff_stage1_nulls: NULL buffer");
+  nul::Args a;
+  memset(&a, 0, sizeof(a));
+  a.fld[0] = open; a.fld[1] = high; a.fld[2] = low; a.fld[3] = close;
+  a.fld[4] = reinterpret_cast<const float*>(volume);
+  a.sd_list = null_sd; a.nmask = null_mask; a.nbits = null_bits; a.K = K;
+  a.val = val; a.state = state; a.S = S; a.D = D;
+  for (int i = 0; i < NF; ++i) a.row[i] = -1;
+  for (int r = 0; r < nf; ++r) {
+    const int id = factor_ids[r];
+    MFF_REQUIRE(id >= 0 && id < NF, "mff_stage1_nulls: factor id %d out of range", id);
+    a.row[id] = (int8_t)r;
+    a.fam |= kFactorFamily[id];
+  }
+  if (phase == 1) a.fam &= F_PDF;
+  if (phase == 2) a.fam &= ~F_PDF;
+  if (!a.fam) return 0;
+  if (a.fam & F_PDF) {
+    MFF_REQUIRE(pdf_query && pdf_levels, "mff_stage1_nulls: doc_pdf needs pdf_query and pdf_levels");
+    size_t ok, ow;
+    pdf_levels_split(S, D, &ok, &ow);
+    char* base = reinterpret_cast<char*>(pdf_levels);
+    a.pdfq = pdf_query;
+    a.lvl_count = reinterpret_cast<uint32_t*>(base);
+    a.lvl_key = reinterpret_cast<uint64_t*>(base + ok);
+    a.lvl_w = reinterpret_cast<uint8_t*>(base + ow);
+  }
+  const int blocks = (K + nul::WPB - 1) / nul::WPB < 4096 ? (K + nul::WPB - 1) / nul::WPB : 4096;
+  hipLaunchKernelGGL(nul::k_stage1_nulls, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+  MFF_LAUNCH_CHECK();
+  return 0;
+}

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib, catalog
-from .synth import pack_mask, stack_fields
+from .synth import null_set, pack_mask, stack_fields
 
 ABSENT, NULL, VALUE = 0, 1, 2
 VOLUME_MAX = 2 ** 32 - 2  # MFF_VOLUME_MAX: u32 shares per bar (all-ones = absent sort key)
@@ -34,12 +34,51 @@ def _stream(device) -> int:
 
 
 @dataclass
+class NullSet:
+    """The stock-days of a panel that hold polars nulls (rows that exist with a null
+    field), in the layout of ``mff_stage1_nulls`` (include/mff.h): ``sd`` int32 [K]
+    (d*S + s, ascending), ``mask`` int32 [K][8] their presence words (the panel's own mask
+    holds zeros there), ``bits`` int32 [K][5][8] null bits of open, high, low, close,
+    volume.  All on the panel's device."""
+
+    sd: torch.Tensor
+    mask: torch.Tensor
+    bits: torch.Tensor
+
+    @property
+    def K(self) -> int:
+        return int(self.sd.numel())
+
+    @classmethod
+    def from_host(cls, sd, mask, bits, device) -> Optional["NullSet"]:
+        if len(sd) == 0:
+            return None
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(device)
+        return cls(t(np.asarray(sd, np.int32)), t(np.asarray(mask, np.uint32)), t(np.asarray(bits, np.uint32)))
+
+    def host(self):
+        """(sd int64, mask uint32 [K][8], bits uint32 [K][5][8]) numpy copies."""
+        return (self.sd.cpu().numpy().astype(np.int64), self.mask.cpu().numpy().view(np.uint32),
+                self.bits.cpu().numpy().view(np.uint32))
+
+    def shard(self, S: int, s0: int, s1: int, device=None) -> Optional["NullSet"]:
+        """The null stock-days of stocks [s0, s1) re-indexed to a shard of S1 - s0 stocks."""
+        sd, mask, bits = self.host()
+        d, s = sd // S, sd % S
+        keep = (s >= s0) & (s < s1)
+        nsd = d[keep] * (s1 - s0) + (s[keep] - s0)
+        return NullSet.from_host(nsd.astype(np.int32), mask[keep], bits[keep], device or self.sd.device)
+
+
+@dataclass
 class DevicePanel:
     """One device's dense panel.
 
     bars: [5][D][S][240] 4-byte words: open, high, low, close (float32) and the volume
           plane's u32 shares (include/mff.h); a float32 tensor, plane 4 viewed as ints
-    mask: int32 [D][S][8] presence bits (bit m%32 of word m//32)
+    mask: int32 [D][S][8] presence bits (bit m%32 of word m//32); zero for the stock-days
+          listed in ``nulls``
+    nulls: the stock-days that hold polars nulls (computed by mff_stage1_nulls), or None
     """
 
     bars: torch.Tensor
@@ -49,6 +88,7 @@ class DevicePanel:
     # ingest with skip_bad: {input table index: reason} of the tables dropped (their days
     # hold no bars)
     dropped: dict = field(default_factory=dict)
+    nulls: Optional[NullSet] = None
 
     @property
     def D(self) -> int:
@@ -71,18 +111,25 @@ class DevicePanel:
         contract the kernels rely on (include/mff.h)."""
         validate_host_panel(panel)
         bars = torch.from_numpy(np.ascontiguousarray(stack_fields(panel))).to(device)
-        mask = torch.from_numpy(pack_mask(panel["present"]).view(np.int32)).to(device)
-        return cls(bars, mask, list(panel["codes"]), list(panel["dates"]))
+        words = pack_mask(panel["present"])
+        sd, nmask, nbits = null_set(panel)
+        if sd.size:  # the null-holding stock-days go to mff_stage1_nulls only
+            words.reshape(-1, 8)[sd] = 0
+        mask = torch.from_numpy(words.view(np.int32)).to(device)
+        return cls(bars, mask, list(panel["codes"]), list(panel["dates"]),
+                   nulls=NullSet.from_host(sd, nmask, nbits, device))
 
 
 def validate_host_panel(panel) -> None:
     pres = panel["present"]
-    v = np.asarray(panel["volume"][pres], dtype=np.float64)
+    nb = panel.get("null")
+    ok = lambda i: pres if nb is None else pres & ((nb >> i) & 1 == 0)  # non-null present bars
+    v = np.asarray(panel["volume"][ok(4)], dtype=np.float64)
     if v.size and (not np.all(np.isfinite(v)) or np.any(v < 0) or np.any(v > VOLUME_MAX)
                    or np.any(v != np.rint(v))):
         raise ValueError(f"volume must be integral and within [0, {VOLUME_MAX}] shares")
-    for k in ("open", "high", "low", "close"):
-        x = panel[k][pres]
+    for i, k in enumerate(("open", "high", "low", "close")):
+        x = panel[k][ok(i)]
         if x.size and (not np.all(np.isfinite(x)) or np.any(x <= 0)):
             raise ValueError(f"{k} must be finite and > 0 on present bars")
 
@@ -121,6 +168,19 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
     if frame_pdf and comm is not None:
         raise ValueError("frame-wide doc_pdf ranks of a multi-date frame are single-GPU; "
                          "shard day files (per-day semantics) instead")
+    nl = panel.nulls
+
+    def nulls_phase(phase: int, stream) -> None:
+        """mff_stage1_nulls for the null-holding stock-days (ABSENT to every other launch):
+        phase 1 = doc_pdf queries + levels (before the doc_pdf sort), 2 = the other rows
+        (after every launch that writes them)."""
+        if nl is None or (phase == 1 and not need_pdf):
+            return
+        _lib.check(lib.mff_stage1_nulls(*args[:5], S, D, _lib.ptr(nl.sd), _lib.ptr(nl.mask), _lib.ptr(nl.bits),
+                                        nl.K, _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
+                                        _lib.ptr(pdfq), _lib.ptr(levels), phase, stream.cuda_stream),
+                   f"mff_stage1_nulls({phase})")
+
     if events is not None:
         events[0].record(main)
     if need_pdf and PDF_OVERLAP and not frame_pdf:
@@ -140,6 +200,7 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
         if PDF_FIRST:
             # the doc_pdf phases (whole-CU workgroups) on the launch stream before part 2:
             # behind the wave-pair kernel they only get CUs its blocks have drained
+            nulls_phase(1, main)
             pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
             if hl is not None and HL_AT == "pdf":
                 launch_hl()
@@ -149,6 +210,7 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             side.wait_stream(main)
             if EXACT_SIDE:  # the exact list kernel ahead of the doc_pdf phases, off the launch stream
                 _lib.check(lib.mff_stage1_part(*(args[:-1] + [side.cuda_stream]), 32), "mff_stage1_part(32)")
+            nulls_phase(1, side)
             sorted_ev = torch.cuda.Event() if SORT_FIRST and comm is None else None
             with torch.cuda.stream(side):
                 pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch,
@@ -161,14 +223,17 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             launch_hl()
         if hl is not None:
             main.wait_stream(hl)
+        nulls_phase(2, main)
         if events is not None:  # after the doc_pdf tail on the side stream
             events[1].record(main)
         return val, state, ids
     _lib.check(lib.mff_stage1(*args), "mff_stage1")
+    nulls_phase(1, main)
     if frame_pdf:
         pdf_ranks_frame(panel, pdfq, levels, rows, val, state)
     elif need_pdf:
         pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
+    nulls_phase(2, main)
     if events is not None:
         events[1].record(main)
     return val, state, ids
@@ -213,6 +278,20 @@ def _side_stream(dev, which: int = 0) -> torch.cuda.Stream:
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(dev, priority=HL_PRIO if which == 1 else PDF_PRIO)
     return _SIDE[key]
+
+
+def stage1_frame(panel: DevicePanel, ids: Sequence[int], val, state) -> None:
+    """Overwrite the rows of the four factors whose windows run over('code') only
+    (liq_amihud_1min, corr_prvr, trade_bottom20/50retRatio) with the semantics of ONE
+    reference call on the panel's multi-date frame (mff_stage1_frame, csrc/mff_frame.hip),
+    null-holding stock-days included."""
+    lib = _lib.load()
+    b, nl = panel.bars, panel.nulls
+    _lib.check(lib.mff_stage1_frame(_lib.ptr(b[0]), _lib.ptr(b[3]), _lib.ptr(b[4]), _lib.ptr(panel.mask),
+                                    panel.S, panel.D, _lib.ptr(nl.sd) if nl else None,
+                                    _lib.ptr(nl.mask) if nl else None, _lib.ptr(nl.bits) if nl else None,
+                                    nl.K if nl else 0, _lib.int_array(list(ids)), len(ids), _lib.ptr(val),
+                                    _lib.ptr(state), _stream(panel.device)), "mff_stage1_frame")
 
 
 def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows: List[int], val, state,

@@ -41,7 +41,7 @@ def compute_dense(df, names: Sequence[str] | None = None, device=None, per_day: 
     :func:`compute_long`."""
     import torch
 
-    from . import _lib, engine, ingest
+    from . import engine, ingest
 
     names = list(catalog.NAMES if names is None else
                  [n[4:] if n.startswith("cal_") else n for n in names])
@@ -50,12 +50,7 @@ def compute_dense(df, names: Sequence[str] | None = None, device=None, per_day: 
     dp = ingest.to_device_panel(df, _device(device), skip_bad=skip_bad)  # GPU long -> dense (mff_ingest_rows)
     val, state, ids = engine.compute_factors(dp, names, frame=not per_day)
     if not per_day and dp.D > 1 and any(n in FRAME_XDAY for n in names):
-        lib = _lib.load()
-        b = dp.bars
-        _lib.check(lib.mff_stage1_frame(_lib.ptr(b[0]), _lib.ptr(b[3]), _lib.ptr(b[4]), _lib.ptr(dp.mask),
-                                        dp.S, dp.D, _lib.int_array(ids), len(ids), _lib.ptr(val),
-                                        _lib.ptr(state), torch.cuda.current_stream(dp.device).cuda_stream),
-                   "mff_stage1_frame")
+        engine.stage1_frame(dp, ids, val, state)
     torch.cuda.synchronize(dp.device)
     return val.cpu().numpy(), state.cpu().numpy(), names, dp.codes, dp.dates, dp.dropped
 

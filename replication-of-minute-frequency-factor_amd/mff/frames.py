@@ -43,18 +43,28 @@ def minute_to_time(m: np.ndarray) -> np.ndarray:
     return (clock // 60) * 10000000 + (clock % 60) * 100000
 
 
-def _columns(df) -> Dict[str, np.ndarray]:
+def _columns(df):
+    """Frame -> ({name: numpy values}, {name: null mask}) -- a null mask only for the
+    columns holding polars nulls (pyarrow nulls, pandas None / pd.NA); a float NaN is a
+    value, not a null."""
     if hasattr(df, "to_arrow") and not hasattr(df, "to_pandas_dtype"):
         df = df.to_arrow()
-    try:
-        import pyarrow as pa
-        if isinstance(df, pa.Table):
-            return {n: df.column(n).to_numpy(zero_copy_only=False) for n in df.column_names}
-    except ImportError:  # pragma: no cover
-        pass
-    if isinstance(df, dict):
-        return {k: np.asarray(v) for k, v in df.items()}
-    return {c: df[c].to_numpy() for c in df.columns}
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    if not isinstance(df, pa.Table):
+        if isinstance(df, dict):
+            df = {k: np.asarray(v) for k, v in df.items()}
+            return df, {}
+        df = pa.Table.from_pandas(df, preserve_index=False)
+    vals, nulls = {}, {}
+    for n in df.column_names:
+        col = df.column(n)
+        if col.null_count and n in FIELDS:
+            nulls[n] = np.asarray(col.is_null().to_numpy(zero_copy_only=False), dtype=bool)
+            col = pc.fill_null(col.cast(pa.float64()), 0.0 if n == "volume" else 1.0)
+        vals[n] = col.to_numpy(zero_copy_only=False)
+    return vals, nulls
 
 
 def _as_date(x):
@@ -73,8 +83,9 @@ def _as_date(x):
 
 def to_dense(df, codes: Sequence[str] | None = None) -> Dict:
     """Long frame -> host panel dict (see mff.synth): float32 price planes and a float64
-    volume plane [D][S][240], present mask, sorted codes and dates."""
-    cols = _columns(df)
+    volume plane [D][S][240], present mask, sorted codes and dates; ``null`` (uint8
+    [D][S][240], bit i = FIELDS[i]) when a row holds a polars null (values there NaN)."""
+    cols, nulls = _columns(df)
     for k in ("code", "date", "time") + FIELDS:
         if k not in cols:
             raise ValueError(f"missing column {k!r}")
@@ -103,6 +114,13 @@ def to_dense(df, codes: Sequence[str] | None = None) -> Dict:
     pres = np.zeros(D * S * MINUTES, dtype=bool)
     pres[flat] = True
     panel["present"] = pres.reshape(D, S, MINUTES)
+    if nulls:
+        nb = np.zeros(D * S * MINUTES, dtype=np.uint8)
+        for i, k in enumerate(FIELDS):
+            if k in nulls:
+                nb[flat[nulls[k]]] |= np.uint8(1 << i)
+                panel[k].reshape(-1)[flat[nulls[k]]] = np.nan
+        panel["null"] = nb.reshape(D, S, MINUTES)
     panel["codes"] = ucodes
     panel["dates"] = udates
     return panel

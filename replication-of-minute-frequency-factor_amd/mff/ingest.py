@@ -82,29 +82,37 @@ def _one(col):
     return col
 
 
-def _numeric(col, dtype):
+def _numeric(col, dtype, fill=float("nan")):
+    """Column -> contiguous numpy array and its null mask (None when it has no null);
+    nulls are replaced by ``fill``."""
     import pyarrow as pa
     import pyarrow.compute as pc
 
     col = _one(col)
+    isnull = None
     if col.null_count:
-        col = pc.fill_null(col.cast(pa.float64()), float("nan"))
-    return np.ascontiguousarray(col.to_numpy(zero_copy_only=False), dtype=dtype)
+        isnull = np.asarray(col.is_null().to_numpy(zero_copy_only=False), dtype=bool)
+        col = pc.fill_null(col.cast(pa.float64()), fill)
+    return np.ascontiguousarray(col.to_numpy(zero_copy_only=False), dtype=dtype), isnull
 
 
 def _volume(col):
-    """A null volume is 0 shares: the reference's volume sums skip nulls and
-    liq_amihud_1min fills them with 0 (CM:743-744)."""
+    """Volume column -> (values, MFF_VOLUME_* kind, null mask or None).  A null volume is
+    NOT 0 shares: polars keeps it null everywhere except cal_liq_amihud_1min's
+    fill_null(0) (CM:743-744), so the row's null bit travels to mff_stage1_nulls; the
+    value under it is 0 (never read as a volume)."""
     import pyarrow.compute as pc
 
     col = _one(col)
+    isnull = None
     if col.null_count:
+        isnull = np.asarray(col.is_null().to_numpy(zero_copy_only=False), dtype=bool)
         col = pc.fill_null(col, 0)
     arr = col.to_numpy(zero_copy_only=False)
     arr = np.ascontiguousarray(arr)
     if arr.dtype not in _VOLUME_KIND:
         arr = arr.astype(np.float64)
-    return arr, _VOLUME_KIND[arr.dtype]
+    return arr, _VOLUME_KIND[arr.dtype], isnull
 
 
 def _dict_codes(t):
@@ -183,10 +191,23 @@ def encode(t, codes: Sequence[str], day_numbers: Sequence[int]):
     else:
         day = np.searchsorted(uday, dn).astype(np.int32)
         day[(day >= uday.size) | (uday[np.minimum(day, uday.size - 1)] != dn)] = -1
-    time = _numeric(t.column("time"), np.int64)
-    px = [_numeric(t.column(k), np.float64) for k in FIELDS[:4]]
-    vol, kind = _volume(t.column("volume"))
-    return stock, day, time, px, vol, kind
+    time, tnull = _numeric(t.column("time"), np.int64, fill=-1)  # a null time is off the grid
+    # a null price is 1.0 for the ingest kernel's contract check; its null bit (bit i of
+    # the row's byte = FIELDS[i]) keeps it out of every factor (mff_stage1_nulls)
+    px, nulls = [], []
+    for k in FIELDS[:4]:
+        x, isn = _numeric(t.column(k), np.float64, fill=1.0)
+        px.append(x)
+        nulls.append(isn)
+    vol, kind, vnull = _volume(t.column("volume"))
+    nulls.append(vnull)
+    nbits = None
+    if any(m is not None for m in nulls):
+        nbits = np.zeros(stock.size, np.uint8)
+        for i, m in enumerate(nulls):
+            if m is not None:
+                nbits |= m.astype(np.uint8) << i
+    return stock, day, time, px, vol, kind, nbits
 
 
 class PanelIngest:
@@ -195,7 +216,16 @@ class PanelIngest:
     ``push(table)`` stages one table (any number of days / stocks of the universes) and
     launches its H2D copy and scatter asynchronously; ``finish()`` checks the error
     counters (raising ValueError like :func:`frames.to_dense`) and returns the
-    :class:`mff.engine.DevicePanel`."""
+    :class:`mff.engine.DevicePanel`.
+
+    Rows with a null field are ingested like any other (the null price as 1.0, the null
+    volume as 0 shares) and their (stock, day, minute, null bits) are kept on the host;
+    ``finish()`` turns them into the panel's :class:`mff.engine.NullSet` (the stock-days'
+    presence words and null bits) and clears those stock-days from the mask, so the fast
+    kernels see them ABSENT and ``mff_stage1_nulls`` computes them with polars' null
+    rules."""
+
+    ERR_CHUNK = 64  # error-counter rows per device allocation (one row per push)
 
     def __init__(self, codes: Sequence[str], day_numbers: Sequence[int], device,
                  slots: int = 2, tables: int = 1):
@@ -209,15 +239,22 @@ class PanelIngest:
         self.S, self.D = S, D
         self.bars = torch.empty((5, D, S, 240), dtype=torch.float32, device=self.dev)
         self.mask = torch.zeros((D, S, 8), dtype=torch.int32, device=self.dev)
-        # contract-violation counters per pushed table ([tables][5]; push k uses row k, a
-        # push beyond `tables` shares the last row), so a caller can drop a bad day file
-        self.err = torch.zeros((max(1, tables), 5), dtype=torch.int32, device=self.dev)
-        self.table_days: List[np.ndarray] = []  # day indices each push touched
+        # contract-violation counters, one [5] row per push (chunks of ERR_CHUNK rows, so
+        # a caller can drop exactly the bad push's cells whatever the number of pushes)
+        self._err: List[torch.Tensor] = []
+        self.table_cells: List[Optional[np.ndarray]] = []  # stock-day cells each push wrote
+        self._null_rows: List[tuple] = []  # (sd int64, minute int64, bits uint8) per push
         self.stream = torch.cuda.Stream(self.dev)
         self.stream.wait_stream(torch.cuda.current_stream(self.dev))  # zero fills first
         self.slots = [None] * slots  # (pinned, device, event)
         self.k = 0
         self.rows = 0
+
+    def _err_row(self, k: int) -> torch.Tensor:
+        while len(self._err) * self.ERR_CHUNK <= k:
+            with torch.cuda.stream(self.stream):
+                self._err.append(torch.zeros((self.ERR_CHUNK, 5), dtype=torch.int32, device=self.dev))
+        return self._err[k // self.ERR_CHUNK][k % self.ERR_CHUNK]
 
     def _slot(self, nbytes: int):
         i = self.k % len(self.slots)
@@ -238,13 +275,29 @@ class PanelIngest:
     def push(self, df) -> None:
         self.push_encoded(encode(_table(df), self.codes, self.day_numbers))
 
+    def _cells(self, stock, day) -> np.ndarray:
+        """The in-range (day * S + stock) cells a push writes, ascending."""
+        ok = (stock >= 0) & (day >= 0)
+        if stock.size and ok.all() and day[0] == day[-1] and (day == day[0]).all():
+            seen = np.zeros(self.S, dtype=bool)  # a day file: one day, mark its stocks
+            seen[stock] = True
+            return int(day[0]) * self.S + np.flatnonzero(seen).astype(np.int64)
+        return np.unique(day[ok].astype(np.int64) * self.S + stock[ok])
+
     def push_encoded(self, enc) -> None:
         """Stage and launch one table already encoded by :func:`encode`."""
-        stock, day, time, px, vol, kind = enc
+        stock, day, time, px, vol, kind, nbits = enc
         n = int(stock.size)
-        k = min(len(self.table_days), self.err.shape[0] - 1)
-        lo, hi = (int(day.min()), int(day.max())) if n else (0, -1)
-        self.table_days.append(np.arange(lo, hi + 1) if lo == hi or n == 0 else np.unique(day))
+        k = len(self.table_cells)
+        err = self._err_row(k)
+        self.table_cells.append(self._cells(stock, day) if n else np.zeros(0, np.int64))
+        if nbits is not None:
+            from .frames import time_to_minute
+            r = np.flatnonzero((nbits != 0) & (stock >= 0) & (day >= 0))
+            if r.size:
+                m = time_to_minute(time[r])
+                on = m >= 0  # off-grid rows are counted as errors by the kernel
+                self._null_rows.append(((day[r].astype(np.int64) * self.S + stock[r])[on], m[on], nbits[r][on]))
         if n == 0:
             return
         cols = [stock, day, time] + px + [vol]
@@ -263,41 +316,72 @@ class PanelIngest:
             b = self.bars
             _lib.check(self.lib.mff_ingest_rows(
                 p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], kind, n, self.S, self.D,
-                b.data_ptr(), self.mask.data_ptr(), self.err[k].data_ptr(),
+                b.data_ptr(), self.mask.data_ptr(), err.data_ptr(),
                 self.stream.cuda_stream), "mff_ingest_rows")
         self.rows += n
 
     def skip_table(self, k: int) -> None:
         """Record a table that could not be pushed (its encode raised): nothing staged."""
-        self.table_days.append(np.zeros(0, dtype=np.int64))
+        self.table_cells.append(np.zeros(0, dtype=np.int64))
+
+    def _null_set(self, dropped_cells: np.ndarray):
+        """Host null rows -> (sd, bits uint32 [K][5][8]) of the null-holding stock-days,
+        without the cells of dropped pushes."""
+        if not self._null_rows:
+            return None
+        sd = np.concatenate([x[0] for x in self._null_rows])
+        m = np.concatenate([x[1] for x in self._null_rows])
+        nb = np.concatenate([x[2] for x in self._null_rows])
+        if dropped_cells.size:
+            keep = ~np.isin(sd, dropped_cells)
+            sd, m, nb = sd[keep], m[keep], nb[keep]
+        if sd.size == 0:
+            return None
+        usd, inv = np.unique(sd, return_inverse=True)
+        bits = np.zeros((usd.size, 5, 8), np.uint32)
+        for i in range(5):
+            r = np.flatnonzero((nb >> i) & 1)
+            np.bitwise_or.at(bits[:, i, :], (inv[r], m[r] // 32), (np.uint32(1) << (m[r] % 32).astype(np.uint32)))
+        return usd, bits
 
     def finish(self, skip_bad: bool = False):
-        """Check the per-table error counters and return the DevicePanel.
+        """Check the per-push error counters and return the DevicePanel.
 
-        A table breaking the input contract raises ValueError (naming the table's index)
-        unless ``skip_bad``: then every day the table touched is dropped from the panel
-        (its presence bits cleared: every stock-day ABSENT, no rows, as when the
-        reference's per-file call fails, MinuteFrequentFactorCICC.py:18-25, 95) and the
-        reasons are returned in ``panel.dropped`` {table index: message}."""
-        from .engine import DevicePanel
+        A push breaking the input contract raises ValueError (naming the push's index when
+        there were several) unless ``skip_bad``: then the stock-day cells that push wrote
+        are dropped from the panel (their presence bits cleared: ABSENT, no rows, as when
+        the reference's per-file call fails, MinuteFrequentFactorCICC.py:18-25, 95) and the
+        reasons are returned in ``panel.dropped`` {push index: message}."""
+        from .engine import DevicePanel, NullSet
 
         torch.cuda.current_stream(self.dev).wait_stream(self.stream)
-        err = self.err.cpu().numpy()  # synchronises the caller's stream
+        npush = len(self.table_cells)
+        err = (torch.cat(self._err).cpu().numpy()[:npush] if self._err
+               else np.zeros((0, 5), np.int32))  # synchronises the caller's stream
         dropped = {}
         for k in range(err.shape[0]):
             bad = [f"{ERRORS[i]} ({int(err[k, i])} rows)" for i in range(5) if err[k, i]]
             if bad:
                 dropped[k] = "; ".join(bad)
         if dropped and not skip_bad:
-            if err.shape[0] == 1:
+            if npush == 1:
                 raise ValueError(dropped[0])
             raise ValueError("; ".join(f"table {k}: {m}" for k, m in sorted(dropped.items())))
-        for k in dropped:
-            days = self.table_days[k] if k < len(self.table_days) else np.zeros(0, np.int64)
-            if days.size:
-                self.mask[torch.as_tensor(days, device=self.dev)] = 0
+        cells = [self.table_cells[k] for k in dropped if self.table_cells[k] is not None]
+        dcells = np.unique(np.concatenate(cells)) if cells else np.zeros(0, np.int64)
+        flat = self.mask.view(-1, 8)
+        if dcells.size:
+            flat[torch.as_tensor(dcells, device=self.dev)] = 0
+        nulls = None
+        ns = self._null_set(dcells)
+        if ns is not None:
+            usd, bits = ns
+            idx = torch.as_tensor(usd, device=self.dev)
+            nmask = flat[idx].cpu().numpy().view(np.uint32)  # the stock-days' real presence
+            flat[idx] = 0  # ... which only mff_stage1_nulls sees
+            nulls = NullSet.from_host(usd.astype(np.int32), nmask, bits, self.dev)
         dates = [_EPOCH + _dt.timedelta(days=x) for x in self.day_numbers]
-        dp = DevicePanel(self.bars, self.mask, self.codes, dates)
+        dp = DevicePanel(self.bars, self.mask, self.codes, dates, nulls=nulls)
         dp.dropped = dropped
         return dp
 

@@ -150,6 +150,81 @@ def unpack_mask(words: np.ndarray) -> np.ndarray:
     return bits[:, :MINUTES].reshape(*sh, MINUTES)
 
 
+FIELDS = ("open", "high", "low", "close", "volume")
+
+
+def null_set(panel: Dict):
+    """The stock-days of a host panel that hold a polars null (``panel["null"]``: optional
+    uint8 [D][S][240], bit i = FIELDS[i] null on a present bar) in the layout of
+    ``mff_stage1_nulls`` (include/mff.h): (sd int32 [K] = d*S + s ascending, presence
+    words uint32 [K][8], null bits uint32 [K][5][8])."""
+    pres = panel["present"]
+    D, S = pres.shape[:2]
+    nb = panel.get("null")
+    if nb is None:
+        return (np.zeros(0, np.int32), np.zeros((0, 8), np.uint32), np.zeros((0, 5, 8), np.uint32))
+    nb = np.where(pres, nb, 0).astype(np.uint8)
+    d, s = np.nonzero((nb != 0).any(axis=2))
+    sd = (d.astype(np.int64) * S + s).astype(np.int32)
+    mask = pack_mask(pres[d, s])
+    bits = np.stack([pack_mask(((nb[d, s] >> i) & 1).astype(bool)) for i in range(5)], axis=1)
+    return sd, mask.reshape(-1, 8), bits.reshape(-1, 5, 8)
+
+
+def add_nulls(panel: Dict, seed: int = 0, rate: float = 0.002, patterns: bool = True) -> Dict:
+    """Put polars nulls into a host panel (in place; returns it): ``rate`` of the present
+    bars get one random field null, and (``patterns``) one stock-day per pattern below
+    gets a structured null: the first bar's volume / open, the last bar's close
+    (close.last() null), a whole day of null volume / close / every field, a mid-day run
+    of null highs and lows (OLS windows), every other volume.  Values under a null are
+    NaN (never read)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    pres = panel["present"]
+    D, S, M = pres.shape
+    nb = np.zeros((D, S, M), np.uint8) if panel.get("null") is None else panel["null"].copy()
+    hit = pres & (rng.random((D, S, M)) < rate)
+    nb[hit] |= (1 << rng.integers(0, 5, size=int(hit.sum()))).astype(np.uint8)
+    if patterns:
+        days = [(d, s) for d in range(D) for s in range(S) if pres[d, s].any()]
+        pick = rng.permutation(len(days))
+        pats = ["first_volume", "first_open", "last_close", "day_volume", "day_close", "day_all",
+                "midday_hl", "alternate_volume", "first_close", "head_volume"]
+        for j, name in enumerate(pats):
+            if j >= len(days):
+                break
+            d, s = days[pick[j]]
+            bars = np.flatnonzero(pres[d, s])
+            f, l = bars[0], bars[-1]
+            if name == "first_volume":
+                nb[d, s, f] |= 16
+            elif name == "first_open":
+                nb[d, s, f] |= 1
+            elif name == "last_close":
+                nb[d, s, l] |= 8
+            elif name == "day_volume":
+                nb[d, s, bars] |= 16
+            elif name == "day_close":
+                nb[d, s, bars] |= 8
+            elif name == "day_all":
+                nb[d, s, bars] |= 31
+            elif name == "midday_hl":
+                nb[d, s, bars[len(bars) // 3: len(bars) // 3 + 20]] |= 2 | 4
+            elif name == "alternate_volume":
+                nb[d, s, bars[::2]] |= 16
+            elif name == "first_close":
+                nb[d, s, f] |= 8
+            elif name == "head_volume":
+                nb[d, s, bars[bars <= 20]] |= 16
+    nb[~pres] = 0
+    panel["null"] = nb
+    for i, k in enumerate(FIELDS):
+        arr = panel[k]
+        if arr.dtype.kind != "f":
+            panel[k] = arr = arr.astype(np.float64)
+        arr[(nb >> i) & 1 == 1] = np.nan
+    return panel
+
+
 def volume_u32(volume: np.ndarray) -> np.ndarray:
     """Host volume (float, NaN on absent bars) -> the device's u32 share counts (absent 0)."""
     v = np.asarray(volume, dtype=np.float64)
@@ -166,7 +241,8 @@ def stack_fields(panel: Dict) -> np.ndarray:
 def subpanel(panel: Dict, stocks=None, days=None) -> Dict:
     st = slice(None) if stocks is None else stocks
     dy = slice(None) if days is None else days
-    out = {k: panel[k][dy][:, st] for k in ("open", "high", "low", "close", "volume", "present")}
+    keys = ("open", "high", "low", "close", "volume", "present") + (("null",) if panel.get("null") is not None else ())
+    out = {k: panel[k][dy][:, st] for k in keys}
     out["codes"] = list(np.asarray(panel["codes"])[st])
     out["dates"] = list(np.asarray(panel["dates"], dtype=object)[dy])
     return out

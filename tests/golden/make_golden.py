@@ -7,6 +7,10 @@ Fixtures (numpy .npz, no pickles):
                      for all 58 factors + stage 2/3 expectations on four factors.
   panel_edge.npz   — hand-built stock-days, one edge case per stock (see EDGE_CASES),
                      + stage-1 expectations.
+  panel_null.npz   — seeded ragged panel (S=40, D=3) with polars nulls (synth.add_nulls:
+                     random single-field nulls + the structured patterns) + stage-1
+                     expectations under the null rules N1-N11 / C8; ``null`` uint8
+                     [D][S][240], bit i = open, high, low, close, volume.
 Inputs are float32 bar planes [D][S][240] and a bool presence mask; expectations are
 val float64 [F][D][S] and state uint8 [F][D][S] (0 ABSENT, 1 NULL, 2 VALUE).
 """
@@ -112,6 +116,8 @@ def edge_panel():
 
 def _save(path, panel, val, state, extra=None):
     arrs = {k: panel[k] for k in ("open", "high", "low", "close", "volume", "present")}
+    if panel.get("null") is not None:
+        arrs["null"] = panel["null"]
     arrs["codes"] = np.array(panel["codes"])
     arrs["names"] = np.array(O.ORACLE_NAMES)
     arrs["val"] = val
@@ -125,6 +131,8 @@ def _save(path, panel, val, state, extra=None):
 def load(name):
     z = np.load(os.path.join(HERE, name), allow_pickle=False)
     panel = {k: z[k] for k in ("open", "high", "low", "close", "volume", "present")}
+    if "null" in z.files:
+        panel["null"] = z["null"]
     panel["codes"] = list(z["codes"])
     panel["dates"] = synth.trading_dates(panel["present"].shape[0])
     return panel, z
@@ -151,6 +159,20 @@ def main():
     val, state = O.oracle_stage1(ep)
     _save(os.path.join(HERE, "panel_edge.npz"), ep, val, state)
 
+    npn = null_panel()
+    val, state = O.oracle_stage1(npn)
+    _save(os.path.join(HERE, "panel_null.npz"), npn, val, state)
+
+
+def null_panel():
+    panel = synth.make_panel(40, 3, config=6, ragged=True)
+    return synth.add_nulls(panel, seed=11, rate=0.01)
+
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["null"]:  # only the null fixture (the others stay byte-identical)
+        npn = null_panel()
+        val, state = O.oracle_stage1(npn)
+        _save(os.path.join(HERE, "panel_null.npz"), npn, val, state)
+    else:
+        main()

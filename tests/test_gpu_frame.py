@@ -5,8 +5,8 @@
 * mff_stage1_frame with a NULL open plane (only liq_amihud_1min / corr_prvr requested);
 * the driver's per-file error semantics (MinuteFrequentFactorCICC.py:18-25, 95): a day
   file that breaks the input contract in the middle of a GPU batch is reported with the
-  reference's message and dropped, the other days exact; strict=True raises naming it;
-* a null volume is 0 shares (CM:743-744).
+  reference's message and dropped, the other days exact; strict=True raises naming it.
+Null rows (polars null semantics) are tested in test_gpu_nulls.py.
 """
 import os
 
@@ -73,6 +73,7 @@ def test_stage1_frame_null_open(dev):
     lib = _lib.load()
     b = dp.bars
     _lib.check(lib.mff_stage1_frame(None, _lib.ptr(b[3]), _lib.ptr(b[4]), _lib.ptr(dp.mask), dp.S, dp.D,
+                                    None, None, None, 0,
                                     _lib.int_array(ids), len(ids), _lib.ptr(val), _lib.ptr(state),
                                     torch.cuda.current_stream(dev).cuda_stream), "mff_stage1_frame")
     torch.cuda.synchronize()
@@ -84,7 +85,7 @@ def test_stage1_frame_null_open(dev):
     # a trade_bottom row without the open plane is refused, not dereferenced
     ids2 = [catalog.ID["trade_bottom20retRatio"]]
     rc = lib.mff_stage1_frame(None, _lib.ptr(b[3]), _lib.ptr(b[4]), _lib.ptr(dp.mask), dp.S, dp.D,
-                              _lib.int_array(ids2), 1, _lib.ptr(val), _lib.ptr(state), None)
+                              None, None, None, 0, _lib.int_array(ids2), 1, _lib.ptr(val), _lib.ptr(state), None)
     assert rc != 0 and b"open" in lib.mff_last_error()
 
 
@@ -105,9 +106,8 @@ def test_bad_day_files_dropped_mid_batch(dev, tmp_path, capsys):
     write_day_files(panel, folder)
     dates = panel["dates"]
 
-    def null_close(df):
-        df["close"] = df["close"].astype("object")
-        df.loc[5, "close"] = None
+    def inf_close(df):
+        df.loc[5, "close"] = float("inf")  # a null close is a polars null, not an error
         return df
 
     def off_grid(df):
@@ -118,7 +118,7 @@ def test_bad_day_files_dropped_mid_batch(dev, tmp_path, capsys):
         df.loc[7, "volume"] = -100.0
         return df
 
-    bad_files = {1: _rewrite(folder, dates[1], null_close), 3: _rewrite(folder, dates[3], off_grid),
+    bad_files = {1: _rewrite(folder, dates[1], inf_close), 3: _rewrite(folder, dates[3], off_grid),
                  4: _rewrite(folder, dates[4], negative_volume)}
     good = [d for d in range(6) if d not in bad_files]
     names = ["doc_pdf60", "vol_return1min"]
@@ -138,23 +138,3 @@ def test_bad_day_files_dropped_mid_batch(dev, tmp_path, capsys):
         MinFreqFactor("vol_return1min").cal_exposure_by_min_data(
             CM.cal_vol_return1min, path=str(tmp_path / "exp"), folder_path=folder, strict=True)
     assert catalog.ID["vol_return1min"] >= 0
-
-
-def test_null_volume_is_zero_shares(dev):
-    import mff_oracle as O
-    import MinuteFrequentFactorCalculateMethodsCICC as CM
-    from mff import catalog, synth
-    panel = synth.make_panel(12, 1, config=44)
-    df = long_frame(panel)
-    rows = [10, 300, 301, 1000]
-    df["volume"] = df["volume"].astype("object")
-    df.loc[rows, "volume"] = None
-    res = CM.compute_long(pa.Table.from_pandas(df, preserve_index=False))
-    s_idx, m_idx = np.nonzero(panel["present"][0])
-    panel["volume"][0, s_idx[rows], m_idx[rows]] = 0.0
-    ov, os_ = O.oracle_stage1(panel)
-    bad = []
-    for i, nm in enumerate(catalog.NAMES):
-        v, s = _dense(res[nm], nm, panel)
-        bad += compare(v, s, ov[i], os_[i], nm)
-    assert not bad, "\n".join(bad)

@@ -27,7 +27,8 @@ def test_encode_indices_match_host_restatement():
     ref = frames.to_dense(t)
     assert codes == ref["codes"]
     assert [dt.date(1970, 1, 1) + dt.timedelta(days=x) for x in days] == ref["dates"]
-    stock, day, time, px, vol, kind = ingest.encode(t, codes, days)
+    stock, day, time, px, vol, kind, nbits = ingest.encode(t, codes, days)
+    assert nbits is None  # no null in the frame
     assert stock.dtype == np.int32 and day.dtype == np.int32 and time.dtype == np.int64
     assert (np.asarray(codes)[stock] == df["code"].to_numpy()).all()
     assert [ref["dates"][i] for i in day] == list(df["date"])
@@ -51,7 +52,7 @@ def test_encode_column_types():
             t = ingest._table(pd.DataFrame({**base, "date": date, "volume": vol}))
             codes, days = ingest.universes([t])
             assert codes == ["A", "B"] and days == [(dt.date(2024, 1, 2) - dt.date(1970, 1, 1)).days]
-            s, d, tm, px, v, k = ingest.encode(t, codes, days)
+            s, d, tm, px, v, k, nb = ingest.encode(t, codes, days)
             assert list(s) == [1, 0] and list(d) == [0, 0] and k == kind and v.dtype == vol.dtype
     with pytest.raises(ValueError, match="missing column"):
         ingest.encode(pa.table({"code": ["A"]}), ["A"], [0])
@@ -137,7 +138,7 @@ def test_ingest_errors(dev):
         (df.assign(volume=2.0 ** 40), "volume"),
         (df.assign(volume=-1.0), "volume"),
         (df.assign(close=0.0), "prices"),
-        (df.assign(high=float("nan")), "prices"),
+        (df.assign(high=float("-inf")), "prices"),
         (df.assign(low=float("inf")), "prices"),
     ]
     for bad, msg in cases:
