@@ -333,18 +333,66 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
                    "mff_pdf_rank_local")
 
 
+NBAR = 240
+PDF_MAX_QUERIES = 1 << 24  # mff_pdf_count_frame: queries of one sorted list (PDF_MAXM)
+
+
+def _pdf_ranks_frame_chunked(lib, panel, pdfq, levels, rows, val, state, chunk_days: int) -> None:
+    """pdf_ranks_frame for a frame whose 5*S*D queries exceed one sorted list: the rank of
+    a query is n_less + (n_eq + 1) / 2 over ALL keys of the frame, whatever list it sits
+    in, so the queries go in day chunks -- each chunk's queries sorted as one list and
+    counted against the level keys of every day of the frame -- and each chunk's ranks are
+    written row by row (its [5][Dc][S] queries copied to one contiguous list)."""
+    D, S = panel.D, panel.S
+    dev = panel.device
+    st = _stream(dev)
+    plane = D * S
+    for d0 in range(0, D, chunk_days):
+        d1 = min(D, d0 + chunk_days)
+        DS = (d1 - d0) * S
+        M = 5 * DS
+        qc = pdfq[:, d0:d1].contiguous()  # [5][Dc][S] = the one-day view [5][1][Dc*S]
+        ws = torch.empty(lib.mff_pdf_workspace_bytes(DS, 1, 1), dtype=torch.uint8, device=dev)
+        q_sorted = torch.empty((1, M), dtype=torch.int64, device=dev)
+        _lib.check(lib.mff_pdf_sort(_lib.ptr(qc), 1, DS, 1, 0, 1, _lib.ptr(q_sorted), _lib.ptr(ws), st),
+                   "mff_pdf_sort(frame chunk)")
+        counts = torch.zeros((1, M), dtype=torch.int32, device=dev)
+        _lib.check(lib.mff_pdf_count_frame(_lib.ptr(levels), S, D, _lib.ptr(q_sorted), M, _lib.ptr(counts), st),
+                   "mff_pdf_count_frame(chunk)")
+        for t, r in enumerate(rows):  # one output row at a time: its chunk is contiguous
+            if r < 0:
+                continue
+            one = [-1] * 5
+            one[t] = 0
+            off = r * plane + d0 * S
+            _lib.check(lib.mff_pdf_finalize(_lib.ptr(qc), _lib.ptr(q_sorted), _lib.ptr(counts), DS, 1, 0, 1, M,
+                                            _lib.int_array(one), val.data_ptr() + 8 * off,
+                                            state.data_ptr() + off, st), "mff_pdf_finalize(frame chunk)")
+
+
 def pdf_ranks_frame(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows: List[int], val,
-                    state):
+                    state, chunk_days: Optional[int] = None):
     """doc_pdf ranks of a multi-date frame taken as ONE reference frame: `.rank()`
     (CM:1015-1017) is outside any `.over`, so a frame holding D dates ranks every row of
     every date.  The D days' 5*S queries are sorted as one list ([5][D][S] viewed as one
     day of D*S stocks), every day's level keys are counted against it (the words
     2 n_less + n_eq add up over days, mff_pdf_count_frame) and the ranks are written
-    through the same one-day view of the output rows."""
+    through the same one-day view of the output rows.  Beyond PDF_MAX_QUERIES queries
+    (about 670 dates of 5,000 codes) the queries go in day chunks of ``chunk_days``
+    (:func:`_pdf_ranks_frame_chunked`)."""
     lib = _lib.load()
     D, S = panel.D, panel.S
     dev = panel.device
     st = _stream(dev)
+    if NBAR * S * D >= 2 ** 31:  # mff_pdf_count_frame: the words 2 n_less + n_eq stay in u32
+        raise ValueError(f"a frame of {D} dates x {S} codes is too large for one frame-wide doc_pdf "
+                         f"rank (240 * codes * dates must stay below 2^31); pass the day files as a "
+                         f"list (per-day semantics) or split the frame by date")
+    if chunk_days is None:
+        chunk_days = max(1, PDF_MAX_QUERIES // (5 * S))
+    if D > chunk_days:
+        _pdf_ranks_frame_chunked(lib, panel, pdfq, levels, rows, val, state, chunk_days)
+        return
     DS = D * S
     M = 5 * DS
     ws = torch.empty(lib.mff_pdf_workspace_bytes(DS, 1, 1), dtype=torch.uint8, device=dev)

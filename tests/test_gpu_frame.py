@@ -138,3 +138,23 @@ def test_bad_day_files_dropped_mid_batch(dev, tmp_path, capsys):
         MinFreqFactor("vol_return1min").cal_exposure_by_min_data(
             CM.cal_vol_return1min, path=str(tmp_path / "exp"), folder_path=folder, strict=True)
     assert catalog.ID["vol_return1min"] >= 0
+
+
+@pytest.mark.parametrize("chunk", [1, 2])
+def test_doc_pdf_frame_rank_in_day_chunks(dev, monkeypatch, chunk):
+    """A frame whose queries exceed one sorted list (PDF_MAX_QUERIES; ~670 dates of 5,000
+    codes) is ranked in day chunks, each counted against every date's keys: the same exact
+    frame-wide ranks (forced here by a small list cap), nulls included."""
+    import mff_oracle as O
+    import MinuteFrequentFactorCalculateMethodsCICC as CM
+    from mff import engine, synth
+    panel = synth.add_nulls(synth.make_panel(60, 5, config=45, ragged=True), seed=5, rate=0.005)
+    monkeypatch.setattr(engine, "PDF_MAX_QUERIES", 5 * 60 * chunk)
+    names = O.FRAME_RANK_NAMES
+    fx = O.oracle_frame_doc_pdf(panel)
+    res = CM.compute_long(long_frame(panel), names)
+    bad = []
+    for nm in names:
+        v, s = _dense(res[nm], nm, panel)
+        bad += compare(v, s, *fx[nm], nm, rtol=0, atol=0)
+    assert not bad, "\n".join(bad)

@@ -1,4 +1,8 @@
-"""GPU parity at the benchmark sizes (BASELINE configs c4 and c5), by sampling.
+"""GPU parity at the benchmark sizes (BASELINE configs c2, c4 and c5), by sampling.
+
+c2: CSI300-sized, 300 stocks x 240 min x 250 days from the host generator: one stage-1
+    pass of all 58 factors; 500 sampled stock-days (20 days x 25 stocks) against the
+    oracle for every non-doc_pdf factor, doc_pdf on two full days (all 300 codes).
 
 c4: the bench panel itself, 5,000 stocks x 240 min x 2,500 days resident in HBM (plane
     index of the last stock-day ~3.0e9 > 2^31): one stage-1 pass of all 58 factors;
@@ -74,6 +78,24 @@ def _pdf_day(bars, mask, val, state, d):
     for r, nm in enumerate(names):
         bad += compare(gv[r], gs[r], ov[r], os_[r], f"{nm}/day{d}", rtol=0.0, atol=0.0)
     return bad
+
+
+def test_c2_csi300_panel_sampled(dev):
+    """BASELINE.json configs[1]: all 58 factors on 300 x 250 synthetic bars."""
+    from mff import engine, synth
+    S, D = 300, 250
+    panel = synth.make_panel(S, D, config=2)
+    dp = engine.DevicePanel.from_host(panel, dev)
+    val, state, _ = engine.compute_factors(dp)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(22)
+    days = sorted({0, D - 1} | set(rng.choice(np.arange(1, D - 1), 18, replace=False).tolist()))
+    stocks = sorted({0, S - 1} | set(rng.choice(np.arange(1, S - 1), 23, replace=False).tolist()))
+    assert len(days) * len(stocks) == 500
+    bad = _sampled_stage1(dp.bars, dp.mask, val, state, days, stocks)
+    for d in (0, D - 1):
+        bad += _pdf_day(dp.bars, dp.mask, val, state, d)
+    assert not bad, "\n".join(bad[:30])
 
 
 def test_c4_full_panel_sampled(dev):
