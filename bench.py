@@ -319,7 +319,7 @@ def main():
     s0, s1 = dist.shard_bounds(S, world, rank)
     S_loc = s1 - s0
     bars, mask = synth.make_panel_device(S_loc, D, dev, config=4, seed_offset=rank)
-    panel = engine.DevicePanel(bars, mask)
+    panel = engine.DevicePanel(bars, mask, stocks_total=S)
     torch.cuda.synchronize()
 
     def step(events=None):
@@ -347,6 +347,22 @@ def main():
     elapsed = float(el.item())
 
     k_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, len(evs))
+    exchange = None
+    if comm is not None and hasattr(comm, "stats"):
+        # one more (untimed) pass with every collective accounted: bytes this rank sends
+        # and device ms between events around each call (doc_pdf exchange)
+        comm.stats = dist.CommStats()
+        out = step()
+        del out
+        torch.cuda.synchronize()
+        summ = comm.stats.summary()
+        comm.stats = None
+        tot = torch.tensor([sum(v["sent_bytes"] for v in summ.values()), sum(v["ms"] for v in summ.values())],
+                           dtype=torch.float64, device=dev)
+        comm.all_reduce_max(tot)
+        exchange = {"per_collective_rank0": summ,
+                    "pdf_exchange_sent_bytes_per_rank_max": int(tot[0].item()),
+                    "collective_ms_per_rank_max": round(float(tot[1].item()), 3)}
     ids = list(range(catalog.N_FACTORS))
     bytes_launch = catalog.algorithmic_bytes_per_stock_day(ids) * S_loc * D
     achieved = bytes_launch / (k_ms * 1e-3) / 1e9
@@ -387,10 +403,10 @@ def main():
         ms = timed(lambda: engine.rolling(val, state, 20, "z"))
         extras["stage2_z20_all58_ms"] = round(ms, 3)
         extras["stage2_z20_GBps"] = round(xs_bytes / (ms * 1e-3) / 1e9, 1)
-        ms = timed(lambda: engine.cross_section(val, state, "z", comm=comm))
+        ms = timed(lambda: engine.cross_section(val, state, "z", comm=comm, stocks_total=S))
         extras["stage3_z_all58_ms"] = round(ms, 3)
         extras["stage3_z_GBps"] = round(xs_bytes / (ms * 1e-3) / 1e9, 1)
-        ms = timed(lambda: engine.cross_section(val, state, "rank", comm=comm), reps=3)
+        ms = timed(lambda: engine.cross_section(val, state, "rank", comm=comm, stocks_total=S), reps=3)
         extras["stage3_rank_all58_ms"] = round(ms, 3)
         extras["stage3_rank_GBps"] = round(xs_bytes / (ms * 1e-3) / 1e9, 1)
         del val, state
@@ -461,6 +477,8 @@ def main():
             "cpu_baseline": cpu,
             "extras": extras,
         }
+        if exchange is not None:
+            res["exchange"] = exchange
         print(json.dumps(res), flush=True)
 
 

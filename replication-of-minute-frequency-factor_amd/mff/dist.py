@@ -34,8 +34,37 @@ def shard_bounds(S: int, world: int, rank: int) -> Tuple[int, int]:
     return s0, s0 + base + (1 if rank < rem else 0)
 
 
+class CommStats:
+    """Per-collective accounting of one rank (bench.py's N > 1 line): calls, bytes this
+    rank sends, and the device time between HIP events recorded around each call on the
+    stream it is issued on (read with :meth:`summary` after a synchronize)."""
+
+    def __init__(self):
+        self.calls = {}
+        self.events = []  # (name, start, end)
+
+    def begin(self, name: str, sent_bytes: int):
+        c = self.calls.setdefault(name, [0, 0])
+        c[0] += 1
+        c[1] += int(sent_bytes)
+        if not torch.cuda.is_available():
+            return None
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
+        self.events.append((name, ev[0], ev[1]))
+        return ev[1]
+
+    def summary(self) -> dict:
+        ms = {}
+        for name, a, b in self.events:
+            ms[name] = ms.get(name, 0.0) + a.elapsed_time(b)
+        return {n: {"calls": c[0], "sent_bytes": c[1], "ms": round(ms.get(n, 0.0), 3)}
+                for n, c in self.calls.items()}
+
+
 class Comm:
-    """torch.distributed process group; one rank per GPU."""
+    """torch.distributed process group; one rank per GPU.  ``stats``: a CommStats to
+    account every collective in (None = off)."""
 
     def __init__(self, group=None):
         import torch.distributed as dist
@@ -45,10 +74,28 @@ class Comm:
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
+        self.stats: Optional[CommStats] = None
+
+    def _begin(self, name: str, t: torch.Tensor, sent_fraction: float):
+        if self.stats is None:
+            return None
+        return self.stats.begin(name, t.numel() * t.element_size() * sent_fraction)
+
+    @staticmethod
+    def _end(ev) -> None:
+        if ev is not None:
+            ev.record()
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[*shape] on every rank -> [world, *shape] (rank order)."""
         t = t.contiguous()
+        ev = self._begin("all_gather", t, self.world_size - 1)  # to every peer
+        try:
+            return self._all_gather(t)
+        finally:
+            self._end(ev)
+
+    def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         if self.backend == "gloo":  # host collectives (CPU tests; the 1-GPU rehearsal)
             h = t.cpu()
             parts = [torch.empty_like(h) for _ in range(self.world_size)]
@@ -62,6 +109,13 @@ class Comm:
         """[world, *shape]: slice r goes to rank r; returns [world, *shape] with slice r
         received from rank r."""
         t = t.contiguous()
+        ev = self._begin("all_to_all", t, (self.world_size - 1) / self.world_size)
+        try:
+            return self._all_to_all(t)
+        finally:
+            self._end(ev)
+
+    def _all_to_all(self, t: torch.Tensor) -> torch.Tensor:
         if self.backend == "gloo":
             h = t.cpu()
             out = torch.empty_like(h)
@@ -76,6 +130,13 @@ class Comm:
         (RCCL reduce-scatter: each rank sends (world-1)/world of the input once, half
         the bytes of a ring all-reduce of the same array)."""
         t = t.contiguous()
+        ev = self._begin("reduce_scatter", t, (self.world_size - 1) / self.world_size)
+        try:
+            return self._reduce_scatter(t)
+        finally:
+            self._end(ev)
+
+    def _reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
         if self.backend == "gloo":  # host collectives: all-reduce, keep the own slice
             h = t.cpu()
             self._dist.all_reduce(h, op=self._dist.ReduceOp.SUM, group=self.group)

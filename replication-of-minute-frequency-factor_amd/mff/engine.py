@@ -89,6 +89,10 @@ class DevicePanel:
     # hold no bars)
     dropped: dict = field(default_factory=dict)
     nulls: Optional[NullSet] = None
+    # stock-sharded panels: the number of stocks over all ranks (shards by
+    # dist.shard_bounds), so the exchange's padded shard width is known without a
+    # collective; None = agree on it with one all-reduce
+    stocks_total: Optional[int] = None
 
     @property
     def D(self) -> int:
@@ -211,7 +215,7 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             if EXACT_SIDE:  # the exact list kernel ahead of the doc_pdf phases, off the launch stream
                 _lib.check(lib.mff_stage1_part(*(args[:-1] + [side.cuda_stream]), 32), "mff_stage1_part(32)")
             nulls_phase(1, side)
-            sorted_ev = torch.cuda.Event() if SORT_FIRST and comm is None else None
+            sorted_ev = torch.cuda.Event() if SORT_FIRST else None
             with torch.cuda.stream(side):
                 pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch,
                           after_sort=(lambda: sorted_ev.record(side)) if sorted_ev is not None else None)
@@ -298,12 +302,13 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
               comm=None,
               day_batch: Optional[int] = None, workspace_budget: int = 2 << 30, after_sort=None):
     """doc_pdf frame-wide ranks (CM:1015-1017) for all days, in day batches.  ``after_sort``:
-    optional callable, invoked once the first day batch's sort is enqueued (single rank)."""
+    optional callable, invoked once the first day batch's sort is enqueued (sharded: the
+    first window's sort of this rank's days)."""
     lib = _lib.load()
     D, S = panel.D, panel.S
     dev = panel.device
     R = 1 if comm is None else comm.world_size
-    S_all = S if comm is None else _agreed_max(comm, S, dev)
+    S_all = S if comm is None else shard_width(comm, S, panel.stocks_total, dev)
     M = R * 5 * S_all
     st = _stream(dev)
     if comm is not None:
@@ -313,7 +318,7 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
             per_day = 2 * M * 8 + 2 * M * 4 + lib.mff_pdf_workspace_bytes(S_all, R, 1)
             day_batch = max(1, workspace_budget // max(per_day, 1))
         _pdf_ranks_sharded(comm, pdfq, S_all, PdfKernels(lib, levels, S, D, rows, val, state, st),
-                           day_batch=day_batch)
+                           day_batch=day_batch, after_sort=after_sort)
         return
     if day_batch is None:
         per_day = lib.mff_pdf_workspace_bytes(S, R, 1) + M * 8 + M * 8
@@ -519,7 +524,7 @@ class PdfKernels:
                                                  _lib.ptr(self.state), self.st), "mff_pdf_finalize_own")
 
 
-def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern, day_batch: Optional[int] = None):
+def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern, day_batch: Optional[int] = None, after_sort=None):
     """doc_pdf across stock shards.  The days go in windows of at most
     ``day_batch`` x R days (the exchange buffers below are O(window x M) per rank; None:
     one window); inside a window, day d is owned by the rank whose contiguous day block
@@ -559,6 +564,8 @@ def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern, day_batch: Optional[int] = 
         mine = torch.zeros((nd_max, M), dtype=torch.int64, device=dev)
         if nd > 0:
             mine[:nd] = kern.sort(recv, R, S_all, nd)
+        if after_sort is not None and w0 == 0:
+            after_sort()
         gathered = comm.all_gather(mine)  # [R][nd_max][M]
         q_sorted = torch.cat([gathered[r, :e - s] for r, (s, e) in enumerate(blocks)])  # [W][M]
         del gathered
@@ -577,6 +584,20 @@ def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern, day_batch: Optional[int] = 
             own[:, s:e] = back[r, :, :e - s, :S_loc]
         del back
     kern.finalize(pdfq, own)
+
+
+def shard_width(comm, S_loc: int, stocks_total: Optional[int], dev) -> int:
+    """The padded stock width of the exchanges: the largest shard of dist.shard_bounds
+    (rank 0's), from the global stock count when the caller knows it -- no collective,
+    no host sync -- else agreed with one all-reduce."""
+    if stocks_total is not None:
+        from .dist import shard_bounds
+        s0, s1 = shard_bounds(int(stocks_total), comm.world_size, 0)
+        if S_loc > s1 - s0:
+            raise ValueError(f"shard of {S_loc} stocks exceeds the widest shard of {stocks_total} "
+                             f"over {comm.world_size} ranks")
+        return s1 - s0
+    return _agreed_max(comm, S_loc, dev)
 
 
 def _agreed_max(comm, n: int, dev) -> int:
@@ -609,8 +630,10 @@ def rolling(val: torch.Tensor, state: torch.Tensor, N: int, method: str):
     return ov, os_
 
 
-def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None):
-    """Stage 3 on [rows][D][S_loc]: per-day z-score ('z') or average rank ('rank')."""
+def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None,
+                  stocks_total: Optional[int] = None):
+    """Stage 3 on [rows][D][S_loc]: per-day z-score ('z') or average rank ('rank').
+    ``stocks_total``: the stocks over all ranks (sharded), or None (agreed by all-reduce)."""
     lib = _lib.load()
     rows, D, S = val.shape
     dev = val.device
@@ -629,7 +652,7 @@ def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None):
         _lib.check(lib.mff_xs_zscore(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(mom_all), R,
                                      _lib.ptr(ov), _lib.ptr(os_), st), "mff_xs_zscore")
     elif kind == "rank":
-        S_all = S if comm is None else _agreed_max(comm, S, dev)
+        S_all = S if comm is None else shard_width(comm, S, stocks_total, dev)
         v_all = val if comm is None else comm.all_gather(_pad_last(val, S_all, 0.0))
         s_all = state if comm is None else comm.all_gather(_pad_last(state, S_all, ABSENT))
         ws = torch.empty(lib.mff_xs_rank_workspace_bytes(rows, D, S_all, R), dtype=torch.uint8,
@@ -684,7 +707,7 @@ def ic_series(x_val: torch.Tensor, x_state: torch.Tensor, y_val: torch.Tensor,
 def group_returns(x_val: torch.Tensor, x_state: torch.Tensor, pct_val: torch.Tensor,
                   pct_state: torch.Tensor, period_of: torch.Tensor, P: int, group_num: int = 5,
                   w_val: Optional[torch.Tensor] = None, w_state: Optional[torch.Tensor] = None,
-                  comm=None):
+                  comm=None, stocks_total: Optional[int] = None):
     """Factor.py:231-350 on dense [D][S_loc] rows: per-date quantile groups of the
     exposure (mff_bt_qcut), per-period compounding with the previous period's group and
     weight (mff_bt_periods), per (period, group) mean / weighted mean over all ranks
@@ -696,7 +719,7 @@ def group_returns(x_val: torch.Tensor, x_state: torch.Tensor, pct_val: torch.Ten
     st = _stream(dev)
     R = 1 if comm is None else comm.world_size
     G = int(group_num)
-    S_all = S if comm is None else _agreed_max(comm, S, dev)
+    S_all = S if comm is None else shard_width(comm, S, stocks_total, dev)
     v_all = x_val if comm is None else comm.all_gather(_pad_last(x_val, S_all, 0.0))
     s_all = x_state if comm is None else comm.all_gather(_pad_last(x_state, S_all, ABSENT))
     ws = torch.empty(lib.mff_bt_qcut_workspace_bytes(D, S_all, R), dtype=torch.uint8, device=dev)

@@ -238,11 +238,17 @@ def _pdf_worker(rank, world, port, resq, day_batch=None):
     q = torch.from_numpy(_pdf_queries(sub))
     val = np.zeros((5, 5, s1 - s0))
     state = np.zeros((5, 5, s1 - s0), np.uint8)
-    S_all = engine._agreed_max(comm, s1 - s0, torch.device("cpu"))
-    engine._pdf_ranks_sharded(comm, q, S_all, _NumpyPdf(sub, val, state, list(range(5))), day_batch=day_batch)
+    # the padded width from the global stock count (no collective) = the agreed maximum
+    S_all = engine.shard_width(comm, s1 - s0, 13, torch.device("cpu"))
+    assert S_all == engine._agreed_max(comm, s1 - s0, torch.device("cpu"))
+    comm.stats = dist.CommStats()
+    sorted_calls = []
+    engine._pdf_ranks_sharded(comm, q, S_all, _NumpyPdf(sub, val, state, list(range(5))), day_batch=day_batch,
+                              after_sort=lambda: sorted_calls.append(1))
+    stats = comm.stats.summary()
     comm.barrier()
     dist_.destroy_process_group()
-    resq.put((rank, (val, state)))
+    resq.put((rank, (val, state, stats, len(sorted_calls))))
 
 
 @pytest.mark.parametrize("day_batch", [None, 1])  # one window / windows of 2 days (5 = 2 + 2 + 1)
@@ -262,6 +268,15 @@ def test_gloo_sharded_doc_pdf_exchange_world2(day_batch):
         assert p.exitcode == 0
     val = np.concatenate([res[0][0], res[1][0]], axis=2)
     state = np.concatenate([res[0][1], res[1][1]], axis=2)
+    # the exchange is accounted per collective (bench.py's N > 1 line), and the launch
+    # stream's SORT_FIRST hook fired once, after the first window's sort
+    windows = 1 if day_batch is None else 3
+    for r in (0, 1):
+        st, nsort = res[r][2], res[r][3]
+        assert nsort == 1
+        assert st["all_to_all"]["calls"] == 2 * windows and st["all_gather"]["calls"] == windows
+        assert st["reduce_scatter"]["calls"] == windows
+        assert all(v["sent_bytes"] > 0 for v in st.values())
     panel = synth.make_panel(13, 5, config=41, ragged=True)
     names = [f"doc_pdf{p}" for p in (60, 70, 80, 90, 95)]
     ov, os_ = O.oracle_stage1(panel, names)
