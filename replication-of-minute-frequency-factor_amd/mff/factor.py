@@ -153,8 +153,7 @@ class Factor:
         pd = _pd()
         pv = pv_data if pv_data is not None else self._read_daily_pv_data(["code", "date", "pct_change"])
         ex = self.factor_exposure
-        codes = sorted(set(map(str, ex["code"])) | set(map(str, pv["code"])))
-        dates = sorted(set(frames._as_date(x) for x in ex["date"]) | set(frames._as_date(x) for x in pv["date"]))
+        codes, dates = frames.universe(ex, pv)
         dev = _device(device)
         xv, xs, _, _ = frames.from_long(ex, self.factor_name, codes=codes, dates=dates)
         pv_v, pv_s, _, _ = frames.from_long(pv, "pct_change", codes=codes, dates=dates)
@@ -201,10 +200,8 @@ class Factor:
         pv = pv_data if pv_data is not None else self._read_daily_pv_data(
             ["code", "date", "pct_change", "tmc", "cmc"])
         ex = self.factor_exposure
-        dates = sorted(set(frames._as_date(x) for x in ex["date"]))
-        codes = sorted(set(map(str, ex["code"])))
-        pv = pv[pv["code"].astype(str).isin(set(codes)) &
-                pv["date"].map(frames._as_date).isin(set(dates))]
+        codes, dates = frames.universe(ex)
+        pv = pv[frames.rows_in(pv, codes, dates)]
         period_of, labels = rebalance_periods(dates, frequency)
         dev = _device(device)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
@@ -431,7 +428,7 @@ def _pending_files(folder_path, factor_exposure):
     index = pd.DataFrame({"file_name": file_names})
     index["date"] = pd.to_datetime(index["file_name"].str[:8], format="%Y%m%d").dt.date
     if factor_exposure is not None:
-        end_date = max(frames._as_date(x) for x in factor_exposure["date"])
+        end_date = frames.universe(factor_exposure)[1][-1]
         index = index[index["date"] > end_date]
     return index["file_name"].tolist()
 
@@ -449,10 +446,11 @@ def _merge(factor_exposure, valid):
 # ---------------------------------------------------------------- day-file batch results
 # Dense stage-1 results of every factor per day-file batch, keyed by the batch's files
 # (absolute path, size, mtime): a notebook running the 58 cal_* one after another over
-# the same folder reads and ingests every file once.  Entries are added while they fit
-# MFF_RESULT_CACHE_BYTES (default 8 GiB; 0 disables) and never evicted by a later insert
-# (a scan longer than the cache keeps its head cached instead of thrashing);
-# clear_result_cache() frees it.
+# the same folder reads and ingests every file once.  Only batches read and computed without
+# any error are cached (a read failure may be transient: the next call retries the
+# files).  Entries are added while they fit MFF_RESULT_CACHE_BYTES (default 4 GiB; 0
+# disables) and never evicted by a later insert (a scan longer than the cache keeps its
+# head cached instead of thrashing); clear_result_cache() frees it.
 _RESULTS: "OrderedDict" = None
 _RESULTS_BYTES = 0
 
@@ -464,7 +462,11 @@ def clear_result_cache() -> None:
 
 def result_cache_info() -> dict:
     return {"batches": 0 if _RESULTS is None else len(_RESULTS), "bytes": _RESULTS_BYTES,
-            "cap": int(os.environ.get("MFF_RESULT_CACHE_BYTES", str(8 << 30)))}
+            "cap": _cache_cap()}
+
+
+def _cache_cap() -> int:
+    return int(os.environ.get("MFF_RESULT_CACHE_BYTES", str(4 << 30)))
 
 
 def _batch_key(folder_path, files, device):
@@ -491,25 +493,20 @@ def _batch_results(files, folder_path, device):
     key = _batch_key(folder_path, files, device)
     if key is not None and _RESULTS is not None and key in _RESULTS:
         return _RESULTS[key]
-    tables, names, errors = [], [], {}
-    for f in files:
-        try:
-            tables.append(MinFreqFactor._read_day_file(os.path.join(folder_path, f)))
-            names.append(f)
-        except Exception as e:  # noqa: BLE001 -- MF:23-25: report and skip the day
-            errors[f] = str(e)
-    res = None
-    if tables:
-        try:  # one reference call per file (per-day semantics); a bad file drops its day only
-            v, s, _, codes, dates, dropped = compute_dense(tables, None, device, per_day=True, skip_bad=True)
-            res = (v, s, codes, dates)
-        except NoTables as e:
-            dropped = e.dropped
-        errors.update({names[k]: msg for k, msg in dropped.items()})
+    # the day files go to the ingest as paths: its host threads read (parquet, the code
+    # column from the files' dictionary pages) and encode them while earlier files move
+    # to the device; a file that cannot be read is reported like any other bad file
+    paths = [os.path.join(folder_path, f) for f in files]
+    errors, res = {}, None
+    try:  # one reference call per file (per-day semantics); a bad file drops its day only
+        v, s, _, codes, dates, dropped = compute_dense(paths, None, device, per_day=True, skip_bad=True)
+        res = (v, s, codes, dates)
+    except NoTables as e:
+        dropped = e.dropped
+    errors.update({files[k]: msg for k, msg in dropped.items()})
     out = (res, dict(sorted(errors.items())))
     nbytes = 0 if res is None else res[0].nbytes + res[1].nbytes
-    cap = int(os.environ.get("MFF_RESULT_CACHE_BYTES", str(8 << 30)))
-    if key is not None and _RESULTS_BYTES + nbytes <= cap:
+    if key is not None and not errors and res is not None and _RESULTS_BYTES + nbytes <= _cache_cap():
         if _RESULTS is None:
             _RESULTS = OrderedDict()
         _RESULTS[key] = out

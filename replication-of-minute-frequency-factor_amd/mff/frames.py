@@ -147,31 +147,127 @@ def to_long(val: np.ndarray, state: np.ndarray, codes: Sequence[str], dates: Seq
     return out.reset_index(drop=True)
 
 
+def _one(col):
+    """ChunkedArray -> Array without a copy when it has one chunk (a parquet day file
+    read whole usually does)."""
+    import pyarrow as pa
+
+    if isinstance(col, pa.ChunkedArray):
+        return col.chunk(0) if col.num_chunks == 1 else col.combine_chunks()
+    return col
+
+
+def _date32(col):
+    """date column (date32 / timestamp / date objects / ISO strings) -> int32 day numbers."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    col = _one(col)
+    t = col.type
+    if pa.types.is_date32(t):
+        pass
+    elif pa.types.is_date64(t) or pa.types.is_timestamp(t):
+        col = pc.cast(col, pa.date32())
+    elif pa.types.is_string(t) or pa.types.is_large_string(t):
+        col = pc.cast(pc.utf8_slice_codeunits(col, 0, 10), pa.date32())
+    else:
+        col = pa.array([_as_date(x) for x in col.to_pylist()], type=pa.date32())
+    return col.cast(pa.int32()).to_numpy(zero_copy_only=False)
+
+
+
+def _code_array(df):
+    import pyarrow as pa
+
+    return pa.array(df["code"].to_numpy(dtype=object)).cast(pa.string())
+
+
+def _date_array(df):
+    import pyarrow as pa
+
+    return pa.array(df["date"].to_numpy(dtype=object)) if df["date"].dtype == object \
+        else pa.Array.from_pandas(df["date"])
+
+
+def universe(*dfs):
+    """Sorted code strings and dates (datetime.date) over the rows of long frames,
+    vectorised (pyarrow unique)."""
+    import pyarrow.compute as pc
+
+    codes, days = set(), set()
+    for df in dfs:
+        codes.update(x for x in pc.unique(_code_array(df)).to_pylist() if x is not None)
+        days.update(np.unique(_day_numbers(_date_array(df))).tolist())
+    return sorted(codes), [_EPOCH + _dt.timedelta(days=int(v)) for v in sorted(days)]
+
+
+def rows_in(df, codes, dates) -> np.ndarray:
+    """bool mask of the rows whose code is in `codes` and date in `dates` (vectorised)."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    ok = np.asarray(pc.is_in(_code_array(df), value_set=pa.array(list(codes), pa.string()))
+                    .to_numpy(zero_copy_only=False), dtype=bool)
+    dn = _day_numbers(_date_array(df))
+    udn = np.array([(_as_date(v) - _EPOCH).days for v in dates], dtype=np.int64)
+    return ok & np.isin(dn, udn)
+
+
+def _day_numbers(col) -> np.ndarray:
+    """date column (date / datetime / ISO string / objects) -> int32 days since 1970."""
+    return _date32(col)
+
+
+_EPOCH = _dt.date(1970, 1, 1)
+
+
 def from_long(df, name: str, codes: Sequence[str] | None = None,
               dates: Sequence | None = None):
-    """Long exposure frame [code, date, name] -> dense (val, state, codes, dates)."""
-    import pandas as pd
+    """Long exposure frame [code, date, name] -> dense (val, state, codes, dates).
 
-    code = df["code"].astype(str).to_numpy()
-    date = np.array([_as_date(x) for x in df["date"]], dtype=object)
-    ucodes = sorted(set(code.tolist())) if codes is None else list(codes)
-    udates = sorted(set(date.tolist())) if dates is None else list(dates)
-    ci = {c: i for i, c in enumerate(ucodes)}
-    di = {d: i for i, d in enumerate(udates)}
-    D, S = len(udates), len(ucodes)
-    val = np.zeros((D, S), dtype=np.float64)
-    state = np.zeros((D, S), dtype=np.uint8)
+    Vectorised over the rows (pyarrow compute: the codes' positions in the sorted code
+    universe, dates as day numbers, the value column's null mask), no per-row Python."""
+    import pandas as pd
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
     col = df[name]
     if isinstance(col.dtype, pd.ArrowDtype):  # null and NaN kept apart
         arr = col.array._pa_array.combine_chunks()
         isnull = np.asarray(arr.is_null().to_numpy(zero_copy_only=False), dtype=bool)
         x = np.asarray(arr.fill_null(0.0).to_numpy(zero_copy_only=False), dtype=np.float64)
-    else:  # numpy columns: None / pd.NA are nulls, NaN is a value
+    elif col.dtype == object:  # None / pd.NA are nulls, NaN is a value
         obj = col.to_numpy(dtype=object)
-        isnull = np.array([v is None or v is pd.NA for v in obj], dtype=bool)
-        x = np.array([0.0 if n else float(v) for v, n in zip(obj, isnull)], dtype=np.float64)
-    s = np.fromiter((ci[c] for c in code), dtype=np.int64, count=code.size)
-    d = np.fromiter((di[v] for v in date), dtype=np.int64, count=date.size)
+        isnull = pd.isna(obj) & ~np.array([isinstance(v, float) for v in obj], dtype=bool)
+        x = np.where(isnull, 0.0, pd.to_numeric(pd.Series(obj).where(~isnull, 0.0)).to_numpy(np.float64))
+    else:  # a numpy float column: NaN is a value (no nulls)
+        x = np.asarray(col.to_numpy(), dtype=np.float64)
+        isnull = np.zeros(x.size, dtype=bool)
+    code = _code_array(df)
+    dn = _day_numbers(_date_array(df))
+    if codes is None:
+        ucodes = sorted(x_ for x_ in pc.unique(code).to_pylist() if x_ is not None)
+    else:
+        ucodes = list(codes)
+    if dates is None:
+        udn = np.unique(dn)
+        udates = [_EPOCH + _dt.timedelta(days=int(v)) for v in udn]
+    else:
+        udates = list(dates)
+        udn = np.array([(_as_date(v) - _EPOCH).days for v in udates], dtype=np.int64)
+    si = pc.index_in(code, value_set=pa.array(ucodes, pa.string()))
+    if si.null_count:
+        raise KeyError("a code of the frame is not in the code universe")
+    s = si.to_numpy(zero_copy_only=False).astype(np.int64)
+    order = np.argsort(udn, kind="stable")
+    pos = np.searchsorted(udn[order], dn)
+    pos = np.minimum(pos, max(len(udn) - 1, 0))
+    if len(udn) == 0 or (udn[order][pos] != dn).any():
+        raise KeyError("a date of the frame is not in the date universe")
+    d = order[pos]
+    D, S = len(udates), len(ucodes)
+    val = np.zeros((D, S), dtype=np.float64)
+    state = np.zeros((D, S), dtype=np.uint8)
     state[d, s] = np.where(isnull, 1, 2)
     val[d, s] = np.where(isnull, 0.0, x)
     return val, state, ucodes, udates

@@ -36,12 +36,24 @@ _VOLUME_KIND = {np.dtype(np.float64): 0, np.dtype(np.int64): 1, np.dtype(np.floa
 _EPOCH = _dt.date(1970, 1, 1)
 
 
+def read_day_file(path):
+    """A parquet day file -> pyarrow Table, its code column decoded straight from the
+    file's dictionary pages (no hash pass over the strings; MinuteFrequentFactorCICC.py:22
+    reads the same file with pl.read_parquet)."""
+    import pyarrow.parquet as pq
+
+    return pq.read_table(path, read_dictionary=["code"])
+
+
 def _table(df):
-    """pandas / pyarrow / dict / polars-like (``to_arrow``) -> pyarrow Table."""
+    """pandas / pyarrow / dict / polars-like (``to_arrow``) / a parquet path -> pyarrow
+    Table."""
     import pyarrow as pa
 
     if isinstance(df, pa.Table):
         return df
+    if isinstance(df, (str, os.PathLike)):
+        return read_day_file(df)
     if hasattr(df, "to_arrow") and not hasattr(df, "to_pandas_dtype"):
         return df.to_arrow()
     if isinstance(df, dict):
@@ -49,37 +61,7 @@ def _table(df):
     return pa.Table.from_pandas(df, preserve_index=False)
 
 
-def _date32(col):
-    """date column (date32 / timestamp / date objects / ISO strings) -> int32 day numbers."""
-    import pyarrow as pa
-    import pyarrow.compute as pc
-
-    col = _one(col)
-    t = col.type
-    if pa.types.is_date32(t):
-        pass
-    elif pa.types.is_date64(t) or pa.types.is_timestamp(t):
-        col = pc.cast(col, pa.date32())
-    elif pa.types.is_string(t) or pa.types.is_large_string(t):
-        col = pc.cast(pc.utf8_slice_codeunits(col, 0, 10), pa.date32())
-    else:
-        col = pa.array([_as_date(x) for x in col.to_pylist()], type=pa.date32())
-    return col.cast(pa.int32()).to_numpy(zero_copy_only=False)
-
-
-def _as_date(x):
-    from .frames import _as_date as f
-    return f(x)
-
-
-def _one(col):
-    """ChunkedArray -> Array without a copy when it has one chunk (a parquet day file
-    read whole usually does)."""
-    import pyarrow as pa
-
-    if isinstance(col, pa.ChunkedArray):
-        return col.chunk(0) if col.num_chunks == 1 else col.combine_chunks()
-    return col
+from .frames import _as_date, _date32, _one  # noqa: E402  (host-only helpers, no torch)
 
 
 def _numeric(col, dtype, fill=float("nan")):
@@ -123,7 +105,7 @@ def _dict_codes(t):
 
     if "code" not in t.column_names:
         return t
-    col = _one(t.column("code"))
+    col = t.column("code")  # chunked: encoded chunk by chunk against one dictionary
     if pa.types.is_dictionary(col.type):
         return t
     if not (pa.types.is_string(col.type) or pa.types.is_large_string(col.type)):
@@ -132,35 +114,69 @@ def _dict_codes(t):
 
 
 def _code_values(col):
+    """The distinct codes of a column (the chunks' dictionaries when it is dictionary-
+    encoded: parquet row groups may carry different ones)."""
     import pyarrow as pa
     import pyarrow.compute as pc
 
-    col = _one(col)
-    if pa.types.is_dictionary(col.type):
-        return [x for x in col.dictionary.to_pylist() if x is not None]
+    chunks = col.chunks if isinstance(col, pa.ChunkedArray) else [col]
+    if chunks and pa.types.is_dictionary(chunks[0].type):
+        out, seen = set(), []
+        for c in chunks:
+            if any(c.dictionary is d or c.dictionary.equals(d) for d in seen[-1:]):
+                continue
+            seen.append(c.dictionary)
+            out.update(c.dictionary.to_pylist())
+        out.discard(None)
+        return list(out)
     return [x for x in pc.unique(col).to_pylist() if x is not None]
 
 
-def _stock_index(col, codes) -> np.ndarray:
-    """code column -> int32 index into the sorted universe `codes` (-1: not in it / null)."""
+def _stock_index(col, codes, vs=None, pos=None) -> np.ndarray:
+    """code column -> int32 index into the sorted universe `codes` (-1: not in it / null).
+    A dictionary column maps its (small) dictionary through ``pos`` ({code: index}, a
+    plain dict: no pyarrow set lookup is shared between the ingest's threads) and takes
+    the row indices through it."""
     import pyarrow as pa
     import pyarrow.compute as pc
 
-    vs = pa.array(list(codes), pa.string())
     col = _one(col)
     if pa.types.is_dictionary(col.type):
+        memo = pos if isinstance(pos, _DictMemo) else _DictMemo(pos or {c: i for i, c in enumerate(codes)})
         dic = col.dictionary
-        if not (pa.types.is_string(dic.type) or pa.types.is_large_string(dic.type)):
-            dic = pc.cast(dic, pa.string())
-        m = np.asarray(pc.fill_null(pc.index_in(dic, value_set=vs), -1).to_numpy(zero_copy_only=False),
-                       dtype=np.int32)
-        m = np.append(m, np.int32(-1))  # slot for null rows
-        idx = pc.fill_null(col.indices, len(dic)).to_numpy(zero_copy_only=False)
+        m = memo(dic)
+        ind = col.indices
+        idx = (ind.to_numpy(zero_copy_only=False) if ind.null_count == 0
+               else np.where(np.asarray(ind.is_null()), len(dic), ind.to_numpy(zero_copy_only=False)))
         return np.ascontiguousarray(m[idx], dtype=np.int32)
+    if vs is None:
+        vs = pa.array(list(codes), pa.string())
     if not (pa.types.is_string(col.type) or pa.types.is_large_string(col.type)):
         col = pc.cast(col, pa.string())
     stock = pc.fill_null(pc.index_in(col, value_set=vs), -1)
     return np.ascontiguousarray(stock.to_numpy(zero_copy_only=False), dtype=np.int32)
+
+
+class _DictMemo:
+    """dictionary -> int32 universe index per entry (+ a -1 slot for null rows), through
+    a plain {code: index} dict; the record batches of one table usually share one
+    dictionary, so the last mapping is reused when the next dictionary equals it."""
+
+    def __init__(self, pos):
+        self.pos, self.dic, self.m = pos, None, None
+
+    def __call__(self, dic):
+        import pyarrow as pa
+        import pyarrow.compute as pc
+
+        if self.dic is not None and (dic is self.dic or dic.equals(self.dic)):
+            return self.m
+        d = dic
+        if not (pa.types.is_string(d.type) or pa.types.is_large_string(d.type)):
+            d = pc.cast(d, pa.string())
+        m = np.fromiter((self.pos.get(x, -1) for x in d.to_pylist()), dtype=np.int32, count=len(d))
+        self.dic, self.m = dic, np.append(m, np.int32(-1))  # slot for null rows
+        return self.m
 
 
 def universes(tables) -> tuple:
@@ -172,18 +188,12 @@ def universes(tables) -> tuple:
     return sorted(codes), sorted(days)
 
 
-def encode(t, codes: Sequence[str], day_numbers: Sequence[int]):
-    """One table -> (stock int32, day int32, time int64, 4 x price f64, volume, kind).
-    Codes / dates outside the universes get index -1 (counted by the kernel)."""
-    import pyarrow as pa
-    import pyarrow.compute as pc
-
-    for k in ("code", "date", "time") + FIELDS:
-        if k not in t.column_names:
-            raise ValueError(f"missing column {k!r}")
-    stock = _stock_index(t.column("code"), codes)
+def _encode_batch(t, codes, vs, uday, pos=None):
+    """One record batch (or table) -> (stock int32, day int32, time int64, 4 x price f64,
+    volume, kind, null bits uint8 or None); numeric columns zero-copy where the batch's
+    types already match."""
+    stock = _stock_index(t.column("code"), codes, vs, pos)
     dn = _date32(t.column("date"))
-    uday = np.asarray(day_numbers, dtype=np.int32)
     lo, hi = (int(dn.min()), int(dn.max())) if dn.size else (0, 0)
     if lo == hi:  # a day file: one date
         k = int(np.searchsorted(uday, lo))
@@ -208,6 +218,57 @@ def encode(t, codes: Sequence[str], day_numbers: Sequence[int]):
             if m is not None:
                 nbits |= m.astype(np.uint8) << i
     return stock, day, time, px, vol, kind, nbits
+
+
+def code_set(codes: Sequence[str]):
+    """The code universe as a pyarrow string array (the value set of the stock lookups).
+    Built once, on the calling thread: pa.array over Python strings is not safe to run
+    concurrently from several threads (it crashed this pyarrow build)."""
+    import pyarrow as pa
+
+    return pa.array(list(codes), pa.string())
+
+
+def encode_batches(t, codes: Sequence[str], day_numbers: Sequence[int], vs=None, pos=None) -> list:
+    """One table -> a list of encoded record batches (:func:`_encode_batch`), without
+    concatenating its chunks (a parquet file read whole holds one chunk per row group):
+    PanelIngest.push_encoded copies each batch straight into its pinned staging slot.
+    ``vs``: :func:`code_set` of `codes` (required when called from worker threads)."""
+    for k in ("code", "date", "time") + FIELDS:
+        if k not in t.column_names:
+            raise ValueError(f"missing column {k!r}")
+    if vs is None:
+        vs = code_set(codes)
+    uday = np.asarray(day_numbers, dtype=np.int32)
+    if pos is None:
+        pos = {c: i for i, c in enumerate(codes)}
+    memo = _DictMemo(pos)
+    out = [_encode_batch(b, codes, vs, uday, memo) for b in t.to_batches() if b.num_rows]
+    kinds = {e[5] for e in out}
+    if len(kinds) > 1:  # batches of one table share its schema; guard anyway
+        raise ValueError("volume column type differs between record batches")
+    return out
+
+
+def encode(t, codes: Sequence[str], day_numbers: Sequence[int]):
+    """One table -> (stock int32, day int32, time int64, 4 x price f64, volume, kind,
+    null bits uint8 [rows] or None).  Codes / dates outside the universes get index -1
+    (counted by the kernel)."""
+    import pyarrow as pa
+
+    vs = code_set(codes)
+    bs = encode_batches(t, codes, day_numbers, vs)
+    if not bs:
+        return _encode_batch(t.slice(0, 0).combine_chunks() if hasattr(t, "combine_chunks") else t, codes,
+                             vs, np.asarray(day_numbers, dtype=np.int32))
+    if len(bs) == 1:
+        return bs[0]
+    cat = lambda j: np.concatenate([b[j] for b in bs])
+    px = [np.concatenate([b[3][i] for b in bs]) for i in range(4)]
+    nb = None
+    if any(b[6] is not None for b in bs):
+        nb = np.concatenate([b[6] if b[6] is not None else np.zeros(b[0].size, np.uint8) for b in bs])
+    return cat(0), cat(1), cat(2), px, cat(4), bs[0][5], nb
 
 
 class PanelIngest:
@@ -237,6 +298,8 @@ class PanelIngest:
         if S == 0 or D == 0:
             raise ValueError("empty code or date universe")
         self.S, self.D = S, D
+        self.vs = code_set(self.codes)  # built here, on the caller's thread
+        self.pos = {c: i for i, c in enumerate(self.codes)}
         self.bars = torch.empty((5, D, S, 240), dtype=torch.float32, device=self.dev)
         self.mask = torch.zeros((D, S, 8), dtype=torch.int32, device=self.dev)
         # contract-violation counters, one [5] row per push (chunks of ERR_CHUNK rows, so
@@ -273,26 +336,38 @@ class PanelIngest:
         return s
 
     def push(self, df) -> None:
-        self.push_encoded(encode(_table(df), self.codes, self.day_numbers))
+        self.push_encoded(encode_batches(_table(df), self.codes, self.day_numbers, self.vs, self.pos))
 
-    def _cells(self, stock, day) -> np.ndarray:
+    def _cells(self, batches) -> np.ndarray:
         """The in-range (day * S + stock) cells a push writes, ascending."""
-        ok = (stock >= 0) & (day >= 0)
-        if stock.size and ok.all() and day[0] == day[-1] and (day == day[0]).all():
+        days = {int(b[1][0]) for b in batches if b[1].size}
+        one_day = len(days) == 1 and all(b[1].size == 0 or (b[1][0] == b[1][-1] and (b[1] == b[1][0]).all())
+                                         for b in batches)
+        if one_day and next(iter(days)) >= 0:
             seen = np.zeros(self.S, dtype=bool)  # a day file: one day, mark its stocks
-            seen[stock] = True
-            return int(day[0]) * self.S + np.flatnonzero(seen).astype(np.int64)
-        return np.unique(day[ok].astype(np.int64) * self.S + stock[ok])
+            for b in batches:
+                st = b[0]
+                seen[st[st >= 0]] = True
+            return next(iter(days)) * self.S + np.flatnonzero(seen).astype(np.int64)
+        cells = []
+        for b in batches:
+            ok = (b[0] >= 0) & (b[1] >= 0)
+            cells.append(b[1][ok].astype(np.int64) * self.S + b[0][ok])
+        return np.unique(np.concatenate(cells)) if cells else np.zeros(0, np.int64)
 
     def push_encoded(self, enc) -> None:
-        """Stage and launch one table already encoded by :func:`encode`."""
-        stock, day, time, px, vol, kind, nbits = enc
-        n = int(stock.size)
+        """Stage and launch one table already encoded by :func:`encode` (one tuple) or
+        :func:`encode_batches` (a list of record-batch tuples: each copied straight into
+        the pinned staging slot, no concatenation)."""
+        batches = [enc] if isinstance(enc, tuple) else list(enc)
+        n = int(sum(b[0].size for b in batches))
         k = len(self.table_cells)
         err = self._err_row(k)
-        self.table_cells.append(self._cells(stock, day) if n else np.zeros(0, np.int64))
-        if nbits is not None:
-            from .frames import time_to_minute
+        self.table_cells.append(self._cells(batches) if n else np.zeros(0, np.int64))
+        from .frames import time_to_minute
+        for stock, day, time, _, _, _, nbits in batches:
+            if nbits is None:
+                continue
             r = np.flatnonzero((nbits != 0) & (stock >= 0) & (day >= 0))
             if r.size:
                 m = time_to_minute(time[r])
@@ -300,15 +375,20 @@ class PanelIngest:
                 self._null_rows.append(((day[r].astype(np.int64) * self.S + stock[r])[on], m[on], nbits[r][on]))
         if n == 0:
             return
-        cols = [stock, day, time] + px + [vol]
+        kind = batches[0][5]
+        cols = [[b[0] for b in batches], [b[1] for b in batches], [b[2] for b in batches]]
+        cols += [[b[3][i] for b in batches] for i in range(4)]
+        cols.append([b[4] for b in batches])
         offs, o = [], 0
-        for c in cols:
+        for parts in cols:
             offs.append(o)
-            o += (c.nbytes + 15) // 16 * 16
+            o += (sum(c.nbytes for c in parts) + 15) // 16 * 16
         pinned, dbuf, ev = self._slot(o)
         host = pinned.numpy()
-        for c, off in zip(cols, offs):
-            host[off:off + c.nbytes] = c.view(np.uint8).reshape(-1)
+        for parts, off in zip(cols, offs):
+            for c in parts:
+                host[off:off + c.nbytes] = c.view(np.uint8).reshape(-1)
+                off += c.nbytes
         with torch.cuda.stream(self.stream):
             dbuf[:o].copy_(pinned[:o], non_blocking=True)
             ev.record(self.stream)
@@ -410,7 +490,7 @@ def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None, skip_
     dropped = {}
     # pyarrow / numpy kernels release the GIL: tables are encoded by a few host threads
     # (in order, a bounded window ahead) while earlier ones are copied and scattered
-    workers = max(1, min(4, len(raw), os.cpu_count() or 1))
+    workers = max(1, min(8, len(raw), os.cpu_count() or 1))
 
     def prep(t):
         t = _dict_codes(_table(t))
@@ -441,7 +521,7 @@ def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None, skip_
 
         def enc_safe(t):
             try:
-                return encode(t, ing.codes, ing.day_numbers), None
+                return encode_batches(t, ing.codes, ing.day_numbers, ing.vs, ing.pos), None
             except Exception as e:  # noqa: BLE001
                 if not skip_bad:
                     raise

@@ -178,7 +178,7 @@ def test_all_factors_one_ingest_and_result_cache(dev, tmp_path, monkeypatch):
     import mff_oracle as O
     from MinuteFrequentFactorCICC import MinFreqFactor
     import MinuteFrequentFactorCalculateMethodsCICC as CM
-    from mff import catalog, factor, synth
+    from mff import catalog, factor, ingest, synth
     panel = synth.make_panel(25, 4, config=24, ragged=True)
     folder = str(tmp_path / "kl")
     os.mkdir(folder)
@@ -186,8 +186,8 @@ def test_all_factors_one_ingest_and_result_cache(dev, tmp_path, monkeypatch):
     ov, os_ = O.oracle_stage1(panel)
     factor.clear_result_cache()
     reads = []
-    orig = MinFreqFactor._read_day_file
-    monkeypatch.setattr(MinFreqFactor, "_read_day_file", staticmethod(lambda p: reads.append(p) or orig(p)))
+    orig = ingest.read_day_file  # the GPU batches read their day files in the ingest's threads
+    monkeypatch.setattr(ingest, "read_day_file", lambda p: reads.append(p) or orig(p))
     out = MinFreqFactor.cal_exposures_by_min_data(path=str(tmp_path / "exp"), folder_path=folder, batch_days=3)
     assert list(out) == catalog.NAMES and len(reads) == 4
     bad = []
