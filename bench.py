@@ -295,6 +295,8 @@ def main():
     ap.add_argument("--cpu-stocks", type=int, default=400)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--kernel-times", action="store_true",
+                    help="with --no-extras: still time every stage-1 launch alone (roofline.kernels)")
     ap.add_argument("--ingest-days", type=int, default=20)
     ap.add_argument("--ingest-host-days", type=int, default=4)
     ap.add_argument("--e2e-days", type=int, default=8)
@@ -373,6 +375,10 @@ def main():
 
     extras = {}
     per_kernel = None
+    if args.no_extras and args.kernel_times:
+        kt = engine.stage1_launch_times(panel)
+        per_kernel = {k: {"ms": round(x["ms"], 3)} for k, x in kt.items() if x["ms"] > 0}
+        per_kernel["serial_sum_ms"] = round(sum(x["ms"] for x in kt.values()), 3)
     if not args.no_extras:
         val, state, _ = step()
         torch.cuda.synchronize()

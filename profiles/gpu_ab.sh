@@ -27,6 +27,9 @@ rows = {}
 for run in runs:
     d = json.loads([l for l in open(f'{R}/{run}.log') if l.startswith('{')][0])
     rows.setdefault('value M/s', {})[run] = d['value'] / 1e6
+    for k, x in ((d.get('roofline') or {}).get('kernels') or {}).items():
+        if isinstance(x, dict):
+            rows.setdefault('alone ' + k[:54], {})[run] = x['ms']
     for f in glob.glob(f'{R}/{run}/**/*kernel_stats.csv', recursive=True):
         for x in csv.DictReader(open(f)):
             if 'mff' in x['Name']:

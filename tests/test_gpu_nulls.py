@@ -139,6 +139,7 @@ def test_nan_price_from_pandas_is_null(dev):
     v, s, _, _ = frames.from_long(res["vol_volume1min"], "vol_volume1min")
     assert s[0, 0] == 2 and v[0, 0] == pytest.approx(np.std([100.0, 300.0], ddof=1))
     v, s, _, _ = frames.from_long(res["vol_range1min"], "vol_range1min")
-    assert s[0, 0] == 2 and v[0, 0] == pytest.approx(np.std([10.2 / 9.9, 10.3 / 10.1], ddof=1))
+    f = lambda x: float(np.float32(x))  # the device planes hold fp32 prices
+    assert s[0, 0] == 2 and v[0, 0] == pytest.approx(np.std([f(10.2) / f(9.9), f(10.3) / f(10.1)], ddof=1))
     v, s, _, _ = frames.from_long(res["liq_openvol"], "liq_openvol")
     assert s[0, 0] == 2 and v[0, 0] == 100.0
