@@ -107,6 +107,26 @@ def main():
             parts = ", ".join(f"{k}: {v}" for k, v in sorted(table[name].items()))
             print(f"  {name:28s} {sum(table[name].values()):6d}   {parts}")
     print("  total by loop: " + ", ".join(f"{k}: {v}" for k, v in sorted(total.items())))
+    # dynamic estimate: depth-1 blocks once per iteration of the outer loop, depth-2 blocks
+    # `inner_trips` times, the prologue (depth 0) once per `outer_trips` iterations;
+    # per unit = per iteration / `units_per_iteration`
+    dyn = cfg.get("dynamic")
+    if dyn:
+        per_it = {}
+        for name in [s[0] for s in cfg["sections"]] + ["other"]:
+            x = 0.0
+            for k, v in table.get(name, {}).items():
+                depth = int(k.split("depth ")[1].rstrip(")"))
+                x += v * (1.0 / dyn["outer_trips"] if depth == 0 else 1.0 if depth == 1 else dyn["inner_trips"])
+            per_it[name] = x
+        u = dyn["units_per_iteration"]
+        tot = sum(per_it.values())
+        print(f"dynamic estimate per {dyn['unit']} (depth-2 loops x {dyn['inner_trips']}, prologue / "
+              f"{dyn['outer_trips']}; common path, rare branches counted too):")
+        for name, x in per_it.items():
+            if x:
+                print(f"  {name:28s} {x / u:8.1f}   {100.0 * x / tot:5.1f} %")
+        print(f"  {'total':28s} {tot / u:8.1f}" + (f"   (PMC: {dyn['pmc']})" if "pmc" in dyn else ""))
 
 
 if __name__ == "__main__":

@@ -301,31 +301,12 @@ __device__ __forceinline__ void glocal_tail(uint32_t (&a)[K]) {
   glocal<2, false>(a);
   glocal<1, false>(a);
 }
-// ascending sort of a lane's 16 keys: Green's 60-comparator network (depth 10; checked
-// on all 2^16 0-1 inputs), 120 min / max instead of the 160 of the four bitonic sizes
-// 2..16
-__device__ __forceinline__ void gsort16_local(uint32_t (&a)[K]) {
-  constexpr int8_t P[60][2] = {
-      {0, 13}, {1, 12}, {2, 15}, {3, 14}, {4, 8}, {5, 6}, {7, 11}, {9, 10},
-      {0, 5}, {1, 7}, {2, 9}, {3, 4}, {6, 13}, {8, 14}, {10, 15}, {11, 12},
-      {0, 1}, {2, 3}, {4, 5}, {6, 8}, {7, 9}, {10, 11}, {12, 13}, {14, 15},
-      {0, 2}, {1, 3}, {4, 10}, {5, 11}, {6, 7}, {8, 9}, {12, 14}, {13, 15},
-      {1, 2}, {3, 12}, {4, 6}, {5, 7}, {8, 10}, {9, 11}, {13, 14},
-      {1, 4}, {2, 6}, {5, 8}, {7, 10}, {9, 13}, {11, 14},
-      {2, 4}, {3, 6}, {9, 12}, {11, 13},
-      {3, 5}, {6, 8}, {7, 9}, {10, 12},
-      {3, 4}, {5, 6}, {7, 8}, {9, 10}, {11, 12},
-      {6, 7}, {8, 9}};
-#pragma unroll
-  for (int i = 0; i < 60; ++i) {
-    const uint32_t x = a[P[i][0]], y = a[P[i][1]];
-    a[P[i][0]] = min(x, y);
-    a[P[i][1]] = max(x, y);
-  }
-}
 __device__ __forceinline__ void gsort256u(uint32_t (&a)[K]) {
   // sizes 2..16 inside the lane
-  gsort16_local(a);
+  glocal<1, true>(a);
+  glocal<2, true>(a); glocal<1, false>(a);
+  glocal<4, true>(a); glocal<2, false>(a); glocal<1, false>(a);
+  glocal<8, true>(a); glocal<4, false>(a); glocal<2, false>(a); glocal<1, false>(a);
   // size 32: flip with lane ^ 1
   gcross<1, 1, true>(a); glocal_tail(a);
   // size 64: flip lane ^ 3, then lane ^ 1

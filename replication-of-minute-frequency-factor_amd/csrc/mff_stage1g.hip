@@ -53,11 +53,6 @@ int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D
 #ifndef MFF_MERGE_OL
 #define MFF_MERGE_OL 1
 #endif
-// the LVL section's tick-histogram path (no sort for closes on the 0.01 grid); off until
-// it measures faster than the sort (A/B: profiles/r04*)
-#ifndef MFF_TICK
-#define MFF_TICK 0
-#endif
 
 namespace g16 {
 
@@ -194,8 +189,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
   // so a store of 16 consecutive words per group covers the 64 banks once
   // per group: the sorted families need 2 x 240 words (level cumulative volumes and
   // close words; the 256-word key / volume images fit inside), the OLS betas 256 doubles
-  // (the tick histogram of the LVL section: 256 u64 = 2 x 256 words)
-  constexpr int SW = (SET & F_OLS) ? 2 * NB : 2 * 256;  // words
+  constexpr int SW = (SET & F_OLS) ? 2 * NB : 2 * NBAR;  // words
   __shared__ __attribute__((aligned(16))) uint64_t scratch[16][SW / 2 + 8];
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
@@ -816,84 +810,19 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
         const float clastf = gval(c, lb);
         bool fast = !gany(!ok);
         const int e0 = 16 * g;
-        const uint32_t cbase = cmx;
+        uint32_t cw[K], vv[K], cbase = cmx;
         // a day whose closes span >= 2^24 float steps (a close ratio of 2 or more) does
         // not fit the u32 keys: the exact wave64 kernel takes it whole (values, queries
         // and its doc_pdf levels; list entry flagged by the top bit)
         const bool wide = cmx - cmn >= (1u << 24);  // uniform inside the group
-        // Tick path (round 4): closes on the 0.01 grid -- every bar's close is the fp32 of
-        // t * 0.01 for t = rint(100 c) (the canonical (float)(double(t) * 0.01)) -- whose
-        // ticks span < 256 need no sort: levels are the occupied slots tmax - t of a
-        // 256-entry histogram of (bars << 32 | volume), filled by one LDS atomic per bar,
-        // and slot order is descending close, the sorted order below.  The histogram is
-        // filled while the eligibility is checked (slot 256 takes the bars that do not
-        // fit; a wave that is not eligible throws it away and sorts).  Else (off-grid or
-        // wider days, or a day volume of 2^32 or more) the bitonic sort of the bars.
-        uint64_t* hist = scr;  // 257 slots: slot j = tick tmax - j, slot 256 = overflow
-        const bool try_tick = MFF_TICK && !wide && bitsf(cmx) < 65536.0f && ok;  // rint(100 c) exact below 2^24
-        const int tmi = (int)__builtin_rintf(bitsf(cmx) * 100.0f);  // the highest close's tick
-        bool tick = false;
-        if (__any(try_tick)) {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) reinterpret_cast<uint4*>(hist)[8 * g + q] = make_uint4(0u, 0u, 0u, 0u);
-          lds_fence();
-          bool on = true;
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            const float t = __builtin_rintf(c[k] * 100.0f);
-            const bool p = (pb >> k) & 1u;
-            const int slot = tmi - (int)t;  // >= 0: c <= cmax
-            const bool fit = (float)((double)t * 0.01) == c[k] && (uint32_t)slot < 256u;
-            on = on && (!p || fit);
-            const uint32_t j = (p && fit) ? (uint32_t)slot : 256u;  // absent / misfit: slot 256
-            atomicAdd(reinterpret_cast<unsigned long long*>(hist + j), (1ull << 32) | (uint64_t)v[k]);
-          }
-          tick = try_tick && !gany(!on);
-        }
-        // wave-uniform: the tick path only when every active group of the wave takes it (a
-        // divergent wave would keep the bars' registers live across both paths and spill)
-        tick = __all(tick);
         if (wide) {
           if (g == 0) {
             const int idx = atomicAdd(a.fb_count, 1);
             a.fb_list[idx] = (int)((uint32_t)sd | 0x80000000u);
           }
-        }
-        uint32_t* lv = reinterpret_cast<uint32_t*>(scr);
-        uint32_t* lc = lv + NBAR;  // L <= 240 levels
-        int L = 0;
-        if (!wide && tick) {
-          lds_fence();
-          // slot k of this lane: volume hv[k], bars (< 256) in byte k & 3 of hn4[k >> 2]
-          uint32_t hv[K], hn4[K / 4] = {0u, 0u, 0u, 0u}, tv = 0u, tn = 0u, endm = 0u;
 #pragma unroll
-          for (int k = 0; k < K; ++k) {
-            const uint64_t x = hist[16 * g + k];
-            const uint32_t nb = (uint32_t)(x >> 32);
-            hv[k] = (uint32_t)x;
-            hn4[k >> 2] |= nb << (8 * (k & 3));
-            tv += hv[k];
-            tn += nb;
-            endm |= (nb != 0u ? 1u : 0u) << k;
-          }
-          lds_fence();  // lv / lc overwrite the histogram
-          L = gcount(endm);
-          uint32_t cum = gscan_excl_u(tv), ecnt = gscan_excl_u(tn);
-          int li = (int)gscan_excl_u((uint32_t)__builtin_popcount(endm));
-#pragma unroll
-          for (int k = 0; k < K; ++k) {
-            cum += hv[k];
-            ecnt += (hn4[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-            const uint32_t end = (endm >> k) & 1u;
-            const float cl = (float)((double)(tmi - (16 * g + k)) * 0.01);
-            // a non-level slot writes to spare words 500 / 501 of the group's scratch
-            lv[end ? li : 500] = cum;
-            lc[end ? li : 501 - NBAR] = ((cmx - fbits(cl)) << 8) | (ecnt - 1u);
-            li += (int)end;
-          }
-          lds_fence();
-        } else if (!wide) {
-          uint32_t cw[K], vv[K];
+          for (int k = 0; k < K; ++k) { cw[k] = 0u; vv[k] = 0u; }
+        } else {
           // 256 volumes of this group, bar 16g + k at slot 16k + g (the key's low byte):
           // each store instruction writes 16 consecutive words per group (conflict free)
           uint32_t* sv = reinterpret_cast<uint32_t*>(scr);
@@ -912,22 +841,29 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
             vv[k] = sv[key[k] & 0xffu];  // elements past n: key ~0 -> slot 255 (bar 255: none, 0)
           }
           lds_fence();
-          // Levels = runs of equal close words among the n sorted bars.  validm: this lane's
-          // elements e < n; a run ends where the next element's word differs (or at
-          // e = n - 1); the element after an end starts a run.
-          const int nin = min(max(n - e0, 0), K);
-          const uint32_t validm = (uint32_t)((1u << nin) - 1u);
-          const uint32_t nextw = dpp_u<ROW_SHL + 1>(cw[0]);
-          uint32_t diffm = 0u, tv = 0u;
+        }
+        // Levels = runs of equal close words among the n sorted bars.  validm: this lane's
+        // elements e < n; a run ends where the next element's word differs (or at
+        // e = n - 1); the element after an end starts a run.
+        const int nin = min(max(n - e0, 0), K);
+        const uint32_t validm = (uint32_t)((1u << nin) - 1u);
+        const uint32_t nextw = dpp_u<ROW_SHL + 1>(cw[0]);
+        uint32_t diffm = 0u, tv = 0u;
 #pragma unroll
-          for (int k = 0; k < K; ++k) {
-            const uint32_t wn = k < K - 1 ? cw[k + 1] : nextw;
-            diffm |= (cw[k] != wn ? 1u : 0u) << k;
-            tv += vv[k];  // 0 past n
-          }
-          const uint32_t lastm = (n - 1 >= e0 && n - 1 < e0 + K) ? 1u << (n - 1 - e0) : 0u;
-          const uint32_t endm = (diffm | lastm) & validm;
-          L = gcount(endm);
+        for (int k = 0; k < K; ++k) {
+          const uint32_t wn = k < K - 1 ? cw[k + 1] : nextw;
+          diffm |= (cw[k] != wn ? 1u : 0u) << k;
+          tv += vv[k];  // 0 past n
+        }
+        const uint32_t lastm = (n - 1 >= e0 && n - 1 < e0 + K) ? 1u << (n - 1 - e0) : 0u;
+        const uint32_t endm = (diffm | lastm) & validm;
+        const int L = gcount(endm);
+        if (!wide && a.lvl_key) {
+          emitL = (uint32_t)L;
+          emitC = clastf;
+          emitB = cbase;
+        }
+        if (!wide) {
           // Compact the levels (run ends, descending close) into LDS by level index:
           //   lv[l] = cumulative volume through level l (exact u32 when sum(v) < 2^32; a
           //   larger day is not `fast`: its values come from the exact kernel),
@@ -935,6 +871,8 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
           // so level l has volume lv[l] - lv[l-1] and e_l - e_(l-1) bars, and everything
           // per level below runs over ceil(L/16) slots per lane (a lane's levels
           // contiguous) instead of the 16 sorted bars.
+          uint32_t* lv = reinterpret_cast<uint32_t*>(scr);
+          uint32_t* lc = lv + NBAR;  // L <= 240 levels
           uint32_t cum = gscan_excl_u(tv);
           int li = (int)gscan_excl_u((uint32_t)__builtin_popcount(endm));
 #pragma unroll
@@ -947,13 +885,6 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
             }
           }
           lds_fence();
-        }
-        if (!wide && a.lvl_key) {
-          emitL = (uint32_t)L;
-          emitC = clastf;
-          emitB = cbase;
-        }
-        if (!wide) {
           const uint32_t Sv = (uint32_t)sumv;
           const double inv = 1.0 / sumv;
           // level 0 (the highest close) is the member shift of the share moments
