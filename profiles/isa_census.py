@@ -8,7 +8,8 @@ instruction is attributed to the `.loc` line in effect; code inlined from a head
 line of the kernel's own file seen before it (its call site, in program order).
 sections.json: {"file": "csrc/mff_stage1g.hip", "sections": [[name, first, last], ...]}
 where first / last are line numbers or substrings of the source line that opens / closes
-the section (resolved against the source file, so edits do not shift the ranges); lines
+the section (resolved against the source file, so edits do not shift the ranges; with
+"ordered": true each opening marker is searched after the previous section's); lines
 outside every range count as "other".
 
 Output: per section, VALU in the blocks of each loop (LLVM's "Loop Header" annotations:
@@ -78,8 +79,10 @@ def main():
                 return i + 1
         raise SystemExit(f"marker not found: {x!r}")
     secs = []
+    prev = 0  # "ordered": each section's opening marker is searched after the previous one
     for name, a, b in cfg["sections"]:
-        la = resolve(a)
+        la = resolve(a, prev if cfg.get("ordered") else 0)
+        prev = la
         secs.append([name, la, resolve(b, la) if not isinstance(b, int) else b])
     cfg["sections"] = secs
 

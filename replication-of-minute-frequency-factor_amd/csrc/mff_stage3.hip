@@ -354,28 +354,33 @@ struct XrBucket {
   // level-1 bucket of an included value x (x canonical: no -0) and its position in the
   // bucket f in [0, 1] (monotone in x within the bucket)
   __device__ __forceinline__ uint32_t l1(double x, double& f) const {
+    return scheme == 0 ? l1s<0>(x, f) : l1s<1>(x, f);
+  }
+  template <int SCHEME>
+  __device__ __forceinline__ uint32_t l1s(double x, double& f) const {
     f = 0.0;
     if (x == -__builtin_inf()) return 0u;
     if (x == __builtin_inf()) return XB1 - 1;
-    if (scheme == 0) {
+    if constexpr (SCHEME == 0) {
       // halved operands: max - min cannot overflow; t >= 0 for x >= min
       const double t = (x * 0.5 - xmin_h) * scale;
       const double fl = floor(t);
       const int b = min((int)fl, XB1 - 3);
       f = t - (double)b;  // in [0, 1), or up to 2 in the clamped top bucket
       return 1u + (uint32_t)b;
+    } else {
+      constexpr uint32_t N1 = (XB1 - 4) / 2;  // buckets per sign
+      if (x == 0.0) return N1 + 1u;
+      const uint64_t m = (uint64_t)__double_as_longlong(fabs(x));
+      if (x < 0.0) {
+        const uint64_t q = m - nlo;
+        f = (double)((~q) & ((1ull << shn) - 1ull)) * ldexp(1.0, -shn);  // larger |x|: lower
+        return N1 - (uint32_t)(q >> shn);                                           // 1 .. N1
+      }
+      const uint64_t q = m - plo;
+      f = (double)(q & ((1ull << shp) - 1ull)) * ldexp(1.0, -shp);
+      return N1 + 2u + (uint32_t)(q >> shp);  // N1+2 .. 2 N1 + 1
     }
-    constexpr uint32_t N1 = (XB1 - 4) / 2;  // buckets per sign
-    if (x == 0.0) return N1 + 1u;
-    const uint64_t m = (uint64_t)__double_as_longlong(fabs(x));
-    if (x < 0.0) {
-      const uint64_t q = m - nlo;
-      f = (double)((~q) & ((1ull << shn) - 1ull)) * ldexp(1.0, -shn);  // larger |x|: lower
-      return N1 - (uint32_t)(q >> shn);                                           // 1 .. N1
-    }
-    const uint64_t q = m - plo;
-    f = (double)(q & ((1ull << shp) - 1ull)) * ldexp(1.0, -shp);
-    return N1 + 2u + (uint32_t)(q >> shp);  // N1+2 .. 2 N1 + 1
   }
   __device__ __forceinline__ uint32_t operator()(double x) const {
     double f;
@@ -716,6 +721,313 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
   }
 }
 
+// Single rank, S <= 5120 (the benchmark path): the bucketed rank of k_xs_rank_bucket
+// re-cut for fewer instructions per value and fewer barriers per (row, day).
+//  * 512 threads per (row, day) up to 2,048 stocks (two workgroups per CU), 1,024 above,
+//    at most 5 values per thread (128 VGPRs without spills);
+//  * the keys are the canonical doubles themselves (f64 compares, no total-order image);
+//    finite min / max as f64 min / max;
+//  * one counter per u32 (no packed halves); the level-1 bucket and its fraction are
+//    kept from the level-1 histogram for the level-2 one;
+//  * the reference / pack phases (two barriers) run only when some level-2 bucket holds
+//    more than XD_MAXO keys (known from the level-2 histogram's slots), and then only
+//    for those buckets; a bucket of at most XD_MAXO keys is scanned whole;
+//  * counters are cleared in phases that end in a barrier anyway, so a segment ends
+//    without one (the next segment's first barrier orders its rank phase before reuse).
+// Same ranks (exact, S6 average) and the same hand-over to k_xs_rank as
+// k_xs_rank_bucket (XD_MAXO non-reference keys in a bucket under both schemes).
+constexpr int XD_MAXO = 48;
+#ifndef MFF_XD_B2
+#define MFF_XD_B2 4096
+#endif
+constexpr int XD_B2 = MFF_XD_B2;  // level-2 buckets of the 1,024-thread instantiations
+
+// exclusive scan of W consecutive counters per thread (c -> offsets); returns the total.
+// A DPP wave scan, then the wave totals through LDS (one read per lane, a 16-lane DPP scan,
+// two lane reads).  Does not end synced (the callers write the offsets and pass a barrier
+// before wsum is written again).
+template <int T, int W>
+__device__ __forceinline__ uint32_t xd_scan(uint32_t (&c)[W], uint32_t* wsum) {
+  static_assert(T / 64 <= 16, "wave totals in one DPP row");
+  const int lane = (int)threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  uint32_t loc = 0u;
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    const uint32_t t = c[q];
+    c[q] = loc;
+    loc += t;
+  }
+  const uint32_t incl = wscan_dpp(loc);
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  const uint32_t pre = wscan16_dpp(lane < T / 64 ? wsum[lane] : 0u);
+  const uint32_t before = wave ? (uint32_t)__builtin_amdgcn_readlane((int)pre, wave - 1) : 0u;
+  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)pre, T / 64 - 1);
+  const uint32_t off = before + incl - loc;
+#pragma unroll
+  for (int q = 0; q < W; ++q) c[q] += off;
+  return tot;
+}
+
+template <int V>
+struct XdScheme {
+  static constexpr int value = V;
+};
+
+template <int XD_THREADS, int PER, int B2>
+__global__ __launch_bounds__(XD_THREADS) void k_xs_rank_day(const double* val, const uint8_t* state, int nseg,
+                                                            int S, double* out_val, uint8_t* out_state,
+                                                            uint32_t* list) {
+  constexpr int T = XD_THREADS;
+  constexpr int W1 = XB1 / T;  // level-1 counters per thread
+  constexpr int W2 = B2 / T;   // level-2 counters per thread
+  static_assert(XB1 % T == 0 && B2 % T == 0, "bucket counts per thread");
+  __shared__ double sk[PER * T];
+  __shared__ uint32_t tab[XB1];          // level-1 -> level-2 base | n << 16
+  __shared__ uint32_t h1[XB1];           // level-1 counts
+  __shared__ uint32_t st[B2 + 1];        // level-2 counts, then starts; st[B2] = total
+  __shared__ uint32_t ec[B2];            // full buckets: reference-equal keys | pack counter << 16
+  __shared__ unsigned long long mm[6];   // finite min / max (ord64), neg |x| bits min / max, pos bits min / max
+  __shared__ uint32_t wsum[T / 64];
+  __shared__ uint32_t ctl[2];            // [0] some bucket holds > XD_MAXO keys; [1] a full bucket fails
+  const int tid = (int)threadIdx.x, lane = tid & 63;
+  auto reset_mm = [&]() {
+    if (tid < 6) mm[tid] = (tid & 1) ? 0ull : ~0ull;
+  };
+  auto clear_h1 = [&]() {
+#pragma unroll
+    for (int q = 0; q < W1; ++q) h1[tid + q * T] = 0u;
+  };
+  auto clear_l2 = [&]() {  // st, ec, ctl
+#pragma unroll
+    for (int q = 0; q < W2; ++q) {
+      st[tid + q * T] = 0u;
+      ec[tid + q * T] = 0u;
+    }
+    if (tid < 2) ctl[tid] = 0u;
+  };
+  clear_h1();
+  clear_l2();
+  reset_mm();
+  __syncthreads();
+  for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    // segment pointers are wave-uniform (scalar base + the thread's 32-bit offset)
+    const size_t base = (size_t)seg * S;
+    const double* vseg = val + base;
+    const uint8_t* sseg = state + base;
+    double x[PER];
+    uint32_t inc = 0u, stv = 0u, stn = 0u;  // included; state VALUE; state NULL
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + j * T;
+      double v = 0.0;
+      uint32_t sb = MFF_STATE_ABSENT;
+      if (i < S) {
+        v = vseg[i];
+        sb = sseg[i];
+      }
+      const bool in = sb == MFF_STATE_VALUE && !__builtin_isnan(v);
+      x[j] = in && v != 0.0 ? v : 0.0;  // -0 -> +0; excluded -> 0
+      inc |= (uint32_t)in << j;
+      stv |= (uint32_t)(sb == MFF_STATE_VALUE) << j;
+      stn |= (uint32_t)(sb == MFF_STATE_NULL) << j;
+    }
+    // finite min / max (no NaN here: compares, DPP wave reduction)
+    {
+      double lo = __builtin_inf(), hi = -__builtin_inf();
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const bool use = ((inc >> j) & 1u) && __builtin_isfinite(x[j]);
+        lo = use && x[j] < lo ? x[j] : lo;
+        hi = use && x[j] > hi ? x[j] : hi;
+      }
+      wminmax_dpp(lo, hi);
+      if (lane == 0 && lo <= hi) {
+        atomicMin(&mm[0], (unsigned long long)ord64(lo));
+        atomicMax(&mm[1], (unsigned long long)ord64(hi));
+      }
+    }
+    __syncthreads();  // every thread is past the previous segment's rank phase
+    XrBucket bk;
+    const bool fin = mm[0] != ~0ull;
+    const double xmin = fin ? unord64(mm[0]) : 0.0;
+    const double xmax = fin ? unord64(mm[1]) : 0.0;
+    bk.xmin_h = xmin * 0.5;
+    const double range_h = xmax * 0.5 - bk.xmin_h;
+    bk.scale = range_h > 0.0 ? (double)(XB1 - 2) / range_h : 0.0;
+    bk.nlo = bk.plo = 0ull;
+    bk.shn = bk.shp = 0;
+    bk.tab = tab;
+    clear_l2();  // the previous segment's starts / tie counters (read before the barrier)
+    uint32_t bp[PER];   // level-1 bucket, then level-2 bucket << 16 | slot
+    float fr[PER];      // position in the level-1 bucket
+    uint32_t isref = 0u;
+    bool big = false;
+    // one attempt under a bucket scheme: the two histograms, the scatter and, when some
+    // bucket holds more than XD_MAXO keys, the reference / pack phases for those buckets;
+    // false: a full bucket keeps more than XD_MAXO non-reference keys
+    auto attempt = [&](auto scheme) -> bool {
+      constexpr int SCH = decltype(scheme)::value;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if ((inc >> j) & 1u) {
+          double f;
+          bp[j] = bk.template l1s<SCH>(x[j], f);
+          fr[j] = (float)f;  // monotone: equal keys, equal fractions; order kept
+          atomicAdd(&h1[bp[j]], 1u);
+        }
+      }
+      __syncthreads();
+      {  // level-2 bases
+        uint32_t c[W1], nb[W1];
+#pragma unroll
+        for (int q = 0; q < W1; ++q) {
+          const uint32_t h = h1[tid * W1 + q];
+          nb[q] = c[q] = h ? 1u + (h * (uint32_t)(B2 - XB1)) / (uint32_t)S : 0u;
+        }
+        xd_scan<T, W1>(c, wsum);
+#pragma unroll
+        for (int q = 0; q < W1; ++q) tab[tid * W1 + q] = c[q] | (nb[q] << 16);
+      }
+      __syncthreads();
+      // level 2: histogram (slots); h1 and mm are free again (read before the barrier)
+      clear_h1();
+      reset_mm();
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if ((inc >> j) & 1u) {
+          const uint32_t t = tab[bp[j]], n = t >> 16;
+          const uint32_t b = (t & 0xFFFFu) + min(n - 1u, (uint32_t)(fr[j] * (float)n));
+          const uint32_t slot = atomicAdd(&st[b], 1u);
+          if (slot == (uint32_t)XD_MAXO) ctl[0] = 1u;  // the bucket's key XD_MAXO + 1
+          bp[j] = (b << 16) | slot;
+        }
+      }
+      __syncthreads();
+      {
+        uint32_t c[W2];
+#pragma unroll
+        for (int q = 0; q < W2; ++q) c[q] = st[tid * W2 + q];
+        const uint32_t tot = xd_scan<T, W2>(c, wsum);
+#pragma unroll
+        for (int q = 0; q < W2; ++q) st[tid * W2 + q] = c[q];
+        if (tid == T - 1) st[B2] = tot;
+      }
+      __syncthreads();
+      big = ctl[0] != 0u;  // block-uniform
+      // scatter: the key at a bucket's slot 0 is its reference
+#pragma unroll
+      for (int j = 0; j < PER; ++j)
+        if ((inc >> j) & 1u) sk[st[bp[j] >> 16] + (bp[j] & 0xFFFFu)] = x[j];
+      __syncthreads();
+      isref = 0u;
+      if (!big) return true;
+      // buckets of more than XD_MAXO keys: count the reference-equal keys, then pack the
+      // others behind them (the reference stays at slot 0)
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if ((inc >> j) & 1u) {
+          const uint32_t b = bp[j] >> 16, s0 = st[b];
+          if (st[b + 1] - s0 > (uint32_t)XD_MAXO && sk[s0] == x[j]) {
+            isref |= 1u << j;
+            atomicAdd(&ec[b], 1u);
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        if (((inc & ~isref) >> j) & 1u) {
+          const uint32_t b = bp[j] >> 16, s0 = st[b], cnt = st[b + 1] - s0;
+          if (cnt > (uint32_t)XD_MAXO) {
+            const uint32_t old = atomicAdd(&ec[b], 1u << 16);
+            const uint32_t e = old & 0xFFFFu;
+            sk[s0 + e + (old >> 16)] = x[j];
+            if (cnt - e > (uint32_t)XD_MAXO) ctl[1] = 1u;
+          }
+        }
+      }
+      __syncthreads();
+      return ctl[1] == 0u;  // block-uniform
+    };
+    bool ok = false;
+    const bool lin = __builtin_isfinite(bk.scale);  // a range of a few denormals: log scheme only
+    if (lin) ok = attempt(XdScheme<0>{});
+    if (!ok) {
+      // log scheme: |x| bit ranges per sign (after a failed linear attempt every thread
+      // has read ctl before the counters are cleared)
+      if (lin) {
+        __syncthreads();
+        clear_l2();
+      }
+#pragma unroll 1
+      for (int q = 2; q < 6; ++q) {
+        const bool mx = q & 1;
+        uint64_t a = mx ? 0ull : ~0ull;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+          const double c = x[j];
+          const bool use = ((inc >> j) & 1u) && __builtin_isfinite(c) && (q < 4 ? c < 0.0 : c > 0.0);
+          const uint64_t k = (uint64_t)__double_as_longlong(fabs(c));
+          if (use) a = mx ? max(a, k) : min(a, k);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const uint64_t y = (uint64_t)__shfl_xor((long long)a, o, 64);
+          a = mx ? max(a, y) : min(a, y);
+        }
+        if (lane == 0) {
+          if (mx) atomicMax(&mm[q], (unsigned long long)a);
+          else atomicMin(&mm[q], (unsigned long long)a);
+        }
+      }
+      __syncthreads();
+      bk.nlo = mm[2];
+      bk.plo = mm[4];
+      constexpr uint32_t N1 = (XB1 - 4) / 2;
+      bk.shn = xr_shift(mm[2] == ~0ull ? 0ull : mm[3] - mm[2], N1);
+      bk.shp = xr_shift(mm[4] == ~0ull ? 0ull : mm[5] - mm[4], N1);
+      ok = attempt(XdScheme<1>{});
+    }
+    if (!ok) {  // hand the segment to the sorting kernel
+      if (tid == 0) list[1 + atomicAdd(&list[0], 1u)] = (uint32_t)seg;
+      continue;
+    }
+    double* ov = out_val + base;
+    uint8_t* os = out_state + base;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int s = tid + j * T;
+      if (s >= S) break;
+      const bool in = (inc >> j) & 1u, vl = (stv >> j) & 1u;
+      double r = vl ? qnan() : 0.0;
+      if (in) {
+        const double k = x[j];
+        const uint32_t b = bp[j] >> 16;
+        uint32_t q = st[b];
+        const uint32_t s1 = st[b + 1];
+        uint32_t less = q, eq = 0u;
+        if (big && s1 - q > (uint32_t)XD_MAXO) {
+          const uint32_t e = ec[b] & 0xFFFFu;
+          const double ref = sk[q];
+          less += ref < k ? e : 0u;
+          eq = ref == k ? e : 0u;
+          q += e;
+        }
+        for (; q < s1; ++q) {
+          const double y = sk[q];
+          less += y < k ? 1u : 0u;
+          eq += y == k ? 1u : 0u;
+        }
+        r = (double)less + (double)(eq + 1u) * 0.5;
+      }
+      ov[s] = r;
+      os[s] = vl ? MFF_STATE_VALUE : ((stn >> j) & 1u) ? MFF_STATE_NULL : MFF_STATE_ABSENT;
+    }
+  }
+}
+
 constexpr int XS_RANK_GRID = 2048;
 
 }  // namespace mff
@@ -802,6 +1114,23 @@ int mff_xs_rank(const double* val, const uint8_t* state, int rows, int D, int S_
     MFF_REQUIRE(nseg < (1ll << 32), "mff_xs_rank: too many segments");
     hipLaunchKernelGGL(k_xs_rank_list_init, dim3(1), dim3(1), 0, st, list);
     const int gb = (int)(nseg < 4 * XS_RANK_GRID ? nseg : 4 * XS_RANK_GRID);
+    // MFF_XS_RANK_IMPL=bucket: the 1,024-thread kernel for a single rank too (A/B timing)
+    if (R == 1 && M <= 5 * 1024 && !(impl && impl[0] == 'b')) {
+      // 512 threads (two workgroups per CU) up to 2,048 stocks, then 1,024 threads: at most
+      // 5 values per thread within 128 VGPRs
+      auto kd = M <= 1024 ? k_xs_rank_day<512, 2, XB2> : M <= 2048 ? k_xs_rank_day<512, 4, XB2>
+              : M <= 3072 ? k_xs_rank_day<1024, 3, XD_B2> : M <= 4096 ? k_xs_rank_day<1024, 4, XD_B2>
+              : k_xs_rank_day<1024, 5, XD_B2>;
+      const int td = M <= 2048 ? 512 : 1024;
+      MFF_REQUIRE(nseg < (1ll << 31), "mff_xs_rank: too many segments");
+      hipLaunchKernelGGL(kd, dim3(gb), dim3(td), 0, st, val, state, (int)nseg, S_loc, out_val, out_state,
+                         list);
+      MFF_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_xs_rank, dim3(g), dim3(SORT_THREADS), 0, st, val, state, rows, D, S_loc, val_all,
+                         state_all, R, S_all, out_val, out_state, sortws, (const uint32_t*)list);
+      MFF_LAUNCH_CHECK();
+      return 0;
+    }
     constexpr int thr = XR_THREADS;
     auto kern = R == 1 ? (M <= XR_PER_LO * thr ? k_xs_rank_bucket<XR_PER_LO, true, thr> : k_xs_rank_bucket<XR_PER, true, thr>)
                        : (M <= XR_PER_LO * thr ? k_xs_rank_bucket<XR_PER_LO, false, thr> : k_xs_rank_bucket<XR_PER, false, thr>);

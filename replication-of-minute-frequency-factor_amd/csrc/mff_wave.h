@@ -100,6 +100,57 @@ __device__ __forceinline__ uint32_t wsum_u32(uint32_t x) {
   return x;
 }
 
+// ---------------------------------------------------------------- DPP scans / reductions
+// GFX9 DPP: row_shr:1/2/4/8 inside each 16-lane row (Hillis-Steele), then row_bcast:15 into
+// rows 1 and 3 and row_bcast:31 into rows 2 and 3 -- one VALU op per step, no LDS.  Lanes
+// without a source (and rows outside the row mask) read `id`.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x, uint32_t id) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, CTRL, ROW_MASK, 0xF, false);
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double x, double id) {
+  const uint64_t b = dbits(x), i = dbits(id);
+  const uint32_t lo = dpp_u32<CTRL, ROW_MASK>((uint32_t)b, (uint32_t)i);
+  const uint32_t hi = dpp_u32<CTRL, ROW_MASK>((uint32_t)(b >> 32), (uint32_t)(i >> 32));
+  return bitsd(((uint64_t)hi << 32) | lo);
+}
+// inclusive prefix sum over the first 16 lanes (lanes >= 16: their row's prefix)
+__device__ __forceinline__ uint32_t wscan16_dpp(uint32_t x) {
+  x += dpp_u32<0x111, 0xF>(x, 0u);
+  x += dpp_u32<0x112, 0xF>(x, 0u);
+  x += dpp_u32<0x114, 0xF>(x, 0u);
+  x += dpp_u32<0x118, 0xF>(x, 0u);
+  return x;
+}
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ uint32_t wscan_dpp(uint32_t x) {
+  x = wscan16_dpp(x);
+  x += dpp_u32<0x142, 0xA>(x, 0u);
+  x += dpp_u32<0x143, 0xC>(x, 0u);
+  return x;
+}
+// wave min and max of non-NaN doubles, returned in every lane
+__device__ __forceinline__ void wminmax_dpp(double& lo, double& hi) {
+  const double pinf = __builtin_inf(), ninf = -__builtin_inf();
+#define MFF_MINMAX_STEP(C, R)                         \
+  {                                                   \
+    const double a = dpp_f64<C, R>(lo, pinf);         \
+    const double b = dpp_f64<C, R>(hi, ninf);         \
+    lo = a < lo ? a : lo;                             \
+    hi = b > hi ? b : hi;                             \
+  }
+  MFF_MINMAX_STEP(0x111, 0xF)
+  MFF_MINMAX_STEP(0x112, 0xF)
+  MFF_MINMAX_STEP(0x114, 0xF)
+  MFF_MINMAX_STEP(0x118, 0xF)
+  MFF_MINMAX_STEP(0x142, 0xA)
+  MFF_MINMAX_STEP(0x143, 0xC)
+#undef MFF_MINMAX_STEP
+  lo = rdlane(lo, 63);
+  hi = rdlane(hi, 63);
+}
+
 // ---------------------------------------------------------------- presence bits
 struct Bits {
   uint64_t b[4];

@@ -318,15 +318,20 @@ def test_stage3_live(dev, kind, S, ties):
     assert not bad, "\n".join(bad)
 
 
-@pytest.mark.parametrize("S", [5000, 8000])
-def test_stage3_rank_distributions(dev, S):
+@pytest.mark.parametrize("S,impl", [(300, ""), (1500, ""), (2500, ""), (3500, ""), (5000, ""), (5000, "bucket"),
+                                    (8000, "")])
+def test_stage3_rank_distributions(dev, S, impl, monkeypatch):
     """The bucketed rank on the distributions that defeat a one-level histogram: one
     dominant exact tie (1.0) among near values, two tie groups one ulp apart, a dense
     cluster with far outliers (lognormal sigma 6), a range of a few denormals, only
     infinities and zeros of both signs, integer-valued days (heavy ties everywhere), a
-    day of one value; S = 8000 runs the 8-per-thread instantiation."""
+    day of one value.  S <= 5120 runs k_xs_rank_day (each of its five instantiations:
+    512 x 2, 512 x 4, 1024 x 3 / 4 / 5), impl="bucket" the 1,024-thread k_xs_rank_bucket
+    at S = 5000, S = 8000 its 8-per-thread instantiation."""
     import mff_oracle as O
     from mff import engine
+    if impl:
+        monkeypatch.setenv("MFF_XS_RANK_IMPL", impl)
     rng = np.random.default_rng(S + 1)
     D = 8
     val = np.empty((D, S))
