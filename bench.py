@@ -217,7 +217,9 @@ def e2e_extras(panel, days: int):
         (parquet read + host encode + H2D + ingest kernel + stage-1 pass + long frames);
       * the other 57 factors one after another, as a notebook would (the batch result
         cache serves them: no re-read, no re-ingest);
-      * MinFreqFactor.cal_exposures_by_min_data() for all 58 from cold.
+      * MinFreqFactor.cal_exposures_by_min_data() for all 58 from cold, with the wall time
+        of each phase (mff._timing: parquet read / encode thread-seconds, read + encode +
+        H2D + ingest wall, stage-1 pass, D2H, to_long, merge).
     Rates are stock-days of the files per second of wall time, host work included."""
     import shutil
     import tempfile
@@ -225,7 +227,7 @@ def e2e_extras(panel, days: int):
     import pyarrow as pa
     import pyarrow.parquet as pq
     import torch
-    from mff import catalog, factor, factors, synth
+    from mff import _timing, catalog, factor, factors, synth
 
     S = panel.S
     nd = min(days, panel.D)
@@ -266,7 +268,8 @@ def e2e_extras(panel, days: int):
         t2 = time.perf_counter()
         factor.clear_result_cache()
         t3 = time.perf_counter()
-        allf = MinFreqFactor.cal_exposures_by_min_data(path=exp, folder_path=folder)
+        with _timing.collect() as phases:
+            allf = MinFreqFactor.cal_exposures_by_min_data(path=exp, folder_path=folder)
         t4 = time.perf_counter()
         factor.clear_result_cache()
         assert len(allf) == 58 and len(f.factor_exposure) > 0
@@ -278,10 +281,42 @@ def e2e_extras(panel, days: int):
             "e2e_58_sequential_stock_days_per_s": round(sd / (t2 - t0)),
             "e2e_58_one_call_s": round(t4 - t3, 3),
             "e2e_58_one_call_stock_days_per_s": round(sd / (t4 - t3)),
+            "e2e_58_one_call_phases_s": {k: round(v, 4) for k, v in phases.items()},
         })
         return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def final_exposure_extras(val, state, days: int = 250, name: str = "vol_return1min"):
+    """MinFreqFactor.cal_final_exposure(20, 'z', mode='days') (MF:187-240) on one
+    factor's exposure of S stocks x `days` days taken from the pass output, as the
+    reference user calls it: long frame in, long frame out (from_long, H2D + stage-2
+    kernel + D2H, to_long), wall time with the phases."""
+    import datetime as dt
+
+    from mff import _timing, catalog, factor, frames
+
+    i = catalog.ID[name]
+    nd = min(days, val.shape[1])
+    S = val.shape[2]
+    codes = [f"{s:06d}.SZ" for s in range(S)]
+    dates = [dt.date(2015, 1, 5) + dt.timedelta(days=k) for k in range(nd)]
+    ex = frames.to_long(val[i, :nd].cpu().numpy(), state[i, :nd].cpu().numpy(), codes, dates, name)
+    f = factor.MinFreqFactor(name, ex)
+    f.cal_final_exposure(20, "z", mode="days")  # warm: imports, allocator
+    ts, ph = [], None
+    for _ in range(3):
+        with _timing.collect() as p:
+            t = time.perf_counter()
+            out = f.cal_final_exposure(20, "z", mode="days")
+            ts.append(time.perf_counter() - t)
+        if ph is None or ts[-1] <= min(ts):
+            ph = dict(p)
+    assert len(out) == len(ex)
+    return {"final_exposure_days20_z_s": round(float(np.median(ts)), 4),
+            "final_exposure_sample": f"{name}: {S} stocks x {nd} days ({len(ex)} rows)",
+            "final_exposure_phases_s": {k: round(v, 4) for k, v in ph.items()}}
 
 
 def main():
@@ -415,6 +450,8 @@ def main():
         ms = timed(lambda: engine.cross_section(val, state, "rank", comm=comm, stocks_total=S), reps=3)
         extras["stage3_rank_all58_ms"] = round(ms, 3)
         extras["stage3_rank_GBps"] = round(xs_bytes / (ms * 1e-3) / 1e9, 1)
+        if rank == 0 and world == 1:
+            extras.update(final_exposure_extras(val, state))
         del val, state
         if rank == 0:
             extras.update(ingest_extras(panel, args.ingest_days, args.ingest_host_days))

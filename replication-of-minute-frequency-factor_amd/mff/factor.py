@@ -26,7 +26,7 @@ from typing import Literal, Optional
 
 import numpy as np
 
-from . import catalog, frames
+from . import _timing, catalog, frames
 
 _PV_PATH = os.environ.get("MFF_PV_PATH", r"D:\QuantData\Price_Volume.parquet")
 _EXPOSURE_DIR = os.environ.get("MFF_EXPOSURE_DIR", r"D:\QuantData\MinuteFreqFactor")
@@ -325,10 +325,11 @@ class MinFreqFactor(Factor):
         name = getattr(calculate_method, "_mff_factor", None)
         if isinstance(calculate_method, str):
             name = calculate_method[4:] if calculate_method.startswith("cal_") else calculate_method
-        valid = []
+        valid, gpu = [], False
         if files:
             if name is not None and name in catalog.ID:
                 valid = _gpu_batches(files, folder_path, [name], batch_days, device, strict)[name]
+                gpu = True
             else:
                 from joblib import Parallel, delayed
 
@@ -336,7 +337,7 @@ class MinFreqFactor(Factor):
                     delayed(self._process_single_file)(f, folder_path, calculate_method)
                     for f in files)
                 valid = [r for r in results if r is not None]
-        self.factor_exposure = _merge(factor_exposure, valid)
+        self.factor_exposure = _merge(factor_exposure, valid, presorted=gpu)
 
     @classmethod
     def cal_exposures_by_min_data(cls, calculate_methods=None, path: str = None,
@@ -368,7 +369,7 @@ class MinFreqFactor(Factor):
             res = _gpu_batches(list(files), folder_path, grp, batch_days, device, strict) if files else {}
             for nm in grp:
                 f, ex = out[nm]
-                f.factor_exposure = _merge(ex, res.get(nm, []))
+                f.factor_exposure = _merge(ex, res.get(nm, []), presorted=True)
         return {nm: out[nm][0] for nm in names}
 
     def cal_final_exposure(self, frequency, method: str, mode: str = "calendar", pool="full"):
@@ -411,13 +412,17 @@ class MinFreqFactor(Factor):
         from .factors import _device
 
         name = f"{self.factor_name}_{frequency}_{method}"
-        val, state, codes, dates = frames.from_long(self.factor_exposure, self.factor_name)
-        dev = _device(None)
-        v = torch.from_numpy(val[None]).to(dev)
-        s = torch.from_numpy(state[None]).to(dev)
-        ov, os_ = engine.rolling(v, s, frequency, method)
-        torch.cuda.synchronize(dev)
-        return frames.to_long(ov[0].cpu().numpy(), os_[0].cpu().numpy(), codes, dates, name)
+        with _timing.phase("from_long"):
+            val, state, codes, dates = frames.from_long(self.factor_exposure, self.factor_name)
+        with _timing.phase("H2D + stage 2 + D2H"):
+            dev = _device(None)
+            v = torch.from_numpy(val[None]).to(dev)
+            s = torch.from_numpy(state[None]).to(dev)
+            ov, os_ = engine.rolling(v, s, frequency, method)
+            torch.cuda.synchronize(dev)
+            ov, os_ = ov[0].cpu().numpy(), os_[0].cpu().numpy()
+        with _timing.phase("to_long"):
+            return frames.to_long(ov, os_, codes, dates, name)
 
 
 def _pending_files(folder_path, factor_exposure):
@@ -433,14 +438,30 @@ def _pending_files(folder_path, factor_exposure):
     return index["file_name"].tolist()
 
 
-def _merge(factor_exposure, valid):
-    """MF:97-110: old exposure + new rows, sorted [date, code]."""
+def _ordered(frames_):
+    """True if consecutive frames, each in (date, code) order (frames.to_long of the
+    sorted universes), hold strictly increasing dates: their concatenation is sorted."""
+    for a, b in zip(frames_, frames_[1:]):
+        if len(a) and len(b) and not a["date"].iloc[-1] < b["date"].iloc[0]:
+            return False
+    return True
+
+
+def _merge(factor_exposure, valid, presorted=False):
+    """MF:97-110: old exposure + new rows, sorted [date, code].  presorted: `valid` are
+    the GPU batches' frames (each already in (date, code) order), so without an old
+    exposure the sort is skipped when the batches' dates do not overlap."""
     pd = _pd()
-    if factor_exposure is None:
-        return _sort(pd.concat(valid, ignore_index=True)) if valid else None
-    if valid:
-        return _sort(pd.concat([factor_exposure] + valid, ignore_index=True))
-    return factor_exposure
+    with _timing.phase("merge + sort"):
+        if factor_exposure is None:
+            if not valid:
+                return None
+            if presorted and _ordered(valid):
+                return valid[0] if len(valid) == 1 else pd.concat(valid, ignore_index=True)
+            return _sort(pd.concat(valid, ignore_index=True))
+        if valid:
+            return _sort(pd.concat([factor_exposure] + valid, ignore_index=True))
+        return factor_exposure
 
 
 # ---------------------------------------------------------------- day-file batch results
@@ -526,10 +547,11 @@ def _gpu_batches(files, folder_path, names, batch_days, device, strict=False):
         if res is None:
             continue
         v, s, codes, dates = res
-        for nm in names:
-            i = catalog.ID[nm]
-            out[nm].append(frames.to_long(v[i], s[i], codes, dates, nm,
-                                          first="date" if nm == "shape_skratio" else "code"))
+        with _timing.phase("to_long"):
+            for nm in names:
+                i = catalog.ID[nm]
+                out[nm].append(frames.to_long(v[i], s[i], codes, dates, nm,
+                                              first="date" if nm == "shape_skratio" else "code"))
     return out
 
 

