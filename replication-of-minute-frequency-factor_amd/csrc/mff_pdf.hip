@@ -47,6 +47,14 @@ constexpr int PDF_CT = 1024;     // threads per count / finalize workgroup (<= 1
 // The one value every stock-day holds is 1.0 (c_last / c_last: the last close's level),
 // so its equal keys are counted apart, in a full u32.
 constexpr int PDF_LB = 21;
+// count: level-list entries per thread per chunk (8 or 16) and whether the next chunk is
+// loaded while this one is searched
+#ifndef MFF_PDF_UNR
+#define MFF_PDF_UNR 8
+#endif
+#ifndef MFF_PDF_PF
+#define MFF_PDF_PF 1
+#endif
 
 struct QLoader {
   const double* q;  // [R][5][D][S_loc]
@@ -141,45 +149,48 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, 
 // stock-days share e.g. the key 1.0 -- would otherwise deepen every search), build the
 // bucket table and the search depth.  Block-wide; ends synced.
 //   L[0] = Q[P0-1], L[1..nv] = distinct slice values > L[0], L[nv+1 .. nv+PDF_PAD] = ~0
-// C32 (the packed-counter slice): C is a u32 array too small for the compaction's
-// staging, so the distinct values are written straight into L from a second read of the
-// slice in global memory (L2-hot), and the counters zeroed as u32.
+// The slice is copied into L coalesced, then compacted in place: each thread's contiguous
+// chunk (at most PDF_SETUP_PER entries) goes through registers, and the scan's trailing
+// barrier orders every read before the first write.  The bucket table is filled by
+// scatter: distinct value i writes T[b] = i for the buckets between its predecessor's and
+// its own (T[b] = the first value whose bucket is >= b, i.e. lower_bound of the bucket's
+// lower edge), NBK + 1 writes in all instead of a binary search per bucket.
+constexpr int PDF_SETUP_PER = (PDF_ZQ32 + PDF_CT - 1) / PDF_CT;
+static_assert(PDF_ZQ <= PDF_ZQ32, "slice capacities");
 template <typename CT>
 __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, int P0, int P1,
                                                     uint64_t* L, CT* C, uint16_t* T,
                                                     uint32_t* wsum, int* occ_s) {
-  constexpr bool C32 = sizeof(CT) == 4;
   const int nq = P1 - P0;
-  if (!C32)
-    for (int i = threadIdx.x; i < nq; i += blockDim.x) L[1 + i] = Q[P0 + i];
+  for (int i = threadIdx.x; i < nq; i += blockDim.x) L[1 + i] = Q[P0 + i];
   const uint64_t L0 = P0 > 0 ? Q[P0 - 1] : 0ull;
   if (threadIdx.x == 0) {
     L[0] = L0;
     *occ_s = 0;
   }
   __syncthreads();
-  // compaction: a thread's contiguous chunk -> distinct values (into C, then back to L;
-  // C32: straight into L after the offsets are known)
-  const int per = (nq + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int per = (nq + (int)blockDim.x - 1) / (int)blockDim.x;  // <= PDF_SETUP_PER (blockDim = PDF_CT)
   const int i0 = min(nq, (int)threadIdx.x * per), i1 = min(nq, i0 + per);
-  auto at = [&](int i) { return C32 ? Q[P0 + i] : L[1 + i]; };  // slice element i (i >= -1)
-  uint32_t cnt = 0u;
-  for (int i = i0; i < i1; ++i) {
-    const uint64_t x = at(i), xp = i > 0 ? at(i - 1) : L0;
-    cnt += (x != ~0ull && x > L0 && x != xp) ? 1u : 0u;
-  }
-  uint32_t nu;
-  uint32_t off = block_excl_scan(cnt, wsum, &nu);
-  for (int i = i0; i < i1; ++i) {
-    const uint64_t x = at(i), xp = i > 0 ? at(i - 1) : L0;
-    if (x != ~0ull && x > L0 && x != xp) {
-      if (C32) L[1 + off++] = x;
-      else reinterpret_cast<uint64_t*>(C)[off++] = x;
+  uint64_t v[PDF_SETUP_PER];
+  uint32_t keep = 0u, cnt = 0u;
+#pragma unroll
+  for (int k = 0; k < PDF_SETUP_PER; ++k) {
+    const int i = i0 + k;
+    v[k] = 0ull;
+    if (i < i1) {
+      const uint64_t x = L[1 + i], xp = L[i];  // L[0] = Q[P0-1]
+      v[k] = x;
+      if (x != ~0ull && x > L0 && x != xp) {
+        keep |= 1u << k;
+        ++cnt;
+      }
     }
   }
-  __syncthreads();
-  if (!C32)
-    for (int i = threadIdx.x; i < (int)nu; i += blockDim.x) L[1 + i] = reinterpret_cast<uint64_t*>(C)[i];
+  uint32_t nu;
+  uint32_t off = block_excl_scan(cnt, wsum, &nu);  // ends synced: every read above is done
+#pragma unroll
+  for (int k = 0; k < PDF_SETUP_PER; ++k)
+    if ((keep >> k) & 1u) L[1 + off++] = v[k];
   for (int i = threadIdx.x; i < nq; i += blockDim.x) C[i] = (CT)0;
   if (threadIdx.x < PDF_PAD) L[1 + nu + threadIdx.x] = ~0ull;
   __syncthreads();
@@ -193,13 +204,11 @@ __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, in
   int sh = 0;
   while (sl.nv > 0 && ((sl.qmax - sl.qmin) >> sh) >= (uint64_t)PDF_NBK) ++sh;
   sl.sh = sh;
-  for (int b = threadIdx.x; b <= PDF_NBK; b += blockDim.x) {
-    int v = sl.nv;
-    if (sl.nv > 0 && b < PDF_NBK) {
-      const uint64_t edge = sl.qmin + ((uint64_t)b << sh);
-      v = (edge > sl.qmax || edge < sl.qmin) ? sl.nv : lower_bound_u64(L + 1, 0, sl.nv, edge);
-    }
-    T[b] = (uint16_t)v;
+  const uint64_t* L1 = L + 1;
+  for (int i = threadIdx.x; i <= sl.nv; i += blockDim.x) {
+    const int bi = i < sl.nv ? (int)((L1[i] - sl.qmin) >> sh) : PDF_NBK;
+    const int bp = i > 0 ? (int)((L1[i - 1] - sl.qmin) >> sh) : -1;
+    for (int b = bp + 1; b <= bi; ++b) T[b] = (uint16_t)i;
   }
   __syncthreads();
   int occ = 0;
@@ -309,25 +318,24 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
     // at most 6 steps the probes stay inside the PDF_PAD sentinels (probe <= nv + 2^steps
     // - 2), so the steps are unrolled with constant strides: j is a byte offset and each
     // probe is one ds_read_b64 with an immediate offset.
-    constexpr int UNR = 8;
+    constexpr int UNR = MFF_PDF_UNR;
     const uint64_t* L1 = L + 1;
-    const char* L1b = reinterpret_cast<const char*>(L1);
+    const char* Lb = reinterpret_cast<const char*>(L);
     const int nvc = sl.nv;
     const int n = (int)a.lvl_count[d];
     const uint64_t* K = a.lvl_key + (size_t)d * a.cap;
     const uint8_t* Wt = a.lvl_w + (size_t)d * a.cap;
     const int steps = sl.steps;
     const bool shallow = steps <= 6;
-    // software-pipelined: the next UNR entries are loaded before this UNR's searches.
-    // A thread takes UNR consecutive entries (chunk c = entries [UNR c, UNR c + UNR)): the
-    // keys as four 16-B loads and the bars as one 8-B load (a wave reads 4 KB of keys
+    // software-pipelined: the next UNR entries are loaded before this UNR's searches
+    // (two register sets, the loop unrolled twice: no copies between them).  A thread
+    // takes UNR consecutive entries (chunk c = entries [UNR c, UNR c + UNR)): the keys as
+    // four 16-B loads and the bars as one 8-B load (a wave reads 4 KB of keys
     // contiguously) instead of UNR strided key and byte loads.  Every day's list starts
     // 64-B aligned (pdf_levels_split: S x 240 entries per day), so the vector loads are
     // aligned; the last partial chunk loads entry by entry.
-    static_assert(UNR == 8, "chunk loads assume 8 entries");
-    uint64_t nkey[UNR];
-    uint32_t nw[UNR];
-    auto fetch = [&](int c) {
+    static_assert(UNR == 8 || UNR == 16, "chunk loads assume 8 or 16 entries");
+    auto fetch = [&](uint64_t (&nkey)[UNR], uint32_t (&nw)[UNR], int c) {
       const int i0 = c * UNR;
       if (i0 + UNR <= n) {
         const uint4* kp = reinterpret_cast<const uint4*>(K + i0);
@@ -337,9 +345,20 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
           nkey[2 * q] = (uint64_t)t.x | ((uint64_t)t.y << 32);
           nkey[2 * q + 1] = (uint64_t)t.z | ((uint64_t)t.w << 32);
         }
-        const uint2 w2 = *reinterpret_cast<const uint2*>(Wt + i0);
+        uint32_t wv[UNR / 4];
+        if constexpr (UNR == 8) {
+          const uint2 w2 = *reinterpret_cast<const uint2*>(Wt + i0);
+          wv[0] = w2.x;
+          wv[1] = w2.y;
+        } else {
+          const uint4 w4 = *reinterpret_cast<const uint4*>(Wt + i0);
+          wv[0] = w4.x;
+          wv[1] = w4.y;
+          wv[2] = w4.z;
+          wv[3] = w4.w;
+        }
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) nw[u] = ((u < 4 ? w2.x : w2.y) >> (8 * (u & 3))) & 0xFFu;
+        for (int u = 0; u < UNR; ++u) nw[u] = (wv[u >> 2] >> (8 * (u & 3))) & 0xFFu;
       } else {
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
@@ -350,46 +369,46 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
         }
       }
     };
-    const int nch = (n + UNR - 1) / UNR;
-    fetch((int)threadIdx.x);
-    for (int c0 = (int)threadIdx.x; c0 < nch; c0 += (int)blockDim.x) {
-      uint64_t key[UNR];
-      uint32_t w[UNR];
-      int j[UNR];  // byte offset of the probe base into L1 (shallow) or index (deep)
+    // p = the key's position among L[1..]: L1[p - 1] < key <= L1[p].  The search runs on
+    // the byte offset jb = 8 p' of the probe base p' (L[p'] < key), unsigned, so every probe
+    // is one ds_read_b64 at jb + an immediate offset; the bucket lookups of the UNR keys
+    // are issued together (no branch around them).
+    auto process = [&](const uint64_t (&key)[UNR], const uint32_t (&w)[UNR]) {
+      uint32_t jb[UNR];
       bool in[UNR];
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        key[u] = nkey[u];
-        w[u] = nw[u];
-      }
-      fetch(c0 + (int)blockDim.x);
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
         const bool bl = key[u] <= sl.L0;  // (padding entries have weight 0)
         in[u] = !bl && key[u] <= sl.qmax;
         below += bl ? w[u] : 0u;
         inw += in[u] ? w[u] : 0u;
-        const bool gtmin = key[u] > sl.qmin;
-        const int bk = (in[u] && gtmin) ? (int)((key[u] - sl.qmin) >> sl.sh) : 0;
-        j[u] = (in[u] && gtmin) ? (int)sl.T[bk] - 1 : -1;
+        const bool g = in[u] && key[u] > sl.qmin;
+        const uint32_t bk = g ? (uint32_t)((key[u] - sl.qmin) >> sl.sh) : 0u;
+        const uint32_t t = sl.T[bk];
+        jb[u] = g ? t << 3 : 0u;  // L[jb / 8] < key
       }
       if (shallow) {
+        // the probe base as an LDS pointer: each probe is base register + immediate
+        const char* pj[UNR];
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) j[u] *= 8;
+        for (int u = 0; u < UNR; ++u) pj[u] = Lb + jb[u];
 #pragma unroll
         for (int st = 5; st >= 0; --st) {
           if (st < steps) {
-            const int bb = 8 << st;
+            const uint32_t bb = 8u << st;
             uint64_t x[UNR];
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) x[u] = *reinterpret_cast<const uint64_t*>(L1b + j[u] + bb);
+            for (int u = 0; u < UNR; ++u) x[u] = *reinterpret_cast<const uint64_t*>(pj[u] + bb);
 #pragma unroll
-            for (int u = 0; u < UNR; ++u) j[u] += x[u] < key[u] ? bb : 0;
+            for (int u = 0; u < UNR; ++u) pj[u] += x[u] < key[u] ? bb : 0u;
           }
         }
 #pragma unroll
-        for (int u = 0; u < UNR; ++u) j[u] >>= 3;
+        for (int u = 0; u < UNR; ++u) jb[u] = (uint32_t)(pj[u] - Lb);
       } else {
+        int j[UNR];  // index into L1 of the probe base (-1: below L1[0])
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) j[u] = (int)(jb[u] >> 3) - 1;
         for (int bb = (1 << steps) >> 1; bb > 0; bb >>= 1) {
           uint64_t x[UNR];
 #pragma unroll
@@ -397,16 +416,40 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
 #pragma unroll
           for (int u = 0; u < UNR; ++u) j[u] = x[u] < key[u] ? j[u] + bb : j[u];
         }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) jb[u] = (uint32_t)(j[u] + 1) << 3;
       }
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const uint64_t x = L1[j[u] + 1];
+        const uint32_t pos = jb[u] >> 3;
+        const uint64_t x = *reinterpret_cast<const uint64_t*>(Lb + jb[u] + 8);  // L1[pos]
         if (in[u]) {
           if (C32 && x == key[u] && key[u] == K1) atomicAdd(one_s, w[u]);
-          else if (C32) atomicAdd(reinterpret_cast<uint32_t*>(&C[j[u] + 1]), x == key[u] ? (w[u] << PDF_LB) : w[u]);
-          else atomicAdd(reinterpret_cast<unsigned long long*>(&C[j[u] + 1]),
+          else if (C32) atomicAdd(reinterpret_cast<uint32_t*>(&C[pos]), x == key[u] ? (w[u] << PDF_LB) : w[u]);
+          else atomicAdd(reinterpret_cast<unsigned long long*>(&C[pos]),
                          x == key[u] ? ((uint64_t)w[u] << 32) : (uint64_t)w[u]);
         }
+      }
+    };
+    const int nch = (n + UNR - 1) / UNR;
+    const int stride = (int)blockDim.x;
+    uint64_t ka[UNR];
+    uint32_t wa[UNR];
+    if constexpr (MFF_PDF_PF) {
+      uint64_t kb[UNR];
+      uint32_t wb[UNR];
+      fetch(ka, wa, (int)threadIdx.x);
+      for (int c0 = (int)threadIdx.x; c0 < nch; c0 += 2 * stride) {
+        fetch(kb, wb, c0 + stride);
+        process(ka, wa);
+        if (c0 + stride >= nch) break;
+        fetch(ka, wa, c0 + 2 * stride);
+        process(kb, wb);
+      }
+    } else {  // no prefetch: the other waves hide a chunk's loads
+      for (int c0 = (int)threadIdx.x; c0 < nch; c0 += stride) {
+        fetch(ka, wa, c0);
+        process(ka, wa);
       }
     }
     below = (uint32_t)__reduce_add_sync(~0ull, (int)below);
@@ -448,20 +491,34 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
   if (FUSED) {
     // own queries [5][D][S] of day d that fall in this slice -> rank (S6 average)
     if (sl.nv > 0) {
+      // RB queries per thread in flight: their loads issued together, then searched
       const size_t plane = (size_t)a.D * S;
-      for (int i = threadIdx.x; i < 5 * S; i += blockDim.x) {
-        const int t = i / S, s = i - t * S;
-        if (a.rows[t] < 0) continue;
-        const double q = a.q_local[(size_t)t * plane + (size_t)d * S + s];
-        if (__builtin_isnan(q)) continue;  // no level passed (null) or absent stock-day
-        const uint64_t key = ord64(q);
-        if (key <= sl.L0 || key > sl.qmax) continue;  // another slice owns its first copy
-        int lo, hi;
-        sl.range(key, lo, hi);
-        const uint32_t c2 = twice_rank(lower_bound_u64(sl.L + 1, lo, hi, key));
-        const size_t o = (size_t)a.rows[t] * plane + (size_t)d * S + s;
-        a.val[o] = ((double)c2 + 1.0) * 0.5;
-        a.state[o] = MFF_STATE_VALUE;
+      constexpr int RB = 4;
+      const int nqd = 5 * S, bd = (int)blockDim.x;
+      for (int i0 = threadIdx.x; i0 < nqd; i0 += RB * bd) {
+        double q[RB];
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+          const int i = i0 + k * bd;
+          q[k] = __builtin_nan("");
+          if (i < nqd) {
+            const int t = i / S, s = i - t * S;
+            if (a.rows[t] >= 0) q[k] = a.q_local[(size_t)t * plane + (size_t)d * S + s];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+          if (__builtin_isnan(q[k])) continue;  // no level passed (null), absent, or no row
+          const uint64_t key = ord64(q[k]);
+          if (key <= sl.L0 || key > sl.qmax) continue;  // another slice owns its first copy
+          const int i = i0 + k * bd, t = i / S, s = i - t * S;
+          int lo, hi;
+          sl.range(key, lo, hi);
+          const uint32_t c2 = twice_rank(lower_bound_u64(sl.L + 1, lo, hi, key));
+          const size_t o = (size_t)a.rows[t] * plane + (size_t)d * S + s;
+          a.val[o] = ((double)c2 + 1.0) * 0.5;
+          a.state[o] = MFF_STATE_VALUE;
+        }
       }
     }
   } else {
