@@ -97,9 +97,13 @@ int mff_ingest_rows(const int32_t* stock, const int32_t* day, const int64_t* tim
  * pdf_query: float64 [5][D][S] workspace, required when any doc_pdf* id is requested
  * (the doc_pdf values are then produced by mff_pdf_* below), else may be NULL.
  * pdf_levels: mff_pdf_levels_bytes(S, D) bytes, required with doc_pdf (else NULL): per
- * day, the flat list of every stock-day's price levels as (key c_last/c_level, total-
- * order u64; bars at the level, u8) that mff_pdf_count / mff_pdf_rank_local bin against
- * the sorted queries (filled and counted by the call itself).
+ * day, every stock-day's price levels as (key c_last/c_level, total-order u64; bars at
+ * the level, u8) that mff_pdf_count / mff_pdf_rank_local bin against the sorted queries
+ * (filled and counted by the call itself), in two lists split at a key the library sets
+ * per call (the mean median doc_pdf query of earlier calls on the device; 1.0 before
+ * any: any key gives the same ranks): the keys below it from the front of the day's
+ * S*240 slots, the others from the back, with the per-day counts (u32 pairs A, B = one
+ * u64 counter per day) and the split key u64 in front.
  * workspace: mff_stage1_workspace_bytes(S, D) bytes of device scratch (the list of
  * stock-days the exact general path finishes; zeroed by the call itself).
  * Environment MFF_STAGE1_IMPL=w64 selects the wave-per-stock-day kernel for everything.

@@ -37,6 +37,17 @@ void clear_error();
     }                                                                        \
   } while (0)
 
+// doc_pdf level buffer header (pdf_levels_split in mff_stage1g.hip): per day a u64
+// counter (list A count low, list B high), then the u64 split key of this pass's lists
+// at pdf_koff(D) (keys below it in list A)
+__host__ __device__ inline size_t pdf_koff(int D) { return (size_t)8 * (size_t)D; }
+__device__ inline uint64_t pdf_split_key(const uint32_t* lvl_count, int D) {
+  return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(lvl_count) + pdf_koff(D));
+}
+// sets this pass's split key in the header (mff_pdf.hip): the key learned from the
+// previous passes' doc_pdf queries (their per-day median), 1.0 before any
+int pdf_split_init(uint32_t* lvl_count, int D, hipStream_t st);
+
 // factor families (the kernel section that computes a factor); bit per family
 enum Fam : uint32_t {
   F_SEG = 1u << 0,

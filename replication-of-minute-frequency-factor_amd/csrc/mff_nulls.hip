@@ -628,24 +628,44 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
       const Bits LE = ballot4(emit);
       const int Lc = count(LE);
       if (Lc > 0) {
-        const uint64_t lt = (1ull << lane) - 1ull;
-        uint32_t idx = 0u;
+        // two lists (pdf_levels_split): A the keys below the pass's split key, B the
+        // others
+        const uint64_t ksplit = pdf_split_key(a.lvl_count, a.D);
+        uint64_t lkey[4];
+        bool inA[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) idx += (uint32_t)__popcll(LE.b[k] & lt);
-        uint32_t base = 0u;
-        if (lane == 0) base = atomicAdd(a.lvl_count + d, (uint32_t)Lc);
-        idx += (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        for (int k = 0; k < 4; ++k) {
+          lkey[k] = ord64(cl / (double)bitsf(~hi[k]));
+          inA[k] = emit[k] && lkey[k] < ksplit;
+        }
+        const Bits AE = ballot4(inA);
+        const int LA = count(AE);
+        const uint64_t lt = (1ull << lane) - 1ull;
+        uint32_t idxA = 0u, idxL = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          idxA += (uint32_t)__popcll(AE.b[k] & lt);
+          idxL += (uint32_t)__popcll(LE.b[k] & lt);
+        }
+        uint32_t idxB = idxL - idxA;
         double pos[4] = {(double)l4, (double)(l4 + 1), (double)(l4 + 2), (double)(l4 + 3)};
         double ppos[4];
         bool hpp[4];
         prev_valid(pos, lend, ppos, hpp);
+        uint64_t base = 0ull;  // one u64 counter per day: list A count low, list B high
+        if (lane == 0) {
+          base = atomicAdd(reinterpret_cast<unsigned long long*>(a.lvl_count) + d,
+                           (unsigned long long)((uint64_t)(uint32_t)LA | ((uint64_t)(uint32_t)(Lc - LA) << 32)));
+        }
+        idxA += (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base);
+        idxB += (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(base >> 32));
         const size_t cap = (size_t)a.S * NBAR;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (emit[k]) {
-            a.lvl_key[(size_t)d * cap + idx] = ord64(cl / (double)bitsf(~hi[k]));
-            a.lvl_w[(size_t)d * cap + idx] = (uint8_t)(l4 + k - (hpp[k] ? (int)ppos[k] : -1));
-            ++idx;
+            const size_t at = inA[k] ? (size_t)idxA++ : cap - 1 - (size_t)idxB++;
+            a.lvl_key[(size_t)d * cap + at] = lkey[k];
+            a.lvl_w[(size_t)d * cap + at] = (uint8_t)(l4 + k - (hpp[k] ? (int)ppos[k] : -1));
           }
       }
       // threshold level for p = k/20 (CM:1022-1026, C2 / C8): the first level whose

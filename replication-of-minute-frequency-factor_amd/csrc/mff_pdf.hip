@@ -24,6 +24,8 @@
 
 #include <type_traits>
 
+#include <mutex>
+
 #include "../../include/mff.h"
 #include "mff_internal.h"
 #include "mff_sort.h"
@@ -34,11 +36,32 @@ namespace mff {
 
 size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w);  // mff_stage1g.hip
 
-constexpr int PDF_MAXM = 1 << 24;  // queries per day (all ranks): 2 n_less + n_eq stays in u32
+constexpr int PDF_MAXM = 1 << 24;
+// The level lists are split at a key chosen per pass (pdf_split_init: the mean of the
+// previous passes' per-day median queries; ord64(1.0) before any), stored in the level
+// buffer's header: stage 1 writes the keys below it into list A, the others into list B.
+constexpr uint64_t PDF_KSPLIT0 = 0xBFF0000000000000ull;  // ord64(1.0)
+// slice capacity of the split-aligned count (LDS: 12 B per query + the bucket table,
+// within 160 KiB): two slices cover 25,800 queries, a day of 5,160 stocks
+constexpr int PDF_KCAP = 12900;
+// learned split key, one per device: sum / count of the per-day medians seen since the
+// last pass start, and the key in use
+struct PdfLearn {
+  double sum;
+  uint32_t n;
+  uint32_t pad;
+  uint64_t key;
+};  // queries per day (all ranks): 2 n_less + n_eq stays in u32
 constexpr int PDF_ZQ = 9160;     // sorted queries per workgroup, u64 counters (LDS: 16 B each)
-constexpr int PDF_ZQ32 = 12500;  // sorted queries per count workgroup, packed u32 counters (12 B)
+#ifndef MFF_PDF_ZQ32
+#define MFF_PDF_ZQ32 12500
+#endif
+#ifndef MFF_PDF_NBK
+#define MFF_PDF_NBK 4096
+#endif
+constexpr int PDF_ZQ32 = MFF_PDF_ZQ32;  // sorted queries per count workgroup, packed u32 counters (12 B)
 constexpr int PDF_PAD = 64;      // ~0 sentinels after the slice's distinct values
-constexpr int PDF_NBK = 4096;    // bucket table over the workgroup's distinct query values
+constexpr int PDF_NBK = MFF_PDF_NBK;  // bucket table over the workgroup's distinct query values
 constexpr int PDF_CT = 1024;     // threads per count / finalize workgroup (<= 1024: wsum[16])
 // packed counter: n_less part in the low PDF_LB bits, n_eq part above.  Exact while a
 // slice's total weight stays below 2^PDF_LB (240 bars x S_loc < 2^21: S_loc <= 8738) and
@@ -123,6 +146,25 @@ struct PdfSlice {
   }
 };
 
+// lower_bound of key in the sorted Q[0, M), by one wave: 64 probes per round (every
+// lane of the wave calls it and gets the result)
+__device__ __forceinline__ int wave_lower_bound(const uint64_t* Q, int M, uint64_t key) {
+  const int lane = lane_id();
+  int lo = 0, hi = M;  // the answer is in [lo, hi]
+  while (hi - lo > 64) {
+    const int step = (hi - lo + 63) / 64;
+    const int p = lo + (lane + 1) * step - 1;
+    const bool less = p < hi && Q[p] < key;
+    const int c = __popcll(__ballot(less));  // Q sorted: the lanes below c are less
+    const int nlo = lo + c * step;
+    hi = min(hi, lo + (c + 1) * step);
+    lo = nlo;
+  }
+  const int p = lo + lane;
+  const bool less = p < hi && Q[p] < key;
+  return lo + __popcll(__ballot(less));
+}
+
 // block-wide exclusive scan of one u32 per thread (wsum: 16 words of LDS); returns the
 // thread's offset, *total = the block sum.  Ends synced.
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, uint32_t* total) {
@@ -155,15 +197,18 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, 
 // scatter: distinct value i writes T[b] = i for the buckets between its predecessor's and
 // its own (T[b] = the first value whose bucket is >= b, i.e. lower_bound of the bucket's
 // lower edge), NBK + 1 writes in all instead of a binary search per bucket.
-constexpr int PDF_SETUP_PER = (PDF_ZQ32 + PDF_CT - 1) / PDF_CT;
-static_assert(PDF_ZQ <= PDF_ZQ32, "slice capacities");
+constexpr int PDF_SETUP_MAXQ = PDF_ZQ32 > PDF_ZQ ? (PDF_ZQ32 > PDF_KCAP ? PDF_ZQ32 : PDF_KCAP) : (PDF_ZQ > PDF_KCAP ? PDF_ZQ : PDF_KCAP);
+constexpr int PDF_SETUP_PER = (PDF_SETUP_MAXQ + PDF_CT - 1) / PDF_CT;
 template <typename CT>
 __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, int P0, int P1,
                                                     uint64_t* L, CT* C, uint16_t* T,
-                                                    uint32_t* wsum, int* occ_s) {
+                                                    uint32_t* wsum, int* occ_s, uint64_t lo_floor = 0ull) {
   const int nq = P1 - P0;
   for (int i = threadIdx.x; i < nq; i += blockDim.x) L[1 + i] = Q[P0 + i];
-  const uint64_t L0 = P0 > 0 ? Q[P0 - 1] : 0ull;
+  // lo_floor: a slice whose queries are all >= the split key counts every key below it
+  // as `below` (L0 = split key - 1), so it need not read the list those keys are in
+  const uint64_t Lq = P0 > 0 ? Q[P0 - 1] : 0ull;
+  const uint64_t L0 = Lq > lo_floor ? Lq : lo_floor;  // (no max(): it may go through double)
   if (threadIdx.x == 0) {
     L[0] = L0;
     *occ_s = 0;
@@ -280,6 +325,8 @@ struct PdfArgs {
   int rows[5];
   int S, D, d0, nd, M, Z, Mz;
   int packed;  // count: u32 packed counters (PDF_LB), u64 recount on overflow
+  int kslice;  // fused count: slices aligned at the split key (each reads one level list)
+  PdfLearn* learn;  // kslice: the learned split key's state (k_pdf_learn, after the count)
   int frame;   // count: ONE sorted list [M] for every day (a multi-date frame ranked
                // frame-wide, CM:1015-1017); each day's words are atomically added to counts[M]
 };
@@ -290,7 +337,8 @@ struct PdfArgs {
 template <bool FUSED, bool C32>
 __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd, int P0, int P1, int mz,
                                                 unsigned char* smem, uint32_t* wsum, uint32_t* below_s,
-                                                uint32_t* inw_s, uint32_t* one_s, int* occ_s) {
+                                                uint32_t* inw_s, uint32_t* one_s, int* occ_s,
+                                                uint64_t lo_floor) {
   constexpr uint64_t K1 = 0xBFF0000000000000ull;  // ord64(1.0)
   typedef typename std::conditional<C32, uint32_t, uint64_t>::type CT;
   const int S = a.S;
@@ -305,10 +353,35 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
     *inw_s = 0u;
     *one_s = 0u;
   }
-  const PdfSlice sl = pdf_slice_setup(Q, a.M, P0, P1, L, C, T, wsum, occ_s);
+  const PdfSlice sl = pdf_slice_setup(Q, a.M, P0, P1, L, C, T, wsum, occ_s, lo_floor);
 
   uint32_t below = 0u, inw = 0u;
   if (sl.nv > 0) {
+    // The day's levels are two lists split at the pass's key (stage 1 writes keys below
+    // it from the front of the day's region, the others from its back): a slice reads
+    // list A only if some of its keys can exceed L0, list B only if the slice reaches the
+    // split key; list A skipped counts as `below` by its bars (its weight bytes only).
+    const int nA = (int)a.lvl_count[2 * d], nB = (int)a.lvl_count[2 * d + 1];
+    const uint64_t ksplit = pdf_split_key(a.lvl_count, a.D);
+    const bool readA = sl.L0 < ksplit - 1ull, readB = sl.qmax >= ksplit;
+    if (!readA) {
+      // every list-A key is below this slice: their bars, from list A's weight bytes
+      // (1 B per entry, 16 per load; the day's slots start 64-B aligned)
+      const uint8_t* WA = a.lvl_w + (size_t)d * a.cap;
+      for (int i = 16 * (int)threadIdx.x; i < nA; i += 16 * (int)blockDim.x) {
+        if (i + 16 <= nA) {
+          const uint4 q = *reinterpret_cast<const uint4*>(WA + i);
+          const uint32_t wq[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t h = (wq[k] & 0x00FF00FFu) + ((wq[k] >> 8) & 0x00FF00FFu);
+            below += (h & 0xFFFFu) + (h >> 16);
+          }
+        } else {
+          for (int k = i; k < nA; ++k) below += WA[k];
+        }
+      }
+    }
     // The day's level list is flat (stage 1 appends every stock-day's levels: key =
     // c_last / c as ord64, weight = bars at the level), so a thread simply takes every
     // blockDim-th entry, UNR at a time (their loads in flight together, their searches
@@ -322,7 +395,6 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
     const uint64_t* L1 = L + 1;
     const char* Lb = reinterpret_cast<const char*>(L);
     const int nvc = sl.nv;
-    const int n = (int)a.lvl_count[d];
     const uint64_t* K = a.lvl_key + (size_t)d * a.cap;
     const uint8_t* Wt = a.lvl_w + (size_t)d * a.cap;
     const int steps = sl.steps;
@@ -335,9 +407,10 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
     // 64-B aligned (pdf_levels_split: S x 240 entries per day), so the vector loads are
     // aligned; the last partial chunk loads entry by entry.
     static_assert(UNR == 8 || UNR == 16, "chunk loads assume 8 or 16 entries");
+    int s = 0, e = 0, s8 = 0;  // the list being read: entries [s, e), chunks from s8 = s rounded down
     auto fetch = [&](uint64_t (&nkey)[UNR], uint32_t (&nw)[UNR], int c) {
-      const int i0 = c * UNR;
-      if (i0 + UNR <= n) {
+      const int i0 = s8 + c * UNR;
+      if (i0 >= s && i0 + UNR <= e) {
         const uint4* kp = reinterpret_cast<const uint4*>(K + i0);
 #pragma unroll
         for (int q = 0; q < UNR / 2; ++q) {
@@ -363,7 +436,7 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
 #pragma unroll
         for (int u = 0; u < UNR; ++u) {
           const int i = i0 + u;
-          const bool v = i < n;
+          const bool v = i >= s && i < e;
           nkey[u] = v ? K[i] : 0ull;
           nw[u] = v ? (uint32_t)Wt[i] : 0u;
         }
@@ -431,25 +504,31 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
         }
       }
     };
-    const int nch = (n + UNR - 1) / UNR;
     const int stride = (int)blockDim.x;
-    uint64_t ka[UNR];
-    uint32_t wa[UNR];
-    if constexpr (MFF_PDF_PF) {
-      uint64_t kb[UNR];
-      uint32_t wb[UNR];
-      fetch(ka, wa, (int)threadIdx.x);
-      for (int c0 = (int)threadIdx.x; c0 < nch; c0 += 2 * stride) {
-        fetch(kb, wb, c0 + stride);
-        process(ka, wa);
-        if (c0 + stride >= nch) break;
-        fetch(ka, wa, c0 + 2 * stride);
-        process(kb, wb);
-      }
-    } else {  // no prefetch: the other waves hide a chunk's loads
-      for (int c0 = (int)threadIdx.x; c0 < nch; c0 += stride) {
-        fetch(ka, wa, c0);
-        process(ka, wa);
+    for (int list = 0; list < 2; ++list) {
+      if (list == 0 ? !readA : !readB) continue;
+      s = list == 0 ? 0 : (int)a.cap - nB;
+      e = list == 0 ? nA : (int)a.cap;
+      s8 = s & ~(UNR - 1);  // 64-B aligned chunks (every day's region starts 64-B aligned)
+      const int nch = (e - s8 + UNR - 1) / UNR;
+      uint64_t ka[UNR];
+      uint32_t wa[UNR];
+      if constexpr (MFF_PDF_PF) {
+        uint64_t kb[UNR];
+        uint32_t wb[UNR];
+        fetch(ka, wa, (int)threadIdx.x);
+        for (int c0 = (int)threadIdx.x; c0 < nch; c0 += 2 * stride) {
+          fetch(kb, wb, c0 + stride);
+          process(ka, wa);
+          if (c0 + stride >= nch) break;
+          fetch(ka, wa, c0 + 2 * stride);
+          process(kb, wb);
+        }
+      } else {  // no prefetch: the other waves hide a chunk's loads
+        for (int c0 = (int)threadIdx.x; c0 < nch; c0 += stride) {
+          fetch(ka, wa, c0);
+          process(ka, wa);
+        }
       }
     }
     below = (uint32_t)__reduce_add_sync(~0ull, (int)below);
@@ -565,16 +644,45 @@ __global__ __launch_bounds__(PDF_CT) void k_pdf_count(PdfArgs a) {
   const int dd = lid / a.Z, z = lid % a.Z;
   if (dd >= a.nd) return;
   const int d = a.d0 + dd;
-  const int P0 = z * a.Mz, P1 = min(a.M, P0 + a.Mz);
+  int P0 = z * a.Mz, P1 = min(a.M, P0 + a.Mz);
+  uint64_t lo_floor = 0ull;
+  if (a.kslice) {
+    // the queries below the split key [0, PK) and the others [PK, M), each cut into equal
+    // slices of at most Mz: a slice then reads one of the day's two level lists
+    __shared__ int pk_s;
+    const uint64_t ksplit = pdf_split_key(a.lvl_count, a.D);
+    if (threadIdx.x < 64) {
+      const int pk = wave_lower_bound(a.q_sorted + (size_t)dd * a.M, a.M, ksplit);
+      if (threadIdx.x == 0) pk_s = pk;
+    }
+    __syncthreads();
+    const int PK = pk_s;
+    const int zA = (PK + a.Mz - 1) / a.Mz, zB = (a.M - PK + a.Mz - 1) / a.Mz;
+    if (z >= zA + zB) return;  // block-uniform
+    if (z < zA) {
+      const int len = (PK + zA - 1) / zA;
+      P0 = z * len;
+      P1 = min(PK, P0 + len);
+    } else {
+      const int len = (a.M - PK + zB - 1) / zB;
+      P0 = PK + (z - zA) * len;
+      P1 = min(a.M, P0 + len);
+      lo_floor = ksplit - 1ull;
+    }
+  }
   if (a.packed) {
-    if (!pdf_count_slice<FUSED, true>(a, d, dd, P0, P1, a.Mz, smem, wsum, &below_s, &inw_s, &one_s, &occ_s)) {
+    if (!pdf_count_slice<FUSED, true>(a, d, dd, P0, P1, a.Mz, smem, wsum, &below_s, &inw_s, &one_s, &occ_s,
+                                      lo_floor)) {
       __syncthreads();
       const int mid = P0 + (P1 - P0 + 1) / 2;
-      pdf_count_slice<FUSED, false>(a, d, dd, P0, mid, mid - P0, smem, wsum, &below_s, &inw_s, &one_s, &occ_s);
-      pdf_count_slice<FUSED, false>(a, d, dd, mid, P1, P1 - mid, smem, wsum, &below_s, &inw_s, &one_s, &occ_s);
+      pdf_count_slice<FUSED, false>(a, d, dd, P0, mid, mid - P0, smem, wsum, &below_s, &inw_s, &one_s, &occ_s,
+                                    lo_floor);
+      pdf_count_slice<FUSED, false>(a, d, dd, mid, P1, P1 - mid, smem, wsum, &below_s, &inw_s, &one_s, &occ_s,
+                                    lo_floor);
     }
   } else {
-    pdf_count_slice<FUSED, false>(a, d, dd, P0, P1, a.Mz, smem, wsum, &below_s, &inw_s, &one_s, &occ_s);
+    pdf_count_slice<FUSED, false>(a, d, dd, P0, P1, a.Mz, smem, wsum, &below_s, &inw_s, &one_s, &occ_s,
+                                  lo_floor);
   }
 }
 
@@ -651,6 +759,59 @@ __global__ __launch_bounds__(256) void k_pdf_finalize_own(const double* q, const
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// the learned split key (per device, allocated on first use and cleared on the stream)
+static PdfLearn* g_learn[64];
+static std::mutex g_learn_mu;
+static PdfLearn* pdf_learn_state(hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("pdf_learn_state: no device");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(g_learn_mu);
+  if (!g_learn[dev]) {
+    PdfLearn* p = nullptr;
+    if (hipMalloc(&p, sizeof(PdfLearn)) != hipSuccess || hipMemsetAsync(p, 0, sizeof(PdfLearn), st) != hipSuccess) {
+      set_error("pdf_learn_state: allocation failed");
+      return nullptr;
+    }
+    g_learn[dev] = p;
+  }
+  return g_learn[dev];
+}
+
+// every 16th day of the call: its median query (as a ratio) into the learned key's sum
+// (one wave per sampled day, after the count)
+__global__ __launch_bounds__(64) void k_pdf_learn(const uint64_t* q_sorted, int M, PdfLearn* s) {
+  const uint64_t* Qd = q_sorted + (size_t)blockIdx.x * 16 * M;
+  const int nvalid = wave_lower_bound(Qd, M, ~0ull);  // NaN queries sort last
+  if (nvalid > 0 && threadIdx.x == 0) {
+    atomicAdd(&s->sum, unord64(Qd[(nvalid - 1) / 2]));
+    atomicAdd(&s->n, 1u);
+  }
+}
+
+// one thread: this pass's split key = the mean of the medians gathered since the last
+// pass start (as a ratio, then its key), or the key in use, or 1.0 before any
+__global__ void k_pdf_split_init(PdfLearn* s, uint64_t* hdr_key) {
+  if (s->key == 0ull) s->key = PDF_KSPLIT0;
+  if (s->n != 0u) {
+    s->key = ord64(s->sum / (double)s->n);
+    s->sum = 0.0;
+    s->n = 0u;
+  }
+  *hdr_key = s->key;
+}
+
+int pdf_split_init(uint32_t* lvl_count, int D, hipStream_t st) {
+  PdfLearn* s = pdf_learn_state(st);
+  if (!s) return -2;
+  uint64_t* hdr = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(lvl_count) + pdf_koff(D));
+  hipLaunchKernelGGL(k_pdf_split_init, dim3(1), dim3(1), 0, st, s, hdr);
+  MFF_LAUNCH_CHECK();
+  return 0;
+}
+
 }  // namespace mff
 
 using namespace mff;
@@ -688,6 +849,17 @@ static int pdf_launch(PdfArgs& a, const uint64_t* q_sorted, int M, hipStream_t s
   // this rank) fits the n_less field
   a.packed = mode != 2 && (long long)NBAR * a.S < (1ll << PDF_LB) && getenv("MFF_PDF_U64") == nullptr;
   pdf_slices(M, a.Z, a.Mz, lds, a.packed);
+  // one rank, one day per sorted list: slices aligned at PDF_KSPLIT (one more slot per day
+  // for the split; MFF_PDF_KSLICE=0 keeps the plain position slices, A/B timing)
+  const char* ks = getenv("MFF_PDF_KSLICE");
+  a.kslice = mode == 1 && a.packed && !a.frame && !(ks && ks[0] == '0');
+  if (a.kslice) {
+    a.learn = pdf_learn_state(st);
+    if (!a.learn) return -2;
+    a.Mz = PDF_KCAP;
+    a.Z = (M + PDF_KCAP - 1) / PDF_KCAP + 1;  // + 1: the split falls inside a slice's span
+    lds = (size_t)(PDF_KCAP + 1 + PDF_PAD) * 8 + (size_t)PDF_KCAP * 4 + (size_t)(PDF_NBK + 1) * 2;
+  }
   a.q_sorted = q_sorted;
   a.M = M;
   if (mode == 2) {
@@ -697,8 +869,13 @@ static int pdf_launch(PdfArgs& a, const uint64_t* q_sorted, int M, hipStream_t s
   } else {
     const long long nblk = ((long long)a.Z * a.nd + 7) / 8 * 8;
     MFF_REQUIRE(nblk < (1ll << 31), "mff_pdf_count: too many days in one call");
-    if (mode == 1)
+    if (mode == 1) {
       hipLaunchKernelGGL(k_pdf_count<true>, dim3((unsigned)nblk), dim3(PDF_CT), lds, st, a);
+      if (a.kslice) {
+        MFF_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_pdf_learn, dim3((unsigned)((a.nd + 15) / 16)), dim3(64), 0, st, q_sorted, M, a.learn);
+      }
+    }
     else
       hipLaunchKernelGGL(k_pdf_count<false>, dim3((unsigned)nblk), dim3(PDF_CT), lds, st, a);
   }

@@ -441,27 +441,47 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, uin
       if (emit_levels) {
         // doc_pdf level list (as mff_stage1g.hip): per level, key c_last / close (IEEE)
         // and its bar count; one reservation per stock-day in the day's flat list
-        const Bits LE = ballot4(lend);
-        const int L = count(LE);
-        const uint64_t lt = (1ull << lane) - 1ull;
-        uint32_t idx = 0u;
+        // two lists (pdf_levels_split): A the keys below the pass's split key from the
+        // front of the day's slots, B the others from the back
+        const float clf = elem(c, ml);
+        const double cl = (double)clf;
+        const uint64_t ksplit = pdf_split_key(a.lvl_count, a.D);
+        uint64_t lkey[4];
+        bool inA[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) idx += (uint32_t)__popcll(LE.b[k] & lt);
-        uint32_t base = 0u;
-        if (lane == 0) base = atomicAdd(a.lvl_count + d, (uint32_t)L);
-        idx += (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+        for (int k = 0; k < 4; ++k) {
+          lkey[k] = ord64(cl / (double)bitsf(~hi[k]));
+          inA[k] = lend[k] && lkey[k] < ksplit;
+        }
+        const Bits AE = ballot4(inA);
+        const Bits LE = ballot4(lend);
+        const int L = count(LE), LA = count(AE);
+        const uint64_t lt = (1ull << lane) - 1ull;
+        uint32_t idxA = 0u, idxL = 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          idxA += (uint32_t)__popcll(AE.b[k] & lt);
+          idxL += (uint32_t)__popcll(LE.b[k] & lt);
+        }
+        uint32_t idxB = idxL - idxA;
         double pos[4] = {(double)l4, (double)(l4 + 1), (double)(l4 + 2), (double)(l4 + 3)};
         double ppos[4];
         bool hpp[4];
         prev_valid(pos, lend, ppos, hpp);
-        const double cl = (double)elem(c, ml);
+        uint64_t base = 0ull;  // one u64 counter per day: list A count low, list B high
+        if (lane == 0) {
+          base = atomicAdd(reinterpret_cast<unsigned long long*>(a.lvl_count) + d,
+                           (unsigned long long)((uint64_t)(uint32_t)LA | ((uint64_t)(uint32_t)(L - LA) << 32)));
+        }
+        idxA += (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base);
+        idxB += (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(base >> 32));
         const size_t cap = (size_t)a.S * NBAR;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (lend[k]) {
-            a.lvl_key[(size_t)d * cap + idx] = ord64(cl / (double)bitsf(~hi[k]));
-            a.lvl_w[(size_t)d * cap + idx] = (uint8_t)(l4 + k - (hpp[k] ? (int)ppos[k] : -1));
-            ++idx;
+            const size_t at = inA[k] ? (size_t)idxA++ : cap - 1 - (size_t)idxB++;
+            a.lvl_key[(size_t)d * cap + at] = lkey[k];
+            a.lvl_w[(size_t)d * cap + at] = (uint8_t)(l4 + k - (hpp[k] ? (int)ppos[k] : -1));
           }
       }
       if (fam & F_LVL) {

@@ -951,18 +951,43 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
     // ---------------------------------------------------------------- doc_pdf level list
     // One reservation per wave for its four groups' levels: every stock-day of the block
     // is day d, so one returning atomic per 4 stock-days on the day's counter instead of
-    // one per stock-day (5,000 serialized adds per day at c4: 1.3 ms of the kernel).
-    // Issued before the result stores, its value used after them.
+    // one per stock-day (5,000 serialized adds per day at c4: 1.3 ms of the kernel).  The
+    // day's levels go to two lists (pdf_levels_split): list A the keys c_last / close
+    // below the pass's split key, from the front of the day's region, list B the others
+    // from its back; one u64 counter holds both counts (A low, B high), so the
+    // reservation stays one atomic.  Levels are in descending close order (keys
+    // ascending), so a group's list-A levels are its first gA.  Issued before the result stores, the reservation used after them.
     const bool emit = a.lvl_key != nullptr;  // uniform
-    uint32_t lpre = 0u, lwb = 0u;
+    uint32_t lpreA = 0u, lpreB = 0u, gA = 0u;
+    uint64_t lwb = 0ull;
     if (emit) {
-      const uint32_t l0 = (uint32_t)__builtin_amdgcn_readlane((int)emitL, 0);
-      const uint32_t l1 = (uint32_t)__builtin_amdgcn_readlane((int)emitL, 16);
-      const uint32_t l2 = (uint32_t)__builtin_amdgcn_readlane((int)emitL, 32);
-      const uint32_t l3 = (uint32_t)__builtin_amdgcn_readlane((int)emitL, 48);
-      lpre = grp == 0 ? 0u : grp == 1 ? l0 : grp == 2 ? l0 + l1 : l0 + l1 + l2;
-      const uint32_t tot = l0 + l1 + l2 + l3;
-      if (tot != 0u && lane == 0) lwb = atomicAdd(a.lvl_count + d, tot);
+      const uint32_t* lc = reinterpret_cast<const uint32_t*>(scr) + NBAR;
+      const uint64_t ksplit = pdf_split_key(a.lvl_count, a.D);
+      // keys ascend with l (closes descend): gA = lower_bound of the split key over the
+      // group's levels, two rounds of 16 probes (blocks of 16 levels, then within one)
+      auto key_at = [&](int l) {
+        return dbits(fdiv_f32in(emitC, bitsf(emitB - (lc[l] >> 8)))) | 0x8000000000000000ull;
+      };
+      const int pb = 16 * g + 15;
+      const bool lb1 = pb < (int)emitL && key_at(pb) < ksplit;
+      const uint32_t c1 = (uint32_t)__popc((uint32_t)(__ballot(lb1) >> gbase()) & 0xFFFFu);
+      const int pw = 16 * (int)c1 + g;
+      const bool lb2 = pw < (int)emitL && key_at(pw) < ksplit;
+      gA = 16u * c1 + (uint32_t)__popc((uint32_t)(__ballot(lb2) >> gbase()) & 0xFFFFu);
+      const uint32_t nB = emitL - gA;
+      const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)gA, 0);
+      const uint32_t a1 = (uint32_t)__builtin_amdgcn_readlane((int)gA, 16);
+      const uint32_t a2 = (uint32_t)__builtin_amdgcn_readlane((int)gA, 32);
+      const uint32_t a3 = (uint32_t)__builtin_amdgcn_readlane((int)gA, 48);
+      const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)nB, 0);
+      const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)nB, 16);
+      const uint32_t b2 = (uint32_t)__builtin_amdgcn_readlane((int)nB, 32);
+      const uint32_t b3 = (uint32_t)__builtin_amdgcn_readlane((int)nB, 48);
+      lpreA = grp == 0 ? 0u : grp == 1 ? a0 : grp == 2 ? a0 + a1 : a0 + a1 + a2;
+      lpreB = grp == 0 ? 0u : grp == 1 ? b0 : grp == 2 ? b0 + b1 : b0 + b1 + b2;
+      const uint64_t tot = (uint64_t)(a0 + a1 + a2 + a3) | ((uint64_t)(b0 + b1 + b2 + b3) << 32);
+      if (lane == 0 && tot != 0ull)
+        lwb = atomicAdd(reinterpret_cast<unsigned long long*>(a.lvl_count) + d, (unsigned long long)tot);
     }
 
     // ---------------------------------------------------------------- stores
@@ -985,18 +1010,24 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
     if (emit) {
       // key c_last / close (correctly rounded), bars at the level; levels interleaved
       // over the group's lanes (level l from lane l % 16), so one store instruction
-      // writes 16 consecutive entries per group: 128 contiguous bytes of keys and 16 of
-      // weights.  The levels are still in the group's scratch (lc, from the LVL section).
-      const uint32_t base = (uint32_t)__builtin_amdgcn_readfirstlane((int)lwb) + lpre;
+      // writes 16 consecutive entries per group (list B's in descending addresses; the
+      // block holding the group's A / B boundary writes to both lists).  The levels are
+      // still in the group's scratch (lc, from the LVL section).
+      const uint64_t wb = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(lwb >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lwb);
+      const uint32_t baseA = (uint32_t)wb + lpreA, baseB = (uint32_t)(wb >> 32) + lpreB;
       const uint32_t* lc = reinterpret_cast<const uint32_t*>(scr) + NBAR;
-      uint64_t* kd = a.lvl_key + (size_t)d * ((size_t)a.S * NBAR);
-      uint8_t* wd = a.lvl_w + (size_t)d * ((size_t)a.S * NBAR);
+      const size_t capd = (size_t)a.S * NBAR;
+      uint64_t* kd = a.lvl_key + (size_t)d * capd;
+      uint8_t* wd = a.lvl_w + (size_t)d * capd;
       for (int l = g; l < (int)emitL; l += 16) {
         const uint32_t cwb = lc[l];
         const uint32_t ee = cwb & 0xFFu;
         const uint32_t ep = l > 0 ? (lc[l - 1] & 0xFFu) : 0xFFFFFFFFu;  // -1 before level 0
-        kd[base + l] = dbits(fdiv_f32in(emitC, bitsf(emitB - (cwb >> 8)))) | 0x8000000000000000ull;  // ord64 of a positive
-        wd[base + l] = (uint8_t)(ee - ep);
+        const size_t at = (uint32_t)l < gA ? (size_t)(baseA + (uint32_t)l)
+                                          : capd - 1 - (size_t)(baseB + (uint32_t)l - gA);
+        kd[at] = dbits(fdiv_f32in(emitC, bitsf(emitB - (cwb >> 8)))) | 0x8000000000000000ull;  // ord64 of a positive
+        wd[at] = (uint8_t)(ee - ep);
       }
       lds_fence();  // the next iteration rewrites the scratch
     }
@@ -1016,9 +1047,13 @@ extern "C" size_t mff_stage1_workspace_bytes(int S, int D) {
 namespace mff {
 // doc_pdf level side channel: counts u32 [D] | keys u64 [D][S*240] | bars u8 [D][S*240]
 // (a day holds at most one level per bar of every stock)
+// level buffer: per day the entry counts of list A and list B (u32 pairs, A first: one
+// u64 counter per day) and the split key (u64, pdf_koff), then
+// the keys u64 [D][S * 240] and the bars u8 [D][S * 240]; list A (keys below the split
+// key) fills a day's S * 240 slots from the front, list B from the back
 size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w) {
   const size_t cap = (size_t)S * (size_t)D * NBAR;
-  *off_key = ((size_t)D * 4 + 255) & ~(size_t)255;
+  *off_key = (pdf_koff(D) + 8 + 255) & ~(size_t)255;
   *off_w = *off_key + cap * 8;
   return *off_w + cap;
 }
@@ -1110,7 +1145,10 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
                       st, a.lvl_count, a.lvl_key, a.lvl_w);
   }
   if (part & 1) {  // LVL/PDF group + exact list: everything the doc_pdf phases read
-    if (a.fam & F_PDF) MFF_HIP(hipMemsetAsync(a.lvl_count, 0, (size_t)D * 4, st));
+    if (a.fam & F_PDF) {
+      MFF_HIP(hipMemsetAsync(a.lvl_count, 0, (size_t)D * 8, st));
+      if (pdf_split_init(a.lvl_count, D, st) != 0) return -2;
+    }
     MFF_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
     if (w64) {  // the wave-per-stock-day kernel for everything
       const int rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, nullptr, nullptr, ~0u, 0, st);

@@ -456,7 +456,7 @@ def stage1_launch_times(panel: DevicePanel):
         fn()
         evs[i + 1].record(st)
     torch.cuda.synchronize(dev)
-    nlev = int(levels[:4 * D].view(torch.int32).to(torch.int64).sum().item())  # per-day entry counts
+    nlev = int(levels[:8 * D].view(torch.int32).to(torch.int64).sum().item())  # lists A + B per day
     sd = S * D
     fam_rows = {}
     for i in ids:
