@@ -31,7 +31,9 @@ def parse(path, sym):
         if m:
             files[int(m.group(1))] = m.group(3)
     start = next(i for i, l in enumerate(lines) if l.startswith(sym + ":"))
-    end = next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i])
+    # to the function's end label (a kernel may hold several s_endpgm)
+    end = next((i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end")),
+               next(i for i in range(start, len(lines)) if "s_endpgm" in lines[i]))
     blocks = []
     cur = {"label": "entry", "header": None, "depth": 0, "ins": []}
     blocks.append(cur)

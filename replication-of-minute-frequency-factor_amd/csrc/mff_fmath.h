@@ -49,5 +49,16 @@ __device__ __forceinline__ void fsqrt2(double x, double& sq, double& rsq) {
   sq = fma(g, e, g);
   rsq = 2.0 * fma(h, e, h);
 }
+// fsqrt2's outputs alone (the same step, one output each)
+__device__ __forceinline__ double fsqrt(double x) {
+  const double r = __builtin_amdgcn_rsq(x);
+  const double g = x * r, e = fma(-g, 0.5 * r, 0.5);
+  return fma(g, e, g);
+}
+__device__ __forceinline__ double frsq(double x) {
+  const double r = __builtin_amdgcn_rsq(x);
+  const double e = fma(-(x * r), 0.5 * r, 0.5);
+  return fma(r, e, r);
+}
 
 }  // namespace mff

@@ -20,11 +20,11 @@
 //  SUMC  Amihud over the previous present bar                           CM:734-761
 //  CORR  six Pearson sums; prv/pv/pvd/pvl shifted by the first present pair (loaded
 //        directly), prvr/pvr by their first pair (captured in the walk)  CM:834-932
-//  OLS   50-minute windows (t-50, t]: running prefix sums of (low - low0, high - high0)
-//        and their products, and the same prefix 50 bars behind (the bars leaving the
-//        window are walked again: identical additions, so the difference is the g16
-//        kernel's window sum); a window needs all 50 bars; constancy from the last bar
-//        whose low / high differs from the previous bar                 CM:93-376
+//  OLS   50-minute windows (t-50, t]: sliding sums of (low - low0, high - high0) and their
+//        products (each bar added on entry and subtracted when it leaves, 50 bars later:
+//        the first-order sums are exact, f32 differences summed in f64); a window needs
+//        all 50 bars; constancy from the last bar whose low / high differs from the
+//        previous bar                                                     CM:93-376
 //  MOMH  high / low moments shifted by the first ratio                   CM:499-515
 //
 // Semantics are those of the 16-lane kernel; the bar
@@ -276,9 +276,9 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   double rcp_ = 1.0, rcz = 1.0, rvz = 1.0;  // their reciprocals (frcp)
   bool hp = false, hz = false;
 
-  // OLS: prefix through this bar (R*) and through the bar 50 back (Q*)
-  double Rx = 0, Ry = 0, Rxx = 0, Ryy = 0, Rxy = 0, Qx = 0, Qy = 0, Qxx = 0, Qyy = 0, Qxy = 0;
-  int cR = 0, cQ = 0, lcx = -1, lcy = -1;
+  // OLS: sums over the window (t-50, t] and its count of present bars
+  double Sx = 0, Sy = 0, Sxx = 0, Syy = 0, Sxy = 0;
+  int cW = 0, lcx = -1, lcy = -1;
   float plo = 0.f, phi = 0.f;
   bool hph = false;
   double sq = 0, scs = 0, scr = 0, bd1 = 0, bd2 = 0, b0 = 0, bl = 0;
@@ -298,8 +298,8 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     if (pk) {
       if (fam & F_OLS) {
         const double dx = (double)lf - x0, dy = (double)hf - y0;
-        Rx += dx; Ry += dy; Rxx += dx * dx; Ryy += dy * dy; Rxy += dx * dy;
-        if (!ALLP) ++cR;
+        Sx += dx; Sy += dy; Sxx = fma(dx, dx, Sxx); Syy = fma(dy, dy, Syy); Sxy = fma(dx, dy, Sxy);
+        if (!ALLP) ++cW;
         if (ALLP) {
           lcx = (m > 0 && lf != plo) ? m : lcx;
           lcy = (m > 0 && hf != phi) ? m : lcy;
@@ -317,11 +317,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     if (!(fam & F_OLS)) return;
     if (lpk) {  // bar m - 50 leaves the window
       const double dx = (double)llf - x0, dy = (double)lhf - y0;
-      Qx += dx; Qy += dy; Qxx += dx * dx; Qyy += dy * dy; Qxy += dx * dy;
-      if (!ALLP) ++cQ;
+      Sx -= dx; Sy -= dy; Sxx = fma(-dx, dx, Sxx); Syy = fma(-dy, dy, Syy); Sxy = fma(-dx, dy, Sxy);
+      if (!ALLP) --cW;
     }
-    if (m >= 49 && (ALLP || cR - cQ == 50)) {  // window m-49..m, all 50 bars present (CM:129)
-      const double Sx = Rx - Qx, Sy = Ry - Qy, Sxx = Rxx - Qxx, Syy = Ryy - Qyy, Sxy = Rxy - Qxy;
+    if (m >= 49 && (ALLP || cW == 50)) {  // window m-49..m, all 50 bars present (CM:129)
       const bool cx = lcx <= m - 49, cy = lcy <= m - 49;  // constant low / high
       // 50 x the population (co)variances: the factor 1/50 cancels in beta, cov^2/(vx vy)
       // and cov/sqrt(vx vy), and is applied once at the end to sum sqrt(cov)/(vx vy);
@@ -333,10 +332,9 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       const double beta = fdiv(vz ? (cy ? 0.0 : Cv) : y0 + Sy * 0.02, vz ? Vx : x0 + Sx * 0.02);
       const double prod = Vx * Vy;
       if (!cx && !cy && prod != 0.0) {
-        const double ip = frcp(prod);
-        double sp, rp, sc, rc;
-        fsqrt2(prod, sp, rp);  // prod < 0: NaN, as sqrt(prod)
-        fsqrt2(Cv, sc, rc);    // cov < 0: NaN, as cov**0.5
+        const double rp = frsq(prod);  // prod < 0: NaN, as sqrt(prod)
+        const double ip = rp * rp;     // 1 / prod
+        const double sc = fsqrt(Cv);   // cov < 0: NaN, as cov**0.5
         sq += (Cv == 0.0 ? 0.0 : sc) * ip;  // cov**0.5 / (vx*vy) / (50^1.5)   CM:137
         scs += Cv * Cv * ip;                // cov**2 / (vx*vy)     CM:212
         scr += Cv * rp;                     // cov / (vx*vy)**0.5   CM:261
