@@ -43,7 +43,10 @@ constexpr int PDF_MAXM = 1 << 24;
 constexpr uint64_t PDF_KSPLIT0 = 0xBFF0000000000000ull;  // ord64(1.0)
 // slice capacity of the split-aligned count (LDS: 12 B per query + the bucket table,
 // within 160 KiB): two slices cover 25,800 queries, a day of 5,160 stocks
-constexpr int PDF_KCAP = 12900;
+#ifndef MFF_PDF_KCAP
+#define MFF_PDF_KCAP 12900
+#endif
+constexpr int PDF_KCAP = MFF_PDF_KCAP;
 // learned split key, one per device: sum / count of the per-day medians seen since the
 // last pass start, and the key in use
 struct PdfLearn {
