@@ -221,6 +221,9 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
                           after_sort=(lambda: sorted_ev.record(side)) if sorted_ev is not None else None)
             if sorted_ev is not None:  # part 2 after the doc_pdf sort (whole-CU workgroups)
                 main.wait_event(sorted_ev)
+                if hl is not None and HL_AT == "sort":  # set H beside the pair, after the sort
+                    hl.wait_event(sorted_ev)
+                    _lib.check(lib.mff_stage1_part(*(args[:-1] + [hl.cuda_stream]), 4), "mff_stage1_part(4)")
             _lib.check(lib.mff_stage1_part(*args, 10 if hl is not None else 2), "mff_stage1_part(2)")
             main.wait_stream(side)
         if hl is not None and HL_AT == "pdf" and not PDF_FIRST:
@@ -262,7 +265,8 @@ PDF_FIRST = os.environ.get("MFF_PDF_FIRST", "0") != "0"
 # MFF_HL_STREAM=0: launch order of round 1 (A/B timing).
 HL_STREAM = os.environ.get("MFF_HL_STREAM", "1") != "0"
 # MFF_HL_AT: when that stream's launch is issued: "start" (default), "part1" (after the
-# sorted-group launch), "pdf" (after the doc_pdf phases)
+# sorted-group launch), "pdf" (after the doc_pdf phases), "sort" (after the doc_pdf sort,
+# beside the pair)
 HL_AT = os.environ.get("MFF_HL_AT", "start")
 
 # Stream priorities of the side streams (torch / HIP: lower = higher priority; 0 is the
