@@ -182,6 +182,36 @@ def test_doc_pdf_beyond_32768_queries(dev):
     assert not bad, "\n".join(bad)
 
 
+def test_doc_pdf_split_key_extremes(dev):
+    """The split level lists: the split key is learned on the device from
+    earlier calls, so a call whose doc_pdf keys all sit on one side of it must still rank
+    exactly.  Closes rising all day (every key c_last / c >= 1), then falling (every key
+    <= 1, all below the key the rising panel taught), then rising again, each against the
+    oracle at tolerance 0; the rising panel is ranked twice (before and after the falling
+    one), so the answer cannot depend on the learned key."""
+    import mff_oracle as O
+    from mff import synth
+    names = ["doc_pdf60", "doc_pdf80", "doc_pdf95"]
+
+    def trending(sign, seed):
+        panel = synth.make_panel(900, 2, config=seed)
+        ramp = (1.0 + sign * 2e-3 * np.arange(panel["close"].shape[2])).astype(np.float32)
+        panel["close"] = (panel["close"] * ramp).astype(np.float32)
+        for k in ("open", "high", "low"):
+            panel[k] = panel["close"].copy()
+        return panel
+
+    up, down = trending(+1, 21), trending(-1, 22)
+    refs = {"up": O.oracle_stage1(up, names), "down": O.oracle_stage1(down, names)}
+    for tag, panel, ref in (("up", up, "up"), ("down", down, "down"), ("up again", up, "up")):
+        ov, os_ = refs[ref]
+        gv, gs, _ = _run_stage1(panel, dev, names)
+        bad = []
+        for r, nm in enumerate(names):
+            bad += compare(gv[r], gs[r], ov[r], os_[r], f"{tag}/{nm}", atol=0.0, rtol=0.0)
+        assert not bad, "\n".join(bad)
+
+
 def test_stage2_golden(dev):
     from golden.make_golden import STAGE23_FACTORS
     from mff import engine, catalog
