@@ -21,8 +21,10 @@ the pass's average duration from HIP events on its launch stream; peak 8.0 TB/s
 up to the window; profiles/pass_span.py turns the kernel trace into per-pass spans.  bound stays "hbm":
 the north star prices the pass against HBM bandwidth.  traffic: HBM bytes per pass from
 the committed rocprofv3 PMC passes (profiles/pmc_stage1.json: FETCH_SIZE x 2 per the
-gfx950 correction + WRITE_SIZE, summed over the launches), or null; traffic_calibrated:
-the same with the LDS-DMA kernels' factor measured by profiles/ubench/rowload.hip.
+gfx950 correction for wide streaming reads, x 2.400 / 1.986 for the serial kernels'
+64-B LDS-DMA row pieces as calibrated on a known byte count by profiles/ubench/rowload.hip
+(profiles/r04c/fetch_calib.log), + WRITE_SIZE, summed over the launches), or null;
+traffic_calibrated: the same figure (kept for continuity with earlier rounds' lines).
 valu: the issue side from the same PMC passes (VALU wave-instructions per stock-day,
 f64 share, fraction of the VALU pipe-cycles busy: ~0.8 over the pass, 0.8-0.9 in the
 three stage-1 kernels) -- what actually binds the pass.  kernels: every launch of the

@@ -5,7 +5,11 @@
 
 HBM bytes follow MI355X_MICROARCH.md's HBM section: FETCH_SIZE (KiB) x 2 on gfx950 for
 wide streaming reads (it tallies 128-B requests at 64 B) + WRITE_SIZE (KiB, exact for
-16-B-per-lane stores).  Per kernel: the counters summed over its dispatches in the pass,
+16-B-per-lane stores).  The guide leaves other access shapes to a calibration on a known
+byte count: the serial kernels (k_stage1s*, the wave pair) stage rows by LDS-DMA in 64-B
+pieces (16 rows x 64 B per wave-instruction), for which FETCH_SIZE reports 0.83 of the
+bytes read (profiles/ubench/rowload.hip kernel D: 1.986 GB counted for 2.400 GB read,
+profiles/r04c/fetch_calib.log), so their FETCH_SIZE is scaled by 2.400 / 1.986.  Per kernel: the counters summed over its dispatches in the pass,
 VALU wave-instructions per stock-day, f64 share, and the wave-cycle split (waiting /
 issue-stalled / VALU-active, SQ_* quad-cycles)."""
 import csv
@@ -16,6 +20,13 @@ import sys
 from collections import defaultdict
 
 PASS = ("k_stage1", "k_pdf_sort", "k_pdf_count")  # the launches of one stage-1 pass
+DMA64 = 2.400 / 1.986  # FETCH_SIZE -> bytes for the 64-B LDS-DMA row pieces (calibrated)
+
+
+def fetch_factor(name):
+    """FETCH_SIZE correction of a kernel: the serial kernels' LDS-DMA pieces (calibrated),
+    else the guide's x 2 for wide streaming reads."""
+    return DMA64 if name.startswith("k_stage1s") else 2.0
 F64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
 
 
@@ -36,8 +47,9 @@ def main():
     per, tot = {}, defaultdict(float)
     for k, cs in sorted(tab.items()):
         e = dict(cs)
-        hbm = 1024.0 * (2.0 * cs.get("FETCH_SIZE", 0.0) + cs.get("WRITE_SIZE", 0.0))
+        hbm = 1024.0 * (fetch_factor(k) * cs.get("FETCH_SIZE", 0.0) + cs.get("WRITE_SIZE", 0.0))
         e["hbm_bytes"] = hbm
+        e["fetch_factor"] = round(fetch_factor(k), 4)
         n = cs.get("SQ_INSTS_VALU", 0.0)
         f64 = sum(cs.get(c, 0.0) for c in F64)
         wc = cs.get("SQ_WAVE_CYCLES", 0.0)
@@ -54,7 +66,10 @@ def main():
         "kernel": "stage-1 pass: every k_stage1* launch of one bench step + the doc_pdf sort / count",
         "stocks": S, "days": D, "round": rnd,
         "fetch_size_kib": tot.get("FETCH_SIZE"), "write_size_kib": tot.get("WRITE_SIZE"),
-        "hbm_bytes_per_launch": 1024.0 * (2.0 * tot.get("FETCH_SIZE", 0.0) + tot.get("WRITE_SIZE", 0.0)),
+        "hbm_bytes_per_launch": sum(e["hbm_bytes"] for e in per.values()),
+        "hbm_bytes_calibrated": sum(e["hbm_bytes"] for e in per.values()),
+        "hbm_bytes_uncalibrated_x2": 1024.0 * (2.0 * tot.get("FETCH_SIZE", 0.0) + tot.get("WRITE_SIZE", 0.0)),
+        "fetch_calibration": "profiles/r04c/fetch_calib.log (64-B LDS-DMA pieces: x %.4f)" % DMA64,
         "sq": {k: v for k, v in tot.items() if not k.endswith("_SIZE")},
         "per_kernel": per,
     }
