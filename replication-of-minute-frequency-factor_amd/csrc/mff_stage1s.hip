@@ -88,6 +88,11 @@ constexpr uint32_t kPairB = MFF_PAIR_SPLIT ? (F_SUMC | F_CORR) : kSerB;
 #ifndef MFF_PAIR_QREAD
 #define MFF_PAIR_QREAD 0
 #endif
+// set H's lag chunk (c-3, the bars leaving the 50-bar windows) from a register ring of the
+// last three chunks instead of a second LDS-DMA of chunk c-3
+#ifndef MFF_SERH_VRING
+#define MFF_SERH_VRING 1
+#endif
 
 // ---- presence bits of one stock-day: 8 words, bit m%32 of word m/32 (compile-time
 // word indices only, so the array stays in registers)
@@ -522,7 +527,8 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     constexpr int NP = __builtin_popcount(PLM);
     constexpr bool LAG = (SET & F_OLS) != 0u;
     static_assert(!(PAIR && LAG), "the pair form covers sets A and B");
-    constexpr int NB = LAG ? 2 * NP : NP;  // images: the planes, then their lag copies
+    constexpr bool VRING = LAG && MFF_SERH_VRING;
+    constexpr int NB = LAG && !VRING ? 2 * NP : NP;  // images: the planes, then their lag copies
     // chunk = CQ quads (4*CQ bars) per stock-day; the lag sets use 8-bar chunks so the
     // staged registers (NB*CQ float4) leave room for a third wave per SIMD
     constexpr int CQ = PAIR ? 4 : (SET == kSerB || SET == kSerAB) ? 2 : 4, BC = 4 * CQ;
@@ -580,6 +586,14 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       return x;
     };
     Q4 carry;  // lag bars BC-2, BC-1 of chunk c-1-LAGC (in .z .w)
+    // VRING: chunks c-3, c-2, c-1 of the planes (slot 0 = the lag chunk of chunk c)
+    float4 RG[VRING ? LAGC : 1][NP][CQ];
+#pragma unroll
+    for (int j = 0; j < (VRING ? LAGC : 1); ++j)
+#pragma unroll
+      for (int ii = 0; ii < NP; ++ii)
+#pragma unroll
+        for (int k = 0; k < CQ; ++k) RG[j][ii][k] = one4;
     carry.o = carry.h = carry.l = carry.c = one4;
     carry.v = zero4;
     uint32_t pw1 = 0u, pw2 = 0u;  // mask words w-1, w-2
@@ -650,12 +664,16 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       }
       if (!PAIR && c + NBUF < NBAR / BC) {
         dma(sb, c + NBUF, 0);
-        if (LAG && c + 1 >= LAGC) dma(sb, c + 1 - LAGC, NP);
+        if (LAG && !VRING && c + 1 >= LAGC) dma(sb, c + 1 - LAGC, NP);
       }
 #pragma unroll
       for (int k = 0; k < CQ; ++k) {
         const Q4 x = toq(X, 0, k);
-        if constexpr (LAG) {
+        if constexpr (VRING) {
+          const Q4 l1 = toq(RG[0], 0, k);
+          const Q4 l0 = k > 0 ? toq(RG[0], 0, k - 1) : carry;
+          quad(full, BC * c + 4 * k, bits >> (BC * h + 4 * k), lbits >> (BC * h + 4 * k), x, l0.h, l0.l, l1.h, l1.l);
+        } else if constexpr (LAG) {
           const Q4 l1 = toq(X, NP, k);
           const Q4 l0 = k > 0 ? toq(X, NP, k - 1) : carry;
           quad(full, BC * c + 4 * k, bits >> (BC * h + 4 * k), lbits >> (BC * h + 4 * k), x, l0.h, l0.l, l1.h, l1.l);
@@ -663,7 +681,21 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
           quad(full, BC * c + 4 * k, bits >> (BC * h + 4 * k), 0u, x, one4, one4, one4, one4);
         }
       }
-      if constexpr (LAG) carry = toq(X, NP, CQ - 1);
+      if constexpr (VRING) {
+        carry = toq(RG[0], 0, CQ - 1);
+#pragma unroll
+        for (int j = 0; j + 1 < LAGC; ++j)
+#pragma unroll
+          for (int ii = 0; ii < NP; ++ii)
+#pragma unroll
+            for (int k = 0; k < CQ; ++k) RG[j][ii][k] = RG[j + 1][ii][k];
+#pragma unroll
+        for (int ii = 0; ii < NP; ++ii)
+#pragma unroll
+          for (int k = 0; k < CQ; ++k) RG[LAGC - 1][ii][k] = X[ii][k];
+      } else if constexpr (LAG) {
+        carry = toq(X, NP, CQ - 1);
+      }
     };
     auto walk = [&](auto full) {
       dma(sbA, 0, 0);
