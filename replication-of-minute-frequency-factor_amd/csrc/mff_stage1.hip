@@ -669,7 +669,8 @@ __global__ __launch_bounds__(256) void k_stage1(S1Args a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int nf = a.nf;
   double* sv = reinterpret_cast<double*>(smem);                        // [nf][TILE]
-  uint32_t* vscr = reinterpret_cast<uint32_t*>(smem + (size_t)nf * TILE * 8);  // [WPB][256]
+  // list mode needs only the per-wave scratch (its launch allocates just that)
+  uint32_t* vscr = reinterpret_cast<uint32_t*>(a.list ? smem : smem + (size_t)nf * TILE * 8);  // [WPB][256]
   uint8_t* ss = smem + (size_t)nf * TILE * 8 + WPB * 256 * 4;            // [nf][TILE]
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t* vw = vscr + wave * 256;
@@ -738,7 +739,7 @@ int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, c
     a.fam |= kFactorFamily[ids[r]];
   }
   a.fam &= fam_mask;
-  const size_t lds = (size_t)nf * TILE * 8 + WPB * 256 * 4 + (size_t)nf * TILE;
+  const size_t lds = list ? (size_t)WPB * 256 * 4 : (size_t)nf * TILE * 8 + WPB * 256 * 4 + (size_t)nf * TILE;
   long long nblk;
   if (list) {
     nblk = list_grid;
