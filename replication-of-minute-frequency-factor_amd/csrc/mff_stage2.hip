@@ -380,11 +380,17 @@ __device__ __forceinline__ void window_stats(const double (&w)[L], double& mean,
 // Requires D >= 1 (mff_stage2 checks it before any launch).
 template <int N>
 __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, const uint8_t* state, int D, int S,
-                                                         int method, double* out_val, uint8_t* out_state) {
+                                                         int method, double* out_val, uint8_t* out_state, int rows,
+                                                         int seg) {
+  // blocks: (day segment, row, stock block); a segment of `seg` days (a multiple of S2_U)
+  // starts from the window state of its first day, rebuilt from the N present days before
   const int nsb = (S + S2_THREADS - 1) / S2_THREADS;
-  const int row = blockIdx.x / nsb;
-  const int s = (blockIdx.x % nsb) * S2_THREADS + (int)threadIdx.x;
-  if (s >= S || D <= 0) return;
+  const int nb = rows * nsb;
+  const int g = blockIdx.x / nb, rb = blockIdx.x % nb;
+  const int row = rb / nsb;
+  const int s = (rb % nsb) * S2_THREADS + (int)threadIdx.x;
+  const int ds = g * seg, de = min(D, ds + seg);
+  if (s >= S || ds >= de) return;
   const size_t plane = (size_t)D * S;
   const double* v = val + row * plane + s;
   const uint8_t* st = state + row * plane + s;
@@ -400,21 +406,40 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
   for (int k = 0; k < N + S2_U; ++k) w[k] = 0.0;
   uint64_t nullm = 0;  // bit k: w[k] is null
   int cnt = 0;
+  if (ds > 0 && method != MFF_ROLL_O) {
+    // the window after day ds-1 holds at most its last N present days: replay them
+    int dw = ds, found = 0;
+    while (dw > 0 && found < N) {
+      --dw;
+      found += st[(size_t)dw * S] != MFF_STATE_ABSENT ? 1 : 0;
+    }
+    for (int d = dw; d < ds; ++d) {
+      const uint8_t sx = st[(size_t)d * S];
+      if (sx == MFF_STATE_ABSENT) continue;
+      const bool isnull = sx == MFF_STATE_NULL;
+      const double x = v[(size_t)d * S];
+#pragma unroll
+      for (int k = 0; k + 1 < N; ++k) w[k] = w[k + 1];
+      w[N - 1] = isnull ? 0.0 : x;
+      nullm = (nullm >> 1) | ((uint64_t)isnull << (N - 1));
+      cnt = cnt < N ? cnt + 1 : N;
+    }
+  }
   // Stores are deferred by one chunk and issued together, before the next chunk's loads:
   // gfx9 counts stores in vmcnt, so the wait for a chunk's loads also waits for every
   // store issued before them -- issued a whole chunk earlier, they are long complete.
-  const int Dm = D - D % S2_U;  // whole chunks; the last D % S2_U days after the loop
+  const int Dm = ds + (de - ds) - (de - ds) % S2_U;  // whole chunks; the last days after the loop
   double xb[S2_U], rp[S2_U];
   uint8_t sb[S2_U];
   uint32_t sp = 0u;  // the deferred chunk's states, one byte per day
 #pragma unroll
   for (int u = 0; u < S2_U; ++u) {
-    const int d = min(u, D - 1);
+    const int d = min(ds + u, de - 1);
     xb[u] = v[(size_t)d * S];
     sb[u] = st[(size_t)d * S];
     rp[u] = 0.0;
   }
-  for (int d0 = 0; d0 < Dm; d0 += S2_U) {
+  for (int d0 = ds; d0 < Dm; d0 += S2_U) {
     double xc[S2_U];
     uint8_t sc[S2_U];
 #pragma unroll
@@ -422,7 +447,7 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
       xc[u] = xb[u];
       sc[u] = sb[u];
     }
-    if (d0 > 0) {
+    if (d0 > ds) {
 #pragma unroll
       for (int u = 0; u < S2_U; ++u) {
         const size_t o = (size_t)(d0 - S2_U + u) * S;
@@ -432,7 +457,7 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
     }
 #pragma unroll
     for (int u = 0; u < S2_U; ++u) {  // next chunk in flight while this one is processed
-      const int d = min(d0 + S2_U + u, D - 1);
+      const int d = min(d0 + S2_U + u, de - 1);
       xb[u] = v[(size_t)d * S];
       sb[u] = st[(size_t)d * S];
     }
@@ -541,7 +566,7 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
       sp |= (uint32_t)MFF_STATE_VALUE << (8 * u);
     }
   }
-  if (Dm > 0) {
+  if (Dm > ds) {
 #pragma unroll
     for (int u = 0; u < S2_U; ++u) {
       const size_t o = (size_t)(Dm - S2_U + u) * S;
@@ -549,7 +574,7 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
       os[o] = (uint8_t)(sp >> (8 * u));
     }
   }
-  for (int d = Dm; d < D; ++d) {  // the last D % S2_U days, one at a time
+  for (int d = Dm; d < de; ++d) {  // the segment's last days, one at a time
     const size_t o = (size_t)d * S;
     const double x = v[o];
     const uint8_t sx = st[o];
@@ -660,11 +685,29 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
   MFF_REQUIRE(N >= 1, "mff_stage2: N=%d < 1", N);
   MFF_REQUIRE(method >= MFF_ROLL_O && method <= MFF_ROLL_STD, "mff_stage2: unknown method %d", method);
   MFF_REQUIRE(val && state && out_val && out_state, "mff_stage2: NULL buffer");
-  const long long nreg = (long long)rows * ((S + S2_THREADS - 1) / S2_THREADS);
+  // day segments (MFF_S2_SEGS, default 4): more waves in flight for the memory system (a
+  // (row, stock) lane per wave-slot otherwise walks all D days: ~4.4 waves per SIMD at c4);
+  // each segment of >= 16 N days (a multiple of S2_U) rebuilds its window from the N
+  // present days before it.  z at N = 20, 58 rows at c4: 3.56 -> 3.28 ms (4 or 8 segments,
+  // profiles/r04f/s2_segments.log)
+  const char* sg = getenv("MFF_S2_SEGS");
+  int nseg = sg ? atoi(sg) : 4;
+  int seg = D;
+  if (nseg > 1) {
+    seg = (D + nseg - 1) / nseg;
+    if (seg < 16 * N) seg = 16 * N;
+    seg = (seg + S2_U - 1) / S2_U * S2_U;
+  }
+  // MFF_S2_SEG_DAYS: an explicit segment length (tests: segments shorter than the window)
+  const char* sdays = getenv("MFF_S2_SEG_DAYS");
+  if (sdays && atoi(sdays) > 0) seg = (atoi(sdays) + S2_U - 1) / S2_U * S2_U;
+  nseg = (D + seg - 1) / seg;
+  const long long nreg = (long long)nseg * rows * ((S + S2_THREADS - 1) / S2_THREADS);
+  MFF_REQUIRE(nreg < (1ll << 31), "mff_stage2: grid too large");
 #define MFF_S2_REG(NN)                                                                                      \
   case NN:                                                                                                  \
     hipLaunchKernelGGL(k_stage2_reg<NN>, dim3((unsigned)nreg), dim3(S2_THREADS), 0, as_stream(stream), val, \
-                       state, D, S, method, out_val, out_state);                                            \
+                       state, D, S, method, out_val, out_state, rows, seg);                                 \
     MFF_LAUNCH_CHECK();                                                                                     \
     return 0;
   // MFF_STAGE2_IMPL=ring / slide: a sliding kernel for every N (A/B timing)

@@ -245,6 +245,29 @@ def _random_long_panel(D, S, seed):
     return val, state
 
 
+@pytest.mark.parametrize("N,seg", [(3, 4), (20, 12), (20, 40), (64, 8), (64, 100)])
+def test_stage2_day_segments(dev, N, seg, monkeypatch):
+    """k_stage2_reg over day segments (MFF_S2_SEG_DAYS): each segment rebuilds its window
+    from the N present days before it -- segments shorter and longer than the window,
+    with absent days, nulls, NaN / inf and a constant column (exact zeros) crossing the
+    segment boundaries, against the oracle."""
+    import mff_oracle as O
+    from mff import engine
+    monkeypatch.setenv("MFF_S2_SEG_DAYS", str(seg))
+    D = 150
+    val, state = _random_long_panel(D, 130, N + 7)
+    state[30:70, 9] = 0  # a 40-day suspension across several segments
+    v = np.ascontiguousarray(val[None])
+    st = np.ascontiguousarray(state[None])
+    bad = []
+    for meth in ("m", "z", "std"):
+        rv, rs = engine.rolling(torch.from_numpy(v).to(dev), torch.from_numpy(st).to(dev), N, meth)
+        torch.cuda.synchronize()
+        ov, os_ = O.oracle_stage2(v[0], st[0], N, meth)
+        bad += compare(rv[0].cpu().numpy(), rs[0].cpu().numpy(), ov, os_, f"N{N}/seg{seg}/{meth}", atol=1e-9)
+    assert not bad, "\n".join(bad[:20])
+
+
 @pytest.mark.parametrize("N,D", [(1, 70), (2, 70), (3, 70), (5, 70), (7, 70), (10, 70), (20, 70), (60, 150),
                                   (64, 150), (65, 150), (120, 300), (250, 400),
                                   (20, 1), (20, 3), (5, 4), (3, 8), (7, 8)])
