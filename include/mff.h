@@ -62,10 +62,11 @@ const char* mff_factor_name(int id);
 #define MFF_VOLUME_F32 2
 #define MFF_VOLUME_I32 3
 
-/* mff_ingest_rows error counters (uint32 errors[5]) */
+/* mff_ingest_rows counters (uint32 errors[5]) */
 #define MFF_INGEST_ERR_INDEX 0  /* stock / day index outside [0,S) x [0,D): row skipped */
-#define MFF_INGEST_ERR_TIME 1   /* time off the 240-bar grid: row skipped */
-#define MFF_INGEST_ERR_DUP 2    /* (stock, day, minute) already present */
+#define MFF_INGEST_ERR_TIME 1   /* time off the 240-bar grid: row skipped (not an error: the
+                                   caller lists the stock-day in the row set) */
+#define MFF_INGEST_ERR_DUP 2    /* (stock, day, minute) already present (the same) */
 #define MFF_INGEST_ERR_PRICE 3  /* open/high/low/close not finite > 0 */
 #define MFF_INGEST_ERR_VOLUME 4 /* volume not integral in [0, MFF_VOLUME_MAX] */
 #define MFF_VOLUME_MAX 4294967294u /* 2^32 - 2 shares per bar */
@@ -130,28 +131,56 @@ int mff_stage1(const float* open, const float* high, const float* low,
                void* workspace, void* stream);
 
 /*
- * Stage 1 for the stock-days that hold polars nulls (a row that exists with a null open /
- * high / low / close / volume).  Replaces the same `cal_*` calls (CM:12-1406) on those
- * rows, with polars' null rules: only cal_liq_amihud_1min fills a null volume with 0
- * (CM:743-744); first()/last() return the null (CM:799, 829), sums / moments skip it,
- * pl.corr drops the pair (CM:841-931), pct_change forward-fills (CM:745, 861-866),
- * top_k prefers non-null values (CM:393-471), rank() leaves a null key unranked
- * (CM:1016) — the rules N1-N11 / C8 of oracle/mff_oracle.py.
- * The K stock-days null_sd[K] (d*S + s, device int32) carry their own presence words
- * null_mask uint32 [K][8] and per-field null bits null_bits uint32 [K][5][8] (field order
- * open, high, low, close, volume; same bit layout as `valid`); the panel's `valid` mask
- * must hold zeros for them, so the other stage-1 calls see them ABSENT.  Field values under
- * a null bit are don't-care.
+ * Row set: the stock-days computed from their own rows instead of the 240-bar grid.
+ * A stock-day is listed when a row of it holds a polars null (open / high / low / close /
+ * volume) or sits off the grid (a time that is not a 09:30-11:29 / 13:00-14:59 minute:
+ * a 09:25 or 15:00 bar, end-labelled bars, seconds) or shares its time with another row.
+ * The panel's `valid` mask holds zeros for a listed stock-day, so the grid kernels see it
+ * ABSENT; the row set carries every one of its rows:
+ *   rs_sd int32 [K]     d*S + s, ascending
+ *   rs_off int32 [K+1]  rows of stock-day i: rs_rows[rs_off[i] .. rs_off[i+1]), at most
+ *                       MFF_ROWS_MAX, in (time, frame) order (rows at one time
+ *                       keep their frame order), minute_in_trade (CM:98-106) non-decreasing
+ *   rs_rows MffRow [rs_off[K]]  time HHMMSSmmm in [0, 240000000), prices fp32, volume u32
+ *                       shares, nulls = bit i set when field i (open, high, low, close,
+ *                       volume) is null (its value is then don't-care)
+ */
+#define MFF_ROWS_MAX 255
+typedef struct MffRow {
+  int32_t time;
+  float open, high, low, close;
+  uint32_t volume;
+  uint32_t nulls;
+  uint32_t reserved;
+} MffRow; /* 32 B */
+
+/*
+ * Stage 1 of the row set.  Replaces the same `cal_*` calls (CM:12-1406) on those rows:
+ * polars' null rules (only cal_liq_amihud_1min fills a null volume with 0, CM:743-744;
+ * first()/last() return the null, CM:799, 829; sums / moments skip it; pl.corr drops the
+ * pair, CM:841-931; pct_change forward-fills, CM:745, 861-866; top_k prefers non-null
+ * values, CM:393-471; rank() leaves a null key unranked, CM:1016 -- the rules N1-N11 / C8
+ * of oracle/mff_oracle.py), the time filters on each row's own time (CM:18-84, 770-815,
+ * 1212-1387) and the 50-minute OLS windows over minute_in_trade (CM:98-129).
  * phase 1: doc_pdf queries + the stock-days' price levels appended to pdf_levels (call
  *          after mff_stage1_part 1 / 17 and before mff_pdf_sort);
  * phase 2: every other requested row (call after the stage-1 calls that write those rows);
  * phase 3: both (e.g. after mff_stage1 when no doc_pdf row is requested).
  */
-int mff_stage1_nulls(const float* open, const float* high, const float* low, const float* close,
-                     const uint32_t* volume, int S, int D, const int32_t* null_sd,
-                     const uint32_t* null_mask, const uint32_t* null_bits, int K,
-                     const int32_t* factor_ids /* host */, int nf, double* val, uint8_t* state,
-                     double* pdf_query, void* pdf_levels, int phase, void* stream);
+int mff_stage1_rows(int S, int D, const int32_t* rs_sd, const int32_t* rs_off, const MffRow* rs_rows, int K,
+                    const int32_t* factor_ids /* host */, int nf, double* val, uint8_t* state,
+                    double* pdf_query, void* pdf_levels, int phase, void* stream);
+/*
+ * Grid stock-days -> rows (e.g. to list stock-days of a device-built panel): for each of
+ * the K stock-days sd[K], its present bars in minute order, time = the bar's start label,
+ * null bits from null_bits uint32 [K][5][8] (the `valid` bit layout per field; NULL =
+ * none).  Count mode (rows == NULL): counts int32 [K] = rows per stock-day (the caller
+ * turns them into off [K+1]); else the rows are written at rows[off[i] ...].
+ */
+int mff_rows_from_panel(const float* open, const float* high, const float* low, const float* close,
+                        const uint32_t* volume, const uint32_t* valid, int S, int D, const int32_t* sd,
+                        const uint32_t* null_bits, int K, const int32_t* off, int32_t* counts, MffRow* rows,
+                        void* stream);
 
 /*
  * Multi-day frame semantics of the four factors whose reference windows run over('code')
@@ -164,17 +193,16 @@ int mff_stage1_nulls(const float* open, const float* high, const float* low, con
  * overwrites the rows of those four factors (when present in factor_ids) with the frame
  * semantics: the first bar of a day compares with the code's last close of the previous
  * day, and the 14:40+ / 14:10+ volume share uses the code's total over the whole frame.
- * open may be NULL unless a trade_bottom* row is requested.  null_sd / null_mask / null_bits
- * (K entries, the layout of mff_stage1_nulls; K = 0 and NULLs when the frame holds no
- * null) give the null-holding stock-days' presence and null bits: a null volume is 0 for
- * the Amihud sum (CM:743-744) and filtered out by volume != 0 (CM:855), a null close is
- * forward-filled by pct_change (CM:745, 861).
+ * open may be NULL unless a trade_bottom* row is requested.  rs_sd / rs_off / rs_rows (the
+ * panel's row set, K = 0 and NULLs when it has none) give the listed stock-days' rows: a
+ * null volume is 0 for the Amihud sum (CM:743-744) and filtered out by volume != 0
+ * (CM:855), a null close is forward-filled by pct_change (CM:745, 861), the tail windows
+ * test each row's own time (CM:1212, 1233).
  */
 int mff_stage1_frame(const float* open, const float* close, const uint32_t* volume,
-                     const uint32_t* valid, int S, int D, const int32_t* null_sd,
-                     const uint32_t* null_mask, const uint32_t* null_bits, int K,
-                     const int32_t* factor_ids /* host */, int nf, double* val, uint8_t* state,
-                     void* stream);
+                     const uint32_t* valid, int S, int D, const int32_t* rs_sd, const int32_t* rs_off,
+                     const MffRow* rs_rows, int K, const int32_t* factor_ids /* host */, int nf,
+                     double* val, uint8_t* state, void* stream);
 
 /*
  * doc_pdf60..95 frame-wide rank (CM:1015-1017: `.rank()` over ALL rows of the day

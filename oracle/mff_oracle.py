@@ -68,6 +68,19 @@ null propagates or is skipped:
   is null (``sort()`` then ``first()``).
 None of these is pinned by a polars run (parity unpinned); each is the documented
 behaviour of the polars expression the reference uses.
+
+Rows at any time (a 09:25 or 15:00 bar, end-labelled bars, seconds, two rows at one
+time): every function works on the rows and their own ``time`` values, as the reference
+does (``DayFrame.time``; the time filters CM:18-84, 770-815, 1212-1387 and
+``minute_in_trade`` CM:98-106 are restated literally).  Two more rules for them:
+
+* T1 ``rolling(index_column='minute_in_trade', period='50i')`` (CM:114-118) gives every
+  row the window of all rows whose index is in (t-50, t] -- the later rows at the same t
+  included (polars' look-behind windows consume duplicate index values), so the rows of a
+  duplicate minute share one window.
+* C9 ``sort(by=[code, date, time])`` (CM:19, 34, 70, 85) keeps rows at one time in frame
+  order (polars' sort is not promised stable; the build takes the stable order).
+Neither is pinned by a polars run.
 """
 from __future__ import annotations
 
@@ -446,7 +459,9 @@ def _ols_windows_calc(df: DayFrame, s: int, e: int):
     for i in range(mins.size):
         t = mins[i]
         lo = np.searchsorted(mins, t - 50, side="right")
-        hi = i + 1
+        # T1: every row of a duplicate minute shares one window -- polars' look-behind
+        # windows take all rows whose index is <= t, the later rows at t included
+        hi = np.searchsorted(mins, t, side="right")
         n = hi - lo  # pl.len(): rows, nulls included (N11)
         if n < 50:
             continue
@@ -1087,25 +1102,44 @@ ABSENT, NULLV, VALUE = 0, 1, 2
 # ----------------------------------------------------------------------------
 
 
+def day_rows(panel, d: int):
+    """The rows of day ``d`` of a dense panel dict in frame order (code, time; rows at one
+    time in their given order, C4): the present grid bars ([D][S][240] planes, ``present``)
+    plus the stock-days of ``panel["extra"]`` = (sd [K], off [K+1], rows) whose rows do not
+    fit the grid (mff.synth.row_set).  Returns (stock index, time, open, high, low, close,
+    volume as f64 arrays, null bits uint8)."""
+    pres = panel["present"][d]
+    S = pres.shape[0]
+    s_idx, m_idx = np.nonzero(pres)  # row-major: ordered by (stock, minute) = C4
+    f = lambda k: panel[k][d][s_idx, m_idx].astype(np.float64)
+    nb = panel.get("null")
+    cols = [s_idx.astype(np.int64), minute_to_time(m_idx), f("open"), f("high"), f("low"), f("close"),
+            f("volume"), nb[d][s_idx, m_idx].astype(np.uint8) if nb is not None else np.zeros(s_idx.size, np.uint8)]
+    ex = panel.get("extra")
+    if ex is not None:
+        sd, off, rows = ex
+        sd = np.asarray(sd, dtype=np.int64)
+        for i in np.flatnonzero(sd // S == d):
+            r = rows[off[i]:off[i + 1]]
+            add = [np.full(r.size, sd[i] % S, np.int64), r["time"].astype(np.int64)]
+            add += [r[k].astype(np.float64) for k in ("open", "high", "low", "close")]
+            add += [r["volume"].astype(np.float64), r["nulls"].astype(np.uint8)]
+            cols = [np.concatenate([a, b]) for a, b in zip(cols, add)]
+        order = np.lexsort((np.arange(cols[0].size), cols[1], cols[0]))  # (stock, time, given order)
+        cols = [a[order] for a in cols]
+    return cols
+
+
 def day_frame_from_panel(panel, d: int) -> DayFrame:
     """Build the reference day frame for day ``d`` of a dense panel dict with keys
-    open/high/low/close/volume ([D][S][240] f32), present ([D][S][240] bool), codes."""
-    pres = panel["present"][d]
-    s_idx, m_idx = np.nonzero(pres)  # row-major: ordered by (stock, minute) = C4
+    open/high/low/close/volume ([D][S][240] f32), present ([D][S][240] bool), codes, and
+    the optional ``null`` bits and ``extra`` rows (:func:`day_rows`)."""
+    s_idx, time, o, h, lo, c, v, nb = day_rows(panel, d)
     codes = np.asarray(panel["codes"])[s_idx]
-    f = lambda k: panel[k][d][s_idx, m_idx].astype(np.float64)
-    return DayFrame(codes, d, minute_to_time(m_idx), f("open"), f("high"), f("low"),
-                    f("close"), f("volume"), null=panel_nulls(panel, d, s_idx, m_idx))
-
-
-def panel_nulls(panel, d, s_idx, m_idx):
-    """{field: bool} null masks of the rows (s_idx, m_idx) of day d: panel["null"] is an
-    optional uint8 [D][S][240] whose bit i marks FIELDS[i] null on a present bar."""
-    nb = panel.get("null")
-    if nb is None:
-        return None
-    bits = nb[d][s_idx, m_idx]
-    return {k: (bits >> i) & 1 == 1 for i, k in enumerate(FIELDS)}
+    null = None
+    if panel.get("null") is not None or panel.get("extra") is not None:
+        null = {k: (nb >> i) & 1 == 1 for i, k in enumerate(FIELDS)}
+    return DayFrame(codes, d, time, o, h, lo, c, v, null=null)
 
 
 def oracle_stage1(panel, names: Sequence[str] = None):
@@ -1178,14 +1212,15 @@ def oracle_frame_xday(panel):
         st[d, s] = NULLV if x is None else VALUE
         v[d, s] = 0.0 if x is None else x
 
+    days = [day_rows(panel, d) for d in range(D)]
     for s in range(S):
-        dd, mm = np.nonzero(panel["present"][:, s])  # rows of the code, (date, time) order
+        # rows of the code over the frame, (date, time) order
+        parts = [(d, [a[r[0] == s] for a in r]) for d, r in enumerate(days)]
+        dd = np.concatenate([np.full(p[1][0].size, d, np.int64) for d, p in zip(range(D), parts)])
         if dd.size == 0:
             continue
-        g = lambda k: panel[k][dd, s, mm].astype(np.float64)
-        o, c, v = g("open"), g("close"), g("volume")
-        nb = panel.get("null")
-        nbits = nb[dd, s, mm] if nb is not None else np.zeros(dd.size, np.uint8)
+        col = lambda j: np.concatenate([p[1][j] for p in parts])
+        tm, o, c, v, nbits = col(1), col(2), col(5), col(6), col(7)
         nO, nC, nV = (nbits & 1) != 0, (nbits & 8) != 0, (nbits & 16) != 0
         # liq_amihud_1min: volume.fill_null(0); pct_change().over('code') (N5: nulls
         # forward-filled) .abs().fill_null(0); v > 0 ? pct / v : 0
@@ -1202,9 +1237,10 @@ def oracle_frame_xday(panel):
         for d in np.unique(dz):
             sel = [i for i in range(dz.size) if dz[i] == d]
             put("corr_prvr", d, s, pl_corr([cc[i] for i in sel], [vc[i] for i in sel]))
-        # trade_bottom20 / 50: filter(time >= 14:40 / 14:10), volume_d over('code')
-        for name, m0, plus_one in (("trade_bottom20retRatio", 220, True), ("trade_bottom50retRatio", 190, False)):
-            t = mm >= m0
+        # trade_bottom20 / 50: filter(time >= 14:40 / 14:10) (CM:1212, 1233), volume_d over('code')
+        for name, t0, plus_one in (("trade_bottom20retRatio", 144000000, True),
+                                   ("trade_bottom50retRatio", 141000000, False)):
+            t = tm >= t0
             if not t.any():
                 continue
             tot = pl_sum(v[t & ~nV])

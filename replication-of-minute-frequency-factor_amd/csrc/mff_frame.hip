@@ -20,12 +20,13 @@
 // frame sorted by code / date / time).  The per-day kernels compute the
 // one-day semantics; mff_stage1_frame overwrites these rows with the frame semantics.
 //
-// Nulls (the rules N1-N11 of oracle/mff_oracle.py): the stock-days listed by the panel's
-// null set carry their own presence words and null bits (include/mff.h, mff_stage1_nulls).
-// A null volume is 0 for the Amihud sum (fill_null, CM:743-744), filtered out by
-// volume != 0 (CM:855) and skipped by the tail sums; a null close is forward-filled by
-// pct_change (N5: its own change is 0, the next non-null close compares with the last
-// non-null one); a null open or close nulls the tail return (skipped by the sum).
+// Row set (include/mff.h MffRow): the stock-days listed there (a null field or a row off
+// the grid) are walked over their own rows, the tail windows tested on each row's time
+// (CM:1212, 1233).  Nulls follow the rules N1-N11 of oracle/mff_oracle.py: a null volume is
+// 0 for the Amihud sum (fill_null, CM:743-744), filtered out by volume != 0 (CM:855) and
+// skipped by the tail sums; a null close is forward-filled by pct_change (N5: its own
+// change is 0, the next non-null close compares with the last non-null one); a null open
+// or close nulls the tail return (skipped by the sum).
 //
 // Layout: lane = stock, one serial walk over the stock's days and bars (a convenience path
 // of the drop-in cal_* surface, not the batched driver, so it is not tuned).  Quotients as
@@ -46,9 +47,9 @@ struct FrameArgs {
   const float* close;
   const uint32_t* volume;  // u32 shares
   const uint32_t* valid;
-  const int32_t* null_sd;     // [K] ascending d*S + s, or null
-  const uint32_t* null_mask;  // [K][8]
-  const uint32_t* null_bits;  // [K][5][8]
+  const int32_t* rs_sd;   // [K] ascending d*S + s, or null
+  const int32_t* rs_off;  // [K+1]
+  const MffRow* rs_rows;
   int K;
   double* val;
   uint8_t* state;
@@ -70,81 +71,85 @@ __global__ __launch_bounds__(256) void k_frame_xday(FrameArgs a) {
   bool hp = false, hz = false, hzc = false;
   double cp = 1.0, czp = 1.0, vzp = 1.0;
   double tot20 = 0.0, tot50 = 0.0;  // the code's 14:40+ / 14:10+ volume over the frame
-  int ni = 0;  // the next null stock-day of this stock (the list is ascending in d*S + s)
+  int ni = 0;  // the next listed stock-day of this stock (the list is ascending in d*S + s)
   for (int d = 0; d < a.D; ++d) {
     const size_t sd = (size_t)d * a.S + s;
-    const uint32_t* mk = a.valid + sd * 8;
-    const uint32_t* nbO = nullptr;  // null bits of open, close, volume (null: none)
-    const uint32_t* nbC = nullptr;
-    const uint32_t* nbV = nullptr;
+    int li = -1;  // this stock-day's entry in the row set
     if (a.K > 0) {
       // binary search from the last hit: sd grows with d
       int lo = ni, hi = a.K;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if ((size_t)a.null_sd[mid] < sd) lo = mid + 1; else hi = mid;
+        if ((size_t)a.rs_sd[mid] < sd) lo = mid + 1; else hi = mid;
       }
       ni = lo;
-      if (lo < a.K && (size_t)a.null_sd[lo] == sd) {
-        mk = a.null_mask + (size_t)lo * 8;
-        nbO = a.null_bits + ((size_t)lo * 5 + 0) * 8;
-        nbC = a.null_bits + ((size_t)lo * 5 + 3) * 8;
-        nbV = a.null_bits + ((size_t)lo * 5 + 4) * 8;
-      }
+      if (lo < a.K && (size_t)a.rs_sd[lo] == sd) li = lo;
     }
-    const float* C = a.close + sd * NBAR;
     const bool tail = a.row_b20 >= 0 || a.row_b50 >= 0;  // open may be NULL otherwise
-    const uint32_t* V = a.volume + sd * NBAR;
     double amh = 0.0;
     double P[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     double x0 = 0.0, y0 = 0.0;
     int np = 0, nz = 0;
     double r20 = 0.0, r50 = 0.0;
     bool t20 = false, t50 = false, any = false;
-    for (int w = 0; w < 8; ++w) {
-      uint32_t bits = mk[w];
-      while (bits) {
-        const int m = 32 * w + __builtin_ctz(bits);
-        bits &= bits - 1u;
-        any = true;
-        const uint32_t bit = 1u << (m & 31);
-        const bool cok = !(nbC && (nbC[w] & bit)), vok = !(nbV && (nbV[w] & bit));
-        const bool ook = !(nbO && (nbO[w] & bit));
-        const double c = (double)C[m], v = vok ? (double)V[m] : 0.0;  // fill_null(0) (CM:744)
-        // amihud: |pct_change(close)| / volume for volume > 0; the code's first bar 0.  A
-        // null close is forward-filled: its change is 0 and it keeps the last close (N5)
+    // one row: close, volume (0 when null), open (tail windows only), null flags, in the
+    // 14:10+ / 14:40+ windows
+    auto row = [&](double c, double v, double o, bool cok, bool vok, bool ook, bool w50, bool w20) {
+      any = true;
+      // amihud: |pct_change(close)| / volume for volume > 0; the code's first bar 0.  A
+      // null close is forward-filled: its change is 0 and it keeps the last close (N5)
+      if (cok) {
+        if (hp && v > 0.0) amh += fabs(fdiv(c - cp, cp)) / v;
+        cp = c;
+        hp = true;
+      }
+      if (vok && v != 0.0) {  // corr_prvr rows (a null volume is filtered out, N1)
+        ++nz;
+        if (hz && hzc) {  // both changes non-null
+          const double pc = cok ? fdiv(c - czp, czp) : 0.0, pv = fdiv(v - vzp, vzp);
+          if (np == 0) { x0 = pc; y0 = pv; }
+          const double dx = pc - x0, dy = pv - y0;
+          P[0] += dx; P[1] += dy; P[2] += dx * dx; P[3] += dy * dy; P[4] += dx * dy;
+          ++np;
+        }
         if (cok) {
-          if (hp && v > 0.0) amh += fabs(fdiv(c - cp, cp)) / v;
-          cp = c;
-          hp = true;
+          czp = c;
+          hzc = true;
         }
-        if (vok && v != 0.0) {  // corr_prvr rows (a null volume is filtered out, N1)
-          ++nz;
-          if (hz && hzc) {  // both changes non-null
-            const double pc = cok ? fdiv(c - czp, czp) : 0.0, pv = fdiv(v - vzp, vzp);
-            if (np == 0) { x0 = pc; y0 = pv; }
-            const double dx = pc - x0, dy = pv - y0;
-            P[0] += dx; P[1] += dy; P[2] += dx * dx; P[3] += dy * dy; P[4] += dx * dy;
-            ++np;
-          }
-          if (cok) {
-            czp = c;
-            hzc = true;
-          }
-          vzp = v;
-          hz = true;
+        vzp = v;
+        hz = true;
+      }
+      if (tail && w50) {
+        const bool rok = vok && cok && ook;  // volume_d * ret: null unless all three (N1)
+        const double r = rok ? fdiv(c, o) - 1.0 : 0.0;
+        t50 = true;
+        tot50 += v;
+        if (rok) r50 += v * r;
+        if (w20) {
+          t20 = true;
+          tot20 += v;
+          if (rok) r20 += v * r;
         }
-        if (tail && m >= 190) {
-          const bool rok = vok && cok && ook;  // volume_d * ret: null unless all three (N1)
-          const double r = rok ? fdiv(c, (double)a.open[sd * NBAR + m]) - 1.0 : 0.0;
-          t50 = true;
-          tot50 += v;
-          if (rok) r50 += v * r;
-          if (m >= 220) {
-            t20 = true;
-            tot20 += v;
-            if (rok) r20 += v * r;
-          }
+      }
+    };
+    if (li >= 0) {
+      for (int q = a.rs_off[li]; q < a.rs_off[li + 1]; ++q) {
+        const MffRow& R = a.rs_rows[q];
+        const bool cok = !(R.nulls & 8u), vok = !(R.nulls & 16u), ook = !(R.nulls & 1u);
+        row((double)R.close, vok ? (double)R.volume : 0.0, (double)R.open, cok, vok, ook,
+            R.time >= 141000000, R.time >= 144000000);
+      }
+    } else {
+      const uint32_t* mk = a.valid + sd * 8;
+      const float* C = a.close + sd * NBAR;
+      const uint32_t* V = a.volume + sd * NBAR;
+      for (int w = 0; w < 8; ++w) {
+        uint32_t bits = mk[w];
+        while (bits) {
+          const int m = 32 * w + __builtin_ctz(bits);
+          bits &= bits - 1u;
+          row((double)C[m], (double)V[m], tail ? (double)a.open[sd * NBAR + m] : 1.0, true, true, true,
+              m >= 190, m >= 220);
         }
       }
     }
@@ -175,8 +180,8 @@ __global__ __launch_bounds__(256) void k_frame_xday(FrameArgs a) {
 using namespace mff;
 
 extern "C" int mff_stage1_frame(const float* open, const float* close, const uint32_t* volume,
-                                const uint32_t* valid, int S, int D, const int32_t* null_sd,
-                                const uint32_t* null_mask, const uint32_t* null_bits, int K,
+                                const uint32_t* valid, int S, int D, const int32_t* rs_sd,
+                                const int32_t* rs_off, const MffRow* rs_rows, int K,
                                 const int32_t* factor_ids, int nf, double* val, uint8_t* state, void* stream) {
   clear_error();
   MFF_REQUIRE(S > 0 && D > 0 && nf > 0, "mff_stage1_frame: bad sizes S=%d D=%d nf=%d", S, D, nf);
@@ -184,8 +189,8 @@ extern "C" int mff_stage1_frame(const float* open, const float* close, const uin
   FrameArgs a;
   memset(&a, 0, sizeof(a));
   a.open = open; a.close = close; a.volume = volume; a.valid = valid;
-  MFF_REQUIRE(K >= 0 && (K == 0 || (null_sd && null_mask && null_bits)), "mff_stage1_frame: bad null set (K=%d)", K);
-  a.null_sd = null_sd; a.null_mask = null_mask; a.null_bits = null_bits; a.K = K;
+  MFF_REQUIRE(K >= 0 && (K == 0 || (rs_sd && rs_off && rs_rows)), "mff_stage1_frame: bad row set (K=%d)", K);
+  a.rs_sd = rs_sd; a.rs_off = rs_off; a.rs_rows = rs_rows; a.K = K;
   a.val = val; a.state = state; a.S = S; a.D = D;
   a.row_amihud = a.row_prvr = a.row_b20 = a.row_b50 = -1;
   for (int r = 0; r < nf; ++r) {

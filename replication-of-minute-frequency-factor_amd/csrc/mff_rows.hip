@@ -1,25 +1,32 @@
-// mff_nulls.hip — stage 1 for the stock-days that hold polars nulls.
+// mff_rows.hip — stage 1 for the stock-days computed from their own rows (the row set).
 //
-// A day file row may exist with a null open / high / low / close / volume.  That is not a
-// missing bar: the reference's expressions decide what a null does (SURVEY §8(c) S1-S13
-// plus the null rules N1-N11 / C8 of oracle/mff_oracle.py), and only cal_liq_amihud_1min
-// fills a null volume with 0 (CM:743-744):
-//   N1 x op null = null, a null comparison drops the row (filter) or takes otherwise (when)
-//   N2 first() / last() return the row's value, null included (CM:22, 54, 799, 829, 946)
-//   N3 sum / mean / std / skew / kurtosis / product skip nulls (all-null sum 0, mean null)
-//   N4 pl.corr drops a pair with a null side                        (CM:841-931)
-//   N5 pct_change forward-fills, then diff / shift                  (CM:745, 843, 861-866, 929)
-//   N6 shift moves a null with its row                              (CM:899, 913)
-//   N7 top_k / bottom_k prefer non-null values                      (CM:393-471, 1154-1196)
-//   N8 rank() keeps a null key null                                 (CM:1016)
-//   N10 group_by makes one null-key group; C8 it is cum-summed first (CM:948, 1018-1026)
-//   N11 pl.len() counts rows, the rolling var / mean / cov skip nulls (CM:114-129)
-// The ingest (mff/ingest.py) lists those stock-days with their real presence mask and
-// per-field null bits and clears them from the panel's mask, so the fast kernels see
-// them ABSENT (no outputs, no doc_pdf levels); this kernel then computes every requested
-// factor of the listed stock-days.  Null rows are rare (vendor gaps), so the layout is
-// the plain one of the exact kernel (mff_stage1.hip): one wavefront per stock-day, lane l
-// = bars 4l..4l+3, direct stores.
+// The dense panel holds a stock-day as 240 bars on the start-labelled grid 09:30-11:29,
+// 13:00-14:59.  Two kinds of stock-day do not fit it, and the ingest lists them in the
+// panel's row set (include/mff.h MffRow: every row of the stock-day, in (time, frame)
+// order, C4) with their mask words cleared, so the fast kernels see them ABSENT:
+//  * rows that exist with a null open / high / low / close / volume.  That is not a
+//    missing bar: the reference's expressions decide what a null does (SURVEY §8(c)
+//    S1-S13 plus the null rules N1-N11 / C8 of oracle/mff_oracle.py), and only
+//    cal_liq_amihud_1min fills a null volume with 0 (CM:743-744):
+//      N1 x op null = null, a null comparison drops the row (filter) or takes otherwise
+//      N2 first() / last() return the row's value, null included (CM:22, 54, 799, 829, 946)
+//      N3 sum / mean / std / skew / kurtosis / product skip nulls (all-null sum 0, mean null)
+//      N4 pl.corr drops a pair with a null side                        (CM:841-931)
+//      N5 pct_change forward-fills, then diff / shift                  (CM:745, 843, 861-866, 929)
+//      N6 shift moves a null with its row                              (CM:899, 913)
+//      N7 top_k / bottom_k prefer non-null values                      (CM:393-471, 1154-1196)
+//      N8 rank() keeps a null key null                                 (CM:1016)
+//      N10 group_by makes one null-key group; C8 it is cum-summed first (CM:948, 1018-1026)
+//      N11 pl.len() counts rows, the rolling var / mean / cov skip nulls (CM:114-129)
+//  * rows off the grid or at a duplicate time (a 09:25 call-auction bar, a 15:00 closing
+//    bar, end-labelled 09:31..11:30 / 13:01..15:00 bars, times with seconds, two rows at
+//    one time).  The reference computes with whatever `time` a row carries, so this kernel
+//    does too: the time filters on the raw HHMMSSmmm value (CM:18, 33, 49, 69, 84, 770,
+//    784, 815, 1212-1387), minute_in_trade for the 50-minute OLS windows (CM:98-106: on a
+//    duplicate minute every row of the minute shares one window, T1), every other family
+//    over the rows in order.
+// One wavefront per listed stock-day, lane l = rows 4l..4l+3 (at most MFF_ROWS_MAX = 255
+// rows), direct stores: the listed stock-days are rare (vendor gaps and quirks).
 //
 // phase 1: the doc_pdf queries, the stock-day's levels appended to the day's flat list
 //          (non-null keys only, N8) and the NULL placeholders of the doc_pdf rows — after
@@ -35,20 +42,19 @@
 #include "mff_wave.h"
 
 namespace mff {
-namespace nul {
+namespace rws {
 
 constexpr int WPB = 4;  // waves per block
 
 struct Args {
-  const float* fld[5];      // open, high, low, close (fp32), volume (u32) planes [D][S][240]
-  const int32_t* sd_list;   // [K] stock-day indices d*S + s
-  const uint32_t* nmask;    // [K][8] presence words (the panel's own mask is cleared there)
-  const uint32_t* nbits;    // [K][5][8] null bits per field (open, high, low, close, volume)
+  const int32_t* sd_list;  // [K] stock-day indices d*S + s, ascending
+  const int32_t* off;      // [K+1] row offsets
+  const MffRow* rows;      // [off[K]]
   int K;
   double* val;
   uint8_t* state;
-  double* pdfq;             // [5][D][S]
-  uint32_t* lvl_count;      // doc_pdf level side channel (mff_pdf_levels_bytes)
+  double* pdfq;            // [5][D][S]
+  uint32_t* lvl_count;     // doc_pdf level side channel (mff_pdf_levels_bytes)
   uint64_t* lvl_key;
   uint8_t* lvl_w;
   int S, D;
@@ -72,14 +78,12 @@ struct Out {
   __device__ __forceinline__ void null(int f) const { put(f, 0.0, MFF_STATE_NULL); }
 };
 
-__device__ __forceinline__ Bits bits_of(const uint32_t* w) {
-  const int lane = lane_id();
-  const uint32_t mw = lane < 60 ? w[lane >> 3] : 0u;
-  const uint32_t b = (mw >> ((lane & 7) * 4)) & 0xFu;
-  bool f[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) f[k] = (b >> k) & 1u;
-  return ballot4(f);
+// minute_in_trade (CM:98-106): (time // 1e7 * 60 + time % 1e7 / 1e5) cast to Int64, then
+// - 570 before 12:00 and - 660 after.  The true division truncated toward zero is the
+// integer quotient for 0 <= time (a fractional part is >= 1e-5 from the next integer).
+__device__ __forceinline__ int minute_in_trade(int32_t t) {
+  const int te = (t / 10000000) * 60 + (t % 10000000) / 100000;
+  return te < 720 ? te - 570 : te - 660;
 }
 
 // the previous present row's value and flag of x (the row order of a day frame, C4)
@@ -129,14 +133,15 @@ struct Win {  // one OLS window's statistics (ddof = 0), null flags per N11
   bool vxn, vyn, covn;
 };
 
-// CM:114-129: the window (t-50, t] of 50 present minutes; var / mean over the non-null
-// lows / highs, cov over the pairs with both; exact zero for identical values (C3)
-__device__ Win ols_window(const float* lo, const float* hi, const uint8_t* fl, int t) {
+// CM:114-129: the window of rows [r0, r1) (minute_in_trade in (t-50, t]); var / mean
+// over the non-null lows / highs, cov over the pairs with both; exact zero for identical
+// values (C3)
+__device__ Win ols_window(const float* lo, const float* hi, const uint8_t* fl, int r0, int r1) {
   Win w;
   int nx = 0, ny = 0, np_ = 0;
   double x0 = 0.0, y0 = 0.0, px0 = 0.0, py0 = 0.0, sx = 0.0, sy = 0.0, spx = 0.0, spy = 0.0;
   bool cx = true, cy = true, cpx = true, cpy = true;
-  for (int m = t - 49; m <= t; ++m) {
+  for (int m = r0; m < r1; ++m) {
     const bool xo = fl[m] & 1u, yo = fl[m] & 2u;
     const double x = (double)lo[m], y = (double)hi[m];
     if (xo) {
@@ -167,7 +172,7 @@ __device__ Win ols_window(const float* lo, const float* hi, const uint8_t* fl, i
   w.my = ny ? y0 + sy / (double)ny : 0.0;
   const double mpx = np_ ? px0 + spx / (double)np_ : 0.0, mpy = np_ ? py0 + spy / (double)np_ : 0.0;
   double axx = 0.0, ayy = 0.0, axy = 0.0;
-  for (int m = t - 49; m <= t; ++m) {
+  for (int m = r0; m < r1; ++m) {
     const bool xo = fl[m] & 1u, yo = fl[m] & 2u;
     const double x = (double)lo[m], y = (double)hi[m];
     if (xo) axx += (x - w.mx) * (x - w.mx);
@@ -180,81 +185,119 @@ __device__ Win ols_window(const float* lo, const float* hi, const uint8_t* fl, i
   return w;
 }
 
+// first row index in [0, n) whose minute exceeds x (the rows' minutes are non-decreasing:
+// the ingest's contract)
+__device__ __forceinline__ int upper_bound(const int* mi, int n, int x) {
+  int lo = 0, len = n;
+  while (len > 0) {
+    const int half = len >> 1;
+    if (mi[lo + half] <= x) {
+      lo += half + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return lo;
+}
+
 struct Lds {  // per wave
-  uint32_t vw[256];   // volume per bar; 0xffffffff = null
-  float lo[NBAR], hi[NBAR];
-  uint8_t fl[NBAR];   // bit 0 low non-null, bit 1 high non-null (present bars)
+  uint32_t vw[256];   // volume per row; 0xffffffff = null
+  float lo[256], hi[256];
+  int mi[256];        // minute_in_trade per row
+  uint8_t fl[256];    // bit 0 low non-null, bit 1 high non-null
 };
 
 __device__ void stock_day(const Args& a, int i, Lds& L) {
   const int lane = lane_id();
-  const bool lv = lane < 60;
   const uint32_t fam = a.fam;
   const int sdi = __builtin_amdgcn_readfirstlane(a.sd_list[i]);
   const int d = sdi / a.S;
   const size_t sd = (size_t)sdi;
   const Out out{a.val, a.state, a.row, sd, (size_t)a.D * a.S};
-
-  // ---- presence and null bits (N*: per field)
-  const Bits B = bits_of(a.nmask + (size_t)i * 8);
-  Bits NB[5];
-#pragma unroll
-  for (int f = 0; f < 5; ++f) NB[f] = band(bits_of(a.nbits + ((size_t)i * 5 + f) * 8), B);
-  bool p[4], okO[4], okH[4], okL[4], okC[4], okV[4], okR[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    p[k] = mine(B, k);
-    okO[k] = p[k] && !mine(NB[0], k);
-    okH[k] = p[k] && !mine(NB[1], k);
-    okL[k] = p[k] && !mine(NB[2], k);
-    okC[k] = p[k] && !mine(NB[3], k);
-    okV[k] = p[k] && !mine(NB[4], k);
-    okR[k] = okO[k] && okC[k];
-  }
-  const int n = count(B);
+  const int r0 = __builtin_amdgcn_readfirstlane(a.off[i]);
+  int n = __builtin_amdgcn_readfirstlane(a.off[i + 1]) - r0;
+  n = n < 0 ? 0 : n > MFF_ROWS_MAX ? MFF_ROWS_MAX : n;  // the host checks the cap
   if (n == 0) {  // nothing to compute: every output stays ABSENT
     if ((fam & F_PDF) && a.pdfq && lane < 5) a.pdfq[(size_t)lane * a.D * a.S + sd] = qnan();
     return;
   }
+
+  // ---- rows 4 lane + k: time, fields, null bits (N*: per field)
+  int32_t t[4];
+  float o[4], h[4], lo[4], c[4];
+  uint32_t v[4], nb[4];
+  bool p[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = 4 * lane + k;
+    p[k] = e < n;
+    t[k] = 0;
+    o[k] = h[k] = lo[k] = c[k] = 1.0f;
+    v[k] = 0u;
+    nb[k] = 0u;
+    if (p[k]) {
+      const uint4* q = reinterpret_cast<const uint4*>(a.rows + r0 + e);
+      const uint4 x = q[0], y = q[1];
+      t[k] = (int32_t)x.x;
+      o[k] = __uint_as_float(x.y);
+      h[k] = __uint_as_float(x.z);
+      lo[k] = __uint_as_float(x.w);
+      c[k] = __uint_as_float(y.x);
+      v[k] = y.y;
+      nb[k] = y.z;
+    }
+  }
+  bool okO[4], okH[4], okL[4], okC[4], okV[4], okR[4];
+  bool fnO[4], fnC[4], fnV[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    okO[k] = p[k] && !(nb[k] & 1u);
+    okH[k] = p[k] && !(nb[k] & 2u);
+    okL[k] = p[k] && !(nb[k] & 4u);
+    okC[k] = p[k] && !(nb[k] & 8u);
+    okV[k] = p[k] && !(nb[k] & 16u);
+    okR[k] = okO[k] && okC[k];
+    fnO[k] = p[k] && !okO[k];
+    fnC[k] = p[k] && !okC[k];
+    fnV[k] = p[k] && !okV[k];
+  }
+  const Bits B = ballot4(p);
+  const Bits NO = ballot4(fnO), NC = ballot4(fnC), NV = ballot4(fnV);
+  // rows of a time filter, as Bits
+  auto when = [&](auto pred) {
+    bool f[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] = p[k] && pred(t[k]);
+    return ballot4(f);
+  };
   const int mf = first_of(B), ml = last_of(B);
 
-  float o[4], h[4], lo[4], c[4];
-  uint32_t v[4] = {0u, 0u, 0u, 0u};
-  auto load = [&](int f, float (&x)[4]) {
-    float4 t = make_float4(1.f, 1.f, 1.f, 1.f);
-    if (lv) t = reinterpret_cast<const float4*>(a.fld[f] + sd * NBAR)[lane];
-    x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
-  };
-  load(0, o);
-  load(1, h);
-  load(2, lo);
-  load(3, c);
-  if (lv) {
-    const uint4 t = reinterpret_cast<const uint4*>(a.fld[4] + sd * NBAR)[lane];
-    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-  }
   double vd_[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) vd_[k] = okV[k] ? (double)v[k] : 0.0;
   const double sumv = msum(vd_, okV);         // volume.sum(): nulls skipped (N3)
   const int nvok = count(ballot4(okV));
-  const Bits NO = NB[0], NC = NB[3], NV = NB[4];
 
   // ================================================================ SEG CM:10-90
   if (fam & F_SEG) {
-    auto seg = [&](int f, int ma, int mb) {
-      const bool pa = test(B, ma), pbb = test(B, mb);
-      if (!pa && !pbb) return;  // filtered set empty -> absent row
-      const int m0 = pa ? ma : mb, m1 = pbb ? mb : ma;
+    // filter(time in [ta, tb]) -> sort by time (stable: frame order among equal times,
+    // C9) -> close.last() / open.first()
+    auto seg = [&](int f, int32_t ta, int32_t tb) {
+      const Bits SB = when([&](int32_t x) { return x == ta || x == tb; });
+      if (!any(SB)) return;  // filtered set empty -> absent row
+      const int m0 = first_of(SB), m1 = last_of(SB);
       if (test(NC, m1) || test(NO, m0)) out.null(f);  // close.last() / open.first() (N1, N2)
       else out.val1(f, (double)elem(c, m1) / (double)elem(o, m0));
     };
-    seg(0, 120, 239);  // mmt_pm
-    seg(1, 210, 239);  // mmt_last30
-    seg(3, 0, 119);    // mmt_am
-    seg(4, 30, 209);   // mmt_between
-    // mmt_paratio CM:42-60 (C1: PM - AM); a null mmt nulls the difference
-    const Bits am = band(B, range_bits(0, 119)), pm = band(B, range_bits(120, 239));
+    seg(0, 130000000, 145900000);  // mmt_pm       CM:18
+    seg(1, 143000000, 145900000);  // mmt_last30   CM:33
+    seg(3, 93000000, 112900000);   // mmt_am       CM:69
+    seg(4, 100000000, 142900000);  // mmt_between  CM:84
+    // mmt_paratio CM:42-60: am_0_pm_1 = time <= 11:30:00 (CM:49); C1: PM - AM; a null
+    // mmt nulls the difference
+    const Bits am = when([](int32_t x) { return x <= 113000000; });
+    const Bits pm = when([](int32_t x) { return !(x <= 113000000); });
     double g[2];
     bool gn[2];
     int ng = 0;
@@ -342,20 +385,18 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
 
   // ================================================================ SUMV CM:764-831, 1251-1306
   if (fam & F_SUMV) {
-    const int l4 = 4 * lane;
     bool pre[4], cls[4], head[4], tail[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int m = l4 + k;
-      pre[k] = okV[k] && m <= 236;
-      cls[k] = okV[k] && m >= 237;
-      head[k] = okV[k] && m <= 30;
-      tail[k] = okV[k] && m >= 210;
+      pre[k] = okV[k] && t[k] < 145700000;    // CM:770
+      cls[k] = okV[k] && t[k] >= 145700000;   // CM:784, 815
+      head[k] = okV[k] && t[k] <= 100000000;  // CM:1256
+      tail[k] = okV[k] && t[k] >= 143000000;  // CM:1285
     }
     const double spre = msum(vd_, pre), scls = msum(vd_, cls);
     const double shead = msum(vd_, head), stail = msum(vd_, tail);
-    if (any(band(B, range_bits(0, 236)))) out.val1(28, spre);    // liq_closeprevol
-    if (any(band(B, range_bits(237, 239)))) out.val1(29, scls);  // liq_closevol
+    if (any(when([](int32_t x) { return x < 145700000; }))) out.val1(28, spre);    // liq_closeprevol
+    if (any(when([](int32_t x) { return x >= 145700000; }))) out.val1(29, scls);  // liq_closevol
     if (test(NV, mf)) {  // volume.first() is null (N2)
       out.null(30);
       out.null(32);
@@ -456,15 +497,13 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
 
   // ================================================================ TRD CM:1206-1406
   if (fam & F_TRD) {
-    const int l4 = 4 * lane;
     bool t20[4], t50[4], h20[4], h50[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int m = l4 + k;
-      t20[k] = p[k] && m >= 220;
-      t50[k] = p[k] && m >= 190;
-      h20[k] = p[k] && m <= 20;
-      h50[k] = p[k] && m <= 50;
+      t20[k] = p[k] && t[k] >= 144000000;  // CM:1212
+      t50[k] = p[k] && t[k] >= 141000000;  // CM:1233
+      h20[k] = p[k] && t[k] <= 95000000;   // CM:1315, 1359, 1387
+      h50[k] = p[k] && t[k] <= 102000000;  // CM:1337
     }
     auto tail = [&](const bool (&tm)[4], int f, bool plus_one) {
       bool tv[4], tb[4];
@@ -480,11 +519,11 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
       for (int k = 0; k < 4; ++k) tmp[k] = (vd_[k] / den) * r[k];
       out.val1(f, msum(tmp, tb));
     };
-    if (any(band(B, range_bits(220, 239)))) tail(t20, 50, true);   // trade_bottom20retRatio
-    if (any(band(B, range_bits(190, 239)))) tail(t50, 51, false);  // trade_bottom50retRatio
+    if (any(ballot4(t20))) tail(t20, 50, true);   // trade_bottom20retRatio
+    if (any(ballot4(t50))) tail(t50, 51, false);  // trade_bottom50retRatio
     // trade_top{20,50}retRatio, topNeg20, topPos20: mean over the non-null quotients (N3)
-    auto headf = [&](const bool (&hm)[4], int lo_, int hi_, int f_all, int f_neg, int f_pos) {
-      if (!any(band(B, range_bits(lo_, hi_)))) return;
+    auto headf = [&](const bool (&hm)[4], int f_all, int f_neg, int f_pos) {
+      if (!any(ballot4(hm))) return;
       bool hv[4], ha[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -513,8 +552,8 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
         }
       }
     };
-    headf(h20, 0, 20, 54, 56, 57);
-    headf(h50, 0, 50, 55, -1, -1);
+    headf(h20, 54, 56, 57);
+    headf(h50, 55, -1, -1);
   }
 
   // ================================================================ ORD / ORDV (N7)
@@ -572,7 +611,7 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
     // key = close.last() / close: null when the close is null or close.last() is (N2);
     // the null group sorts first (high word 0: C8), then ascending key = descending close
     const bool lastnull = test(NC, ml);
-    if (lv) {
+    {
       uint4 w;
       w.x = okV[0] ? v[0] : 0xffffffffu;
       w.y = okV[1] ? v[1] : 0xffffffffu;
@@ -665,6 +704,7 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
           if (emit[k]) {
             const size_t at = inA[k] ? (size_t)idxA++ : cap - 1 - (size_t)idxB++;
             a.lvl_key[(size_t)d * cap + at] = lkey[k];
+            // rows at the level (<= MFF_ROWS_MAX = 255: fits the weight byte)
             a.lvl_w[(size_t)d * cap + at] = (uint8_t)(l4 + k - (hpp[k] ? (int)ppos[k] : -1));
           }
       }
@@ -675,34 +715,34 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
       int est[5];
       bool need_seq = false;
 #pragma unroll
-      for (int t = 0; t < 5; ++t) {
+      for (int q = 0; q < 5; ++q) {
         if (nvok == 0) {  // every share null: level sums 0, no level passes
-          est[t] = -1;
+          est[q] = -1;
           continue;
         }
         if (sumv == 0.0) {  // shares NaN on levels with a non-null volume; NaN > p (S11)
-          est[t] = first_of(ballot4(lhas));
+          est[q] = first_of(ballot4(lhas));
           continue;
         }
         bool ps[4], ts[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const double lhs = 20.0 * cum[k], rhs = kk[t] * sumv;
+          const double lhs = 20.0 * cum[k], rhs = kk[q] * sumv;
           ps[k] = lend[k] && lhs > rhs;
           ts[k] = lend[k] && lhs == rhs;
         }
         const int ep = first_of(ballot4(ps));
         const int et = first_of(ballot4(ts));
-        est[t] = ep;
+        est[q] = ep;
         if (et >= 0 && (ep < 0 || et < ep)) need_seq = true;
       }
       if (need_seq) {
         // an exact tie: the reference's float sequence (level sums of the non-null shares
-        // in bar order, cum-summed in level order, compared with p as f64)
+        // in row order, cum-summed in level order, compared with p as f64)
         double VD = 0.0, cs = 0.0;
         int done = 0;
 #pragma unroll
-        for (int t = 0; t < 5; ++t) est[t] = -1;
+        for (int q = 0; q < 5; ++q) est[q] = -1;
         for (int e = 0; e < n; ++e) {
           const uint64_t ke = elem(key, e);
           const uint32_t w = L.vw[(uint32_t)ke & 0xffu];
@@ -712,9 +752,9 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
             cs = cs + VD;
             VD = 0.0;
 #pragma unroll
-            for (int t = 0; t < 5; ++t)
-              if (est[t] < 0 && tot_gt(cs, pp[t])) {
-                est[t] = e;
+            for (int q = 0; q < 5; ++q)
+              if (est[q] < 0 && tot_gt(cs, pp[q])) {
+                est[q] = e;
                 ++done;
               }
             if (done == 5) break;
@@ -723,17 +763,17 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
       }
       double qv = qnan();
 #pragma unroll
-      for (int t = 0; t < 5; ++t) {
-        double q = qnan();  // no level passes, or the null level does (sort() puts it first)
-        if (est[t] >= 0) {
-          const uint32_t hk = (uint32_t)(elem(key, est[t]) >> 32);
-          if (hk != 0u) q = cl / (double)bitsf(~hk);
+      for (int q = 0; q < 5; ++q) {
+        double qq = qnan();  // no level passes, or the null level does (sort() puts it first)
+        if (est[q] >= 0) {
+          const uint32_t hk = (uint32_t)(elem(key, est[q]) >> 32);
+          if (hk != 0u) qq = cl / (double)bitsf(~hk);
         }
-        if (lane == t) qv = q;
+        if (lane == q) qv = qq;
       }
       if (lane < 5) a.pdfq[(size_t)lane * a.D * a.S + sd] = qv;
 #pragma unroll
-      for (int t = 0; t < 5; ++t) out.null(PDF0 + t);  // filled by the doc_pdf finalize
+      for (int q = 0; q < 5; ++q) out.null(PDF0 + q);  // filled by the doc_pdf finalize
     }
     if (fam & F_LVL) {
       double xl[4];
@@ -748,55 +788,58 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
       out.val1(40, sk);  // doc_skew
       out.val1(41, sk);  // doc_std: .skew() [sic CM:999]
     }
+    __builtin_amdgcn_wave_barrier();
   }
 
-  // ================================================================ OLS CM:93-376 (N11)
+  // ================================================================ OLS CM:93-376 (N11, T1)
   if (fam & F_OLS) {
-    if (lv) {
+    int mi[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        L.lo[4 * lane + k] = lo[k];
-        L.hi[4 * lane + k] = h[k];
-        L.fl[4 * lane + k] = (uint8_t)((okL[k] ? 1u : 0u) | (okH[k] ? 2u : 0u));
+    for (int k = 0; k < 4; ++k) {
+      mi[k] = minute_in_trade(t[k]);
+      const int e = 4 * lane + k;
+      if (p[k]) {
+        L.lo[e] = lo[k];
+        L.hi[e] = h[k];
+        L.mi[e] = mi[k];
+        L.fl[e] = (uint8_t)((okL[k] ? 1u : 0u) | (okH[k] ? 2u : 0u));
       }
     }
     __builtin_amdgcn_wave_barrier();
-    // window t: a row at t and all of t-49..t present (pl.len() = 50 rows, CM:129)
-    uint32_t pc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) pc[k] = p[k] ? 1u : 0u;
-    scan4_u32(pc);
+    // rolling(index_column='minute_in_trade', period='50i') (CM:114-118): the window of
+    // row r holds every row whose minute is in (m_r - 50, m_r], the rows of m_r that come
+    // after r included (polars' look-behind windows consume duplicate index values: T1);
+    // pl.len() >= 50 rows (CM:129)
     double beta[4], q[4], cs[4], cr[4];
     bool okw[4], okb[4], okq[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int t = 4 * lane + k;
-      const int src = (k < 2) ? lane - 13 : lane - 12;  // element t-50 at (src, k +- 2)
-      const int ks = (k < 2) ? k + 2 : k - 2;
-      uint32_t b = bperm(src < 0 ? 0 : src, ks == 0 ? pc[0] : ks == 1 ? pc[1] : ks == 2 ? pc[2] : pc[3]);
-      if (t - 50 < 0) b = 0u;
-      okw[k] = lv && p[k] && t >= 49 && pc[k] - b == 50u;
       beta[k] = q[k] = cs[k] = cr[k] = 0.0;
-      okb[k] = okq[k] = false;
-      if (okw[k]) {
-        const Win w = ols_window(L.lo, L.hi, L.fl, t);
-        // CM:131-134: when(var_x != 0) cov / var_x, otherwise mean_y / mean_x (null cond
-        // or null operand: N1)
-        if (!w.vxn && w.vx != 0.0) {
-          okb[k] = !w.covn;
-          beta[k] = w.cov / w.vx;
-        } else {
-          okb[k] = !w.vxn && !w.vyn;
-          beta[k] = w.my / w.mx;
+      okb[k] = okq[k] = okw[k] = false;
+      if (p[k]) {
+        const int w1 = upper_bound(L.mi, n, mi[k]);
+        const int w0 = upper_bound(L.mi, n, mi[k] - 50);
+        okw[k] = w1 - w0 >= 50;
+        if (okw[k]) {
+          const Win w = ols_window(L.lo, L.hi, L.fl, w0, w1);
+          // CM:131-134: when(var_x != 0) cov / var_x, otherwise mean_y / mean_x (null
+          // cond or null operand: N1)
+          if (!w.vxn && w.vx != 0.0) {
+            okb[k] = !w.covn;
+            beta[k] = w.cov / w.vx;
+          } else {
+            okb[k] = !w.vxn && !w.vyn;
+            beta[k] = w.my / w.mx;
+          }
+          const double prod = w.vx * w.vy;
+          okq[k] = !w.vxn && !w.vyn && prod != 0.0 && !w.covn;
+          if (okq[k]) {
+            q[k] = sqrt(w.cov) / prod;      // cov**0.5 / (vx*vy)   CM:137
+            cs[k] = (w.cov * w.cov) / prod;  // cov**2 / (vx*vy)     CM:212
+            cr[k] = w.cov / sqrt(prod);      // cov / (vx*vy)**0.5   CM:261
+          }
+          if (!okb[k]) beta[k] = 0.0;
         }
-        const double prod = w.vx * w.vy;
-        okq[k] = !w.vxn && !w.vyn && prod != 0.0 && !w.covn;
-        if (okq[k]) {
-          q[k] = sqrt(w.cov) / prod;      // cov**0.5 / (vx*vy)   CM:137
-          cs[k] = (w.cov * w.cov) / prod;  // cov**2 / (vx*vy)     CM:212
-          cr[k] = w.cov / sqrt(prod);      // cov / (vx*vy)**0.5   CM:261
-        }
-        if (!okb[k]) beta[k] = 0.0;
       }
     }
     const Bits WB = ballot4(okw);
@@ -831,14 +874,75 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_stage1_nulls(Args a) {
+__global__ __launch_bounds__(256) void k_stage1_rows(Args a) {
   __shared__ Lds lds[WPB];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = gridDim.x * WPB;
   for (int i = blockIdx.x * WPB + wave; i < a.K; i += nw) stock_day(a, i, lds[wave]);
 }
 
-}  // namespace nul
+// ---------------------------------------------------------------- grid stock-days -> rows
+struct GatherArgs {
+  const float* fld[5];
+  const uint32_t* valid;
+  const int32_t* sd_list;
+  const uint32_t* null_bits;  // [K][5][8] or null
+  int K;
+  const int32_t* off;  // [K+1] or null (count mode)
+  int32_t* counts;     // count mode: [K]
+  MffRow* rows;
+};
+
+// start label HHMMSSmmm of grid minute m (09:30 + m, 13:00 + m - 120)
+__device__ __forceinline__ int32_t minute_time(int m) {
+  const int clock = m < 120 ? 570 + m : 780 + (m - 120);
+  return (clock / 60) * 10000000 + (clock % 60) * 100000;
+}
+
+__global__ __launch_bounds__(256) void k_rows_from_panel(GatherArgs a) {
+  const int lane = lane_id();
+  const int nw = gridDim.x * WPB;
+  for (int i = blockIdx.x * WPB + (int)(threadIdx.x >> 6); i < a.K; i += nw) {
+    const size_t sd = (size_t)a.sd_list[i];
+    const uint32_t* mk = a.valid + sd * 8;
+    // lane l: bars 4l..4l+3 (lanes 60..63 none)
+    const uint32_t mw = lane < 60 ? mk[lane >> 3] : 0u;
+    const uint32_t b4 = (mw >> ((lane & 7) * 4)) & 0xFu;
+    if (!a.rows) {
+      const uint32_t c = wsum_u32((uint32_t)__popc(b4));
+      if (lane == 0) a.counts[i] = (int32_t)c;
+      continue;
+    }
+    uint32_t nb4[5];
+#pragma unroll
+    for (int f = 0; f < 5; ++f) {
+      const uint32_t w = (a.null_bits && lane < 60) ? a.null_bits[((size_t)i * 5 + f) * 8 + (lane >> 3)] : 0u;
+      nb4[f] = (w >> ((lane & 7) * 4)) & 0xFu;
+    }
+    const uint32_t incl = wscan_incl_u32((uint32_t)__popc(b4));
+    uint32_t at = (uint32_t)a.off[i] + incl - (uint32_t)__popc(b4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!((b4 >> k) & 1u)) continue;
+      const int m = 4 * lane + k;
+      MffRow r;
+      r.time = minute_time(m);
+      r.open = a.fld[0][sd * NBAR + m];
+      r.high = a.fld[1][sd * NBAR + m];
+      r.low = a.fld[2][sd * NBAR + m];
+      r.close = a.fld[3][sd * NBAR + m];
+      r.volume = reinterpret_cast<const uint32_t*>(a.fld[4])[sd * NBAR + m];
+      uint32_t nbits = 0u;
+#pragma unroll
+      for (int f = 0; f < 5; ++f) nbits |= ((nb4[f] >> k) & 1u) << f;
+      r.nulls = nbits;
+      r.reserved = 0u;
+      a.rows[at++] = r;
+    }
+  }
+}
+
+}  // namespace rws
 
 size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w);
 
@@ -846,29 +950,24 @@ size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w);
 
 using namespace mff;
 
-extern "C" int mff_stage1_nulls(const float* open, const float* high, const float* low, const float* close,
-                                const uint32_t* volume, int S, int D, const int32_t* null_sd,
-                                const uint32_t* null_mask, const uint32_t* null_bits, int K,
-                                const int32_t* factor_ids, int nf, double* val, uint8_t* state,
-                                double* pdf_query, void* pdf_levels, int phase, void* stream) {
+extern "C" int mff_stage1_rows(int S, int D, const int32_t* rs_sd, const int32_t* rs_off, const MffRow* rs_rows,
+                               int K, const int32_t* factor_ids, int nf, double* val, uint8_t* state,
+                               double* pdf_query, void* pdf_levels, int phase, void* stream) {
   clear_error();
-  MFF_REQUIRE(S > 0 && D > 0 && (long long)S * D < (1ll << 31), "mff_stage1_nulls: bad sizes S=%d D=%d", S, D);
-  MFF_REQUIRE(K >= 0, "mff_stage1_nulls: K=%d", K);
-  MFF_REQUIRE(phase >= 1 && phase <= 3, "mff_stage1_nulls: phase=%d must be 1, 2 or 3", phase);
-  MFF_REQUIRE(nf > 0 && nf <= NF && factor_ids, "mff_stage1_nulls: bad factor list");
+  MFF_REQUIRE(S > 0 && D > 0 && (long long)S * D < (1ll << 31), "mff_stage1_rows: bad sizes S=%d D=%d", S, D);
+  MFF_REQUIRE(K >= 0, "mff_stage1_rows: K=%d", K);
+  MFF_REQUIRE(phase >= 1 && phase <= 3, "mff_stage1_rows: phase=%d must be 1, 2 or 3", phase);
+  MFF_REQUIRE(nf > 0 && nf <= NF && factor_ids, "mff_stage1_rows: bad factor list");
   if (K == 0) return 0;
-  MFF_REQUIRE(open && high && low && close && volume && null_sd && null_mask && null_bits && val && state,
-              "mff_stage1_nulls: NULL buffer");
-  nul::Args a;
+  MFF_REQUIRE(rs_sd && rs_off && rs_rows && val && state, "mff_stage1_rows: NULL buffer");
+  rws::Args a;
   memset(&a, 0, sizeof(a));
-  a.fld[0] = open; a.fld[1] = high; a.fld[2] = low; a.fld[3] = close;
-  a.fld[4] = reinterpret_cast<const float*>(volume);
-  a.sd_list = null_sd; a.nmask = null_mask; a.nbits = null_bits; a.K = K;
+  a.sd_list = rs_sd; a.off = rs_off; a.rows = rs_rows; a.K = K;
   a.val = val; a.state = state; a.S = S; a.D = D;
   for (int i = 0; i < NF; ++i) a.row[i] = -1;
   for (int r = 0; r < nf; ++r) {
     const int id = factor_ids[r];
-    MFF_REQUIRE(id >= 0 && id < NF, "mff_stage1_nulls: factor id %d out of range", id);
+    MFF_REQUIRE(id >= 0 && id < NF, "mff_stage1_rows: factor id %d out of range", id);
     a.row[id] = (int8_t)r;
     a.fam |= kFactorFamily[id];
   }
@@ -876,7 +975,7 @@ extern "C" int mff_stage1_nulls(const float* open, const float* high, const floa
   if (phase == 2) a.fam &= ~F_PDF;
   if (!a.fam) return 0;
   if (a.fam & F_PDF) {
-    MFF_REQUIRE(pdf_query && pdf_levels, "mff_stage1_nulls: doc_pdf needs pdf_query and pdf_levels");
+    MFF_REQUIRE(pdf_query && pdf_levels, "mff_stage1_rows: doc_pdf needs pdf_query and pdf_levels");
     size_t ok, ow;
     pdf_levels_split(S, D, &ok, &ow);
     char* base = reinterpret_cast<char*>(pdf_levels);
@@ -885,8 +984,30 @@ extern "C" int mff_stage1_nulls(const float* open, const float* high, const floa
     a.lvl_key = reinterpret_cast<uint64_t*>(base + ok);
     a.lvl_w = reinterpret_cast<uint8_t*>(base + ow);
   }
-  const int blocks = (K + nul::WPB - 1) / nul::WPB < 4096 ? (K + nul::WPB - 1) / nul::WPB : 4096;
-  hipLaunchKernelGGL(nul::k_stage1_nulls, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+  const int blocks = (K + rws::WPB - 1) / rws::WPB < 4096 ? (K + rws::WPB - 1) / rws::WPB : 4096;
+  hipLaunchKernelGGL(rws::k_stage1_rows, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+  MFF_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int mff_rows_from_panel(const float* open, const float* high, const float* low, const float* close,
+                                   const uint32_t* volume, const uint32_t* valid, int S, int D,
+                                   const int32_t* sd, const uint32_t* null_bits, int K, const int32_t* off,
+                                   int32_t* counts, MffRow* rows, void* stream) {
+  clear_error();
+  MFF_REQUIRE(S > 0 && D > 0 && K >= 0, "mff_rows_from_panel: bad sizes S=%d D=%d K=%d", S, D, K);
+  if (K == 0) return 0;
+  MFF_REQUIRE(valid && sd, "mff_rows_from_panel: NULL mask / stock-day list");
+  MFF_REQUIRE(rows ? (off && open && high && low && close && volume) : (counts != nullptr),
+              "mff_rows_from_panel: rows need off and the five planes; count mode needs counts");
+  rws::GatherArgs a;
+  memset(&a, 0, sizeof(a));
+  a.fld[0] = open; a.fld[1] = high; a.fld[2] = low; a.fld[3] = close;
+  a.fld[4] = reinterpret_cast<const float*>(volume);
+  a.valid = valid; a.sd_list = sd; a.null_bits = null_bits; a.K = K; a.off = off; a.counts = counts;
+  a.rows = rows;
+  const int blocks = (K + rws::WPB - 1) / rws::WPB < 4096 ? (K + rws::WPB - 1) / rws::WPB : 4096;
+  hipLaunchKernelGGL(rws::k_rows_from_panel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
   MFF_LAUNCH_CHECK();
   return 0;
 }

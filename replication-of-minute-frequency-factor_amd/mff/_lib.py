@@ -37,7 +37,8 @@ SIGNATURES = {
     "mff_pdf_count_frame": (c_int, [P, c_int, c_int, P, c_int, P, P]),
     "mff_pdf_finalize": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, IP, P, P, P]),
     "mff_pdf_rank_local": (c_int, [P, P, c_int, c_int, c_int, c_int, P, c_int, IP, P, P, P]),
-    "mff_stage1_nulls": (c_int, [P, P, P, P, P, c_int, c_int, P, P, P, c_int, IP, c_int, P, P, P, P, c_int, P]),
+    "mff_stage1_rows": (c_int, [c_int, c_int, P, P, P, c_int, IP, c_int, P, P, P, P, c_int, P]),
+    "mff_rows_from_panel": (c_int, [P, P, P, P, P, P, c_int, c_int, P, P, c_int, P, P, P, P]),
     "mff_stage1_frame": (c_int, [P, P, P, P, c_int, c_int, P, P, P, c_int, IP, c_int, P, P, P]),
     "mff_pdf_origin_counts": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P, P]),
     "mff_pdf_finalize_own": (c_int, [P, P, c_int, c_int, IP, P, P, P]),

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib, catalog
-from .synth import null_set, pack_mask, stack_fields
+from .synth import ROW_DTYPE, pack_mask, row_set, stack_fields
 
 ABSENT, NULL, VALUE = 0, 1, 2
 VOLUME_MAX = 2 ** 32 - 2  # MFF_VOLUME_MAX: u32 shares per bar (all-ones = absent sort key)
@@ -33,41 +33,77 @@ def _stream(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+ROWS_MAX = 255  # MFF_ROWS_MAX
+
+
 @dataclass
-class NullSet:
-    """The stock-days of a panel that hold polars nulls (rows that exist with a null
-    field), in the layout of ``mff_stage1_nulls`` (include/mff.h): ``sd`` int32 [K]
-    (d*S + s, ascending), ``mask`` int32 [K][8] their presence words (the panel's own mask
-    holds zeros there), ``bits`` int32 [K][5][8] null bits of open, high, low, close,
-    volume.  All on the panel's device."""
+class RowSet:
+    """The stock-days of a panel computed from their own rows (include/mff.h, row set):
+    those holding a polars null (a row that exists with a null field) and those with a row
+    off the 240-bar grid or at a duplicate time.  ``sd`` int32 [K] (d*S + s, ascending),
+    ``off`` int32 [K+1], ``rows`` the MffRow records (32 B each, a uint8 tensor [R*32]) in
+    (time, frame) order per stock-day.  The panel's own mask holds zeros there.  All on the
+    panel's device."""
 
     sd: torch.Tensor
-    mask: torch.Tensor
-    bits: torch.Tensor
+    off: torch.Tensor
+    rows: torch.Tensor
 
     @property
     def K(self) -> int:
         return int(self.sd.numel())
 
     @classmethod
-    def from_host(cls, sd, mask, bits, device) -> Optional["NullSet"]:
+    def from_host(cls, sd, off, rows, device) -> Optional["RowSet"]:
+        """sd int [K], off int [K+1], rows ROW_DTYPE [R] numpy -> device (None when K = 0)."""
         if len(sd) == 0:
             return None
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(device)
-        return cls(t(np.asarray(sd, np.int32)), t(np.asarray(mask, np.uint32)), t(np.asarray(bits, np.uint32)))
+        rows = np.ascontiguousarray(rows, dtype=ROW_DTYPE)
+        t = lambda a_: torch.from_numpy(np.ascontiguousarray(a_, dtype=np.int32)).to(device)
+        return cls(t(sd), t(off), torch.from_numpy(rows.view(np.uint8).reshape(-1).copy()).to(device))
 
     def host(self):
-        """(sd int64, mask uint32 [K][8], bits uint32 [K][5][8]) numpy copies."""
-        return (self.sd.cpu().numpy().astype(np.int64), self.mask.cpu().numpy().view(np.uint32),
-                self.bits.cpu().numpy().view(np.uint32))
+        """(sd int64 [K], off int64 [K+1], rows ROW_DTYPE [R]) numpy copies."""
+        return (self.sd.cpu().numpy().astype(np.int64), self.off.cpu().numpy().astype(np.int64),
+                self.rows.cpu().numpy().view(ROW_DTYPE).copy())
 
-    def shard(self, S: int, s0: int, s1: int, device=None) -> Optional["NullSet"]:
-        """The null stock-days of stocks [s0, s1) re-indexed to a shard of S1 - s0 stocks."""
-        sd, mask, bits = self.host()
+    def shard(self, S: int, s0: int, s1: int, device=None) -> Optional["RowSet"]:
+        """The listed stock-days of stocks [s0, s1) re-indexed to a shard of s1 - s0 stocks."""
+        sd, off, rows = self.host()
         d, s = sd // S, sd % S
-        keep = (s >= s0) & (s < s1)
+        keep = np.flatnonzero((s >= s0) & (s < s1))
         nsd = d[keep] * (s1 - s0) + (s[keep] - s0)
-        return NullSet.from_host(nsd.astype(np.int32), mask[keep], bits[keep], device or self.sd.device)
+        parts = [rows[off[i]:off[i + 1]] for i in keep]
+        n = np.array([len(x) for x in parts], dtype=np.int64)
+        noff = np.concatenate([[0], np.cumsum(n)])
+        nrows = np.concatenate(parts) if parts else np.zeros(0, ROW_DTYPE)
+        return RowSet.from_host(nsd, noff, nrows, device or self.sd.device)
+
+    @classmethod
+    def from_panel(cls, bars: torch.Tensor, mask: torch.Tensor, sd: torch.Tensor,
+                   null_bits: Optional[torch.Tensor] = None, clear: bool = True) -> "RowSet":
+        """List the grid stock-days ``sd`` (int32 device tensor, ascending) of a device panel
+        as rows (mff_rows_from_panel), with optional null bits int32 [K][5][8]; ``clear``:
+        zero their mask words (the grid kernels then see them ABSENT)."""
+        lib = _lib.load()
+        D, S = int(bars.shape[1]), int(bars.shape[2])
+        K = int(sd.numel())
+        dev = bars.device
+        st = _stream(dev)
+        counts = torch.empty(K, dtype=torch.int32, device=dev)
+        b = bars
+        _lib.check(lib.mff_rows_from_panel(None, None, None, None, None, _lib.ptr(mask), S, D, _lib.ptr(sd),
+                                           None, K, None, _lib.ptr(counts), None, st), "mff_rows_from_panel(count)")
+        off = torch.zeros(K + 1, dtype=torch.int32, device=dev)
+        off[1:] = torch.cumsum(counts, 0)
+        R = int(off[-1].item())
+        rows = torch.empty(max(R, 1) * ROW_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        _lib.check(lib.mff_rows_from_panel(_lib.ptr(b[0]), _lib.ptr(b[1]), _lib.ptr(b[2]), _lib.ptr(b[3]),
+                                           _lib.ptr(b[4]), _lib.ptr(mask), S, D, _lib.ptr(sd), _lib.ptr(null_bits),
+                                           K, _lib.ptr(off), None, _lib.ptr(rows), st), "mff_rows_from_panel")
+        if clear:
+            mask.view(-1, 8)[sd.long()] = 0
+        return cls(sd, off, rows)
 
 
 @dataclass
@@ -77,8 +113,9 @@ class DevicePanel:
     bars: [5][D][S][240] 4-byte words: open, high, low, close (float32) and the volume
           plane's u32 shares (include/mff.h); a float32 tensor, plane 4 viewed as ints
     mask: int32 [D][S][8] presence bits (bit m%32 of word m//32); zero for the stock-days
-          listed in ``nulls``
-    nulls: the stock-days that hold polars nulls (computed by mff_stage1_nulls), or None
+          listed in ``rows``
+    rows: the row set -- the stock-days computed from their own rows (nulls, rows off the
+          grid or at a duplicate time; mff_stage1_rows), or None
     """
 
     bars: torch.Tensor
@@ -88,7 +125,7 @@ class DevicePanel:
     # ingest with skip_bad: {input table index: reason} of the tables dropped (their days
     # hold no bars)
     dropped: dict = field(default_factory=dict)
-    nulls: Optional[NullSet] = None
+    rows: Optional[RowSet] = None
     # stock-sharded panels: the number of stocks over all ranks (shards by
     # dist.shard_bounds), so the exchange's padded shard width is known without a
     # collective; None = agree on it with one all-reduce
@@ -116,12 +153,12 @@ class DevicePanel:
         validate_host_panel(panel)
         bars = torch.from_numpy(np.ascontiguousarray(stack_fields(panel))).to(device)
         words = pack_mask(panel["present"])
-        sd, nmask, nbits = null_set(panel)
-        if sd.size:  # the null-holding stock-days go to mff_stage1_nulls only
+        sd, off, rows = row_set(panel)
+        if sd.size:  # the listed stock-days go to mff_stage1_rows only
             words.reshape(-1, 8)[sd] = 0
         mask = torch.from_numpy(words.view(np.int32)).to(device)
         return cls(bars, mask, list(panel["codes"]), list(panel["dates"]),
-                   nulls=NullSet.from_host(sd, nmask, nbits, device))
+                   rows=RowSet.from_host(sd, off, rows, device))
 
 
 def validate_host_panel(panel) -> None:
@@ -172,18 +209,18 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
     if frame_pdf and comm is not None:
         raise ValueError("frame-wide doc_pdf ranks of a multi-date frame are single-GPU; "
                          "shard day files (per-day semantics) instead")
-    nl = panel.nulls
+    rs = panel.rows
 
-    def nulls_phase(phase: int, stream) -> None:
-        """mff_stage1_nulls for the null-holding stock-days (ABSENT to every other launch):
+    def rows_phase(phase: int, stream) -> None:
+        """mff_stage1_rows for the row set's stock-days (ABSENT to every other launch):
         phase 1 = doc_pdf queries + levels (before the doc_pdf sort), 2 = the other rows
         (after every launch that writes them)."""
-        if nl is None or (phase == 1 and not need_pdf):
+        if rs is None or (phase == 1 and not need_pdf):
             return
-        _lib.check(lib.mff_stage1_nulls(*args[:5], S, D, _lib.ptr(nl.sd), _lib.ptr(nl.mask), _lib.ptr(nl.bits),
-                                        nl.K, _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
-                                        _lib.ptr(pdfq), _lib.ptr(levels), phase, stream.cuda_stream),
-                   f"mff_stage1_nulls({phase})")
+        _lib.check(lib.mff_stage1_rows(S, D, _lib.ptr(rs.sd), _lib.ptr(rs.off), _lib.ptr(rs.rows), rs.K,
+                                       _lib.int_array(ids), nf, _lib.ptr(val), _lib.ptr(state),
+                                       _lib.ptr(pdfq), _lib.ptr(levels), phase, stream.cuda_stream),
+                   f"mff_stage1_rows({phase})")
 
     if events is not None:
         events[0].record(main)
@@ -204,7 +241,7 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
         if PDF_FIRST:
             # the doc_pdf phases (whole-CU workgroups) on the launch stream before part 2:
             # behind the wave-pair kernel they only get CUs its blocks have drained
-            nulls_phase(1, main)
+            rows_phase(1, main)
             pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
             if hl is not None and HL_AT == "pdf":
                 launch_hl()
@@ -214,7 +251,7 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             side.wait_stream(main)
             if EXACT_SIDE:  # the exact list kernel ahead of the doc_pdf phases, off the launch stream
                 _lib.check(lib.mff_stage1_part(*(args[:-1] + [side.cuda_stream]), 32), "mff_stage1_part(32)")
-            nulls_phase(1, side)
+            rows_phase(1, side)
             sorted_ev = torch.cuda.Event() if SORT_FIRST else None
             with torch.cuda.stream(side):
                 pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch,
@@ -230,17 +267,17 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             launch_hl()
         if hl is not None:
             main.wait_stream(hl)
-        nulls_phase(2, main)
+        rows_phase(2, main)
         if events is not None:  # after the doc_pdf tail on the side stream
             events[1].record(main)
         return val, state, ids
     _lib.check(lib.mff_stage1(*args), "mff_stage1")
-    nulls_phase(1, main)
+    rows_phase(1, main)
     if frame_pdf:
         pdf_ranks_frame(panel, pdfq, levels, rows, val, state)
     elif need_pdf:
         pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
-    nulls_phase(2, main)
+    rows_phase(2, main)
     if events is not None:
         events[1].record(main)
     return val, state, ids
@@ -292,13 +329,13 @@ def stage1_frame(panel: DevicePanel, ids: Sequence[int], val, state) -> None:
     """Overwrite the rows of the four factors whose windows run over('code') only
     (liq_amihud_1min, corr_prvr, trade_bottom20/50retRatio) with the semantics of ONE
     reference call on the panel's multi-date frame (mff_stage1_frame, csrc/mff_frame.hip),
-    null-holding stock-days included."""
+    row-set stock-days included."""
     lib = _lib.load()
-    b, nl = panel.bars, panel.nulls
+    b, rs = panel.bars, panel.rows
     _lib.check(lib.mff_stage1_frame(_lib.ptr(b[0]), _lib.ptr(b[3]), _lib.ptr(b[4]), _lib.ptr(panel.mask),
-                                    panel.S, panel.D, _lib.ptr(nl.sd) if nl else None,
-                                    _lib.ptr(nl.mask) if nl else None, _lib.ptr(nl.bits) if nl else None,
-                                    nl.K if nl else 0, _lib.int_array(list(ids)), len(ids), _lib.ptr(val),
+                                    panel.S, panel.D, _lib.ptr(rs.sd) if rs else None,
+                                    _lib.ptr(rs.off) if rs else None, _lib.ptr(rs.rows) if rs else None,
+                                    rs.K if rs else 0, _lib.int_array(list(ids)), len(ids), _lib.ptr(val),
                                     _lib.ptr(state), _stream(panel.device)), "mff_stage1_frame")
 
 

@@ -9,9 +9,10 @@ converts between the two.
 
 * Input frames may be pandas DataFrames, pyarrow Tables, dicts of arrays, or any object
   with ``to_arrow()`` (e.g. a polars DataFrame, when polars is installed).
-* Bars must sit on the 240-bar grid 09:30-11:29, 13:00-14:59 (start-labelled, the grid
-  the reference's time filters assume: CM:18,33,69,84 and minute_in_trade CM:98-106);
-  anything else raises ValueError, as do duplicate (code, date, time) rows.
+* Bars on the 240-bar grid 09:30-11:29, 13:00-14:59 (start-labelled) fill the dense
+  panel; a stock-day with a row off it (09:25, 15:00, end-labelled bars, seconds) or two
+  rows at one time keeps all its rows in the row set (:func:`listed_rows`), computed on
+  each row's own time like the reference (CM:18-84, 98-106, 770-815, 1212-1387).
 * Rows are taken in (code, time) order, the frame order the reference relies on (C4).
 * Output values use pandas' pyarrow-backed float64 so polars null (pd.NA) and NaN stay
   distinct.
@@ -25,6 +26,8 @@ import numpy as np
 
 MINUTES = 240
 FIELDS = ("open", "high", "low", "close", "volume")
+ROWS_MAX = 255  # MFF_ROWS_MAX: rows of one stock-day of the row set
+TIME_END = 240000000  # times are HHMMSSmmm of one day
 
 
 def time_to_minute(time: np.ndarray) -> np.ndarray:
@@ -33,8 +36,82 @@ def time_to_minute(time: np.ndarray) -> np.ndarray:
     hh, mm, rest = t // 10000000, (t // 100000) % 100, t % 100000
     clock = hh * 60 + mm
     m = np.where(clock < 720, clock - 570, clock - 660)
-    ok = (rest == 0) & (((clock >= 570) & (clock < 690)) | ((clock >= 780) & (clock < 900)))
+    ok = (rest == 0) & (mm < 60) & (((clock >= 570) & (clock < 690)) | ((clock >= 780) & (clock < 900)))
     return np.where(ok, m, -1)
+
+
+def listed_rows(cols, S: int, D: int, counted=None):
+    """The row set of one table (include/mff.h): the stock-days with a null field, a row off
+    the 240-bar grid (a time that is not a 09:30-11:29 / 13:00-14:59 minute start) or two
+    rows at one time, and all their rows in (time, frame) order (C4: rows at one time keep
+    the push's order).  Returns (cells int64 [K] = d*S + s ascending, off int64 [K+1], rows
+    ROW_DTYPE [R], internal duplicate rows, irregular bool [K] = the stock-day has a row off
+    the grid or a duplicate time, not only nulls).  ``cols``: (stock, day, time, 4 price
+    arrays, volume, null bits uint8) per row (ingest's encoding).  ``counted``: the kernel's (off-grid, duplicate)
+    counts for the push; more duplicates there than inside the push = rows of another
+    table at the same (code, date, time).  Raises ValueError on an input-contract error of
+    a listed stock-day (include/mff.h: a null or out-of-day time, more than MFF_ROWS_MAX
+    rows, minute_in_trade decreasing -- a row inside the lunch break before an afternoon
+    row, which the reference's rolling() rejects as unsorted -- or a bad price / volume)."""
+    from .synth import ROW_DTYPE
+
+    stock, day, time, px, vol, nb = cols
+    stock = np.asarray(stock)
+    day = np.asarray(day)
+    time = np.asarray(time, dtype=np.int64)
+    ok = (stock >= 0) & (stock < S) & (day >= 0) & (day < D)
+    cell = day.astype(np.int64) * S + stock
+    minute = time_to_minute(time)
+    offg = ok & (minute < 0)
+    on = np.flatnonzero(ok & (minute >= 0))
+    key = cell[on] * 240 + minute[on]
+    order = np.argsort(key, kind="stable")
+    ks = key[order]
+    same = np.flatnonzero(ks[1:] == ks[:-1])
+    ndup = int(same.size)
+    dupc = np.unique(np.concatenate([ks[same], ks[same + 1]]) // 240) if ndup else np.zeros(0, np.int64)
+    if counted is not None:
+        if int(counted[0]) != int(offg.sum()):
+            raise ValueError(f"internal: {int(counted[0])} off-grid rows counted on the device, "
+                             f"{int(offg.sum())} on the host")
+        if int(counted[1]) > ndup:
+            raise ValueError("duplicate (code, date, time) rows across tables")
+    listed = np.unique(np.concatenate([cell[offg], dupc, cell[ok & (nb != 0)]]))
+    irregular = np.isin(listed, np.concatenate([cell[offg], dupc]))
+    if listed.size == 0:
+        return listed, np.zeros(1, np.int64), np.zeros(0, ROW_DTYPE), ndup, irregular
+    sel = np.flatnonzero(ok & np.isin(cell, listed))
+    t = time[sel]
+    if ((t < 0) | (t >= TIME_END)).any():
+        raise ValueError("time must be a non-null HHMMSSmmm in [0, 240000000) on rows off the grid")
+    idx = sel[np.lexsort((sel, t, cell[sel]))]  # (cell, time, frame order)
+    c = cell[idx]
+    n = np.bincount(np.searchsorted(listed, c), minlength=listed.size)
+    if n.max() > ROWS_MAX:
+        raise ValueError(f"a stock-day with nulls or rows off the grid holds more than {ROWS_MAX} rows")
+    te = (time[idx] // 10000000) * 60 + (time[idx] % 10000000) // 100000
+    mi = np.where(te < 720, te - 570, te - 660)
+    if ((np.diff(mi) < 0) & (c[1:] == c[:-1])).any():
+        raise ValueError("minute_in_trade decreases inside a stock-day (a row inside the 11:30-13:00 "
+                         "break before an afternoon row): the reference's rolling() rejects it")
+    rows = np.zeros(idx.size, ROW_DTYPE)
+    rows["time"] = time[idx]
+    nbi = nb[idx]
+    for i, k in enumerate(FIELDS[:4]):
+        x = px[i][idx]
+        nn = (nbi >> i) & 1 == 0
+        if not (np.isfinite(x[nn]) & (x[nn] > 0) & (x[nn] <= 3.4028234663852886e38)).all():
+            raise ValueError("prices must be finite and > 0")
+        rows[k] = np.where(nn, x, 1.0).astype(np.float32)
+    v = np.asarray(vol[idx], dtype=np.float64)
+    vn = (nbi >> 4) & 1 == 0
+    if not ((v[vn] >= 0) & (v[vn] <= 2 ** 32 - 2) & (v[vn] == np.rint(v[vn]))).all():
+        raise ValueError("volume must be integral and within [0, 2**32 - 2] shares")
+    rows["volume"] = np.where(vn, v, 0.0).astype(np.uint32)
+    rows["nulls"] = nbi
+    off = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
+    return listed, off, rows, ndup, irregular
+
 
 
 def minute_to_time(m: np.ndarray) -> np.ndarray:
@@ -63,6 +140,8 @@ def _columns(df):
         if col.null_count and n in FIELDS:
             nulls[n] = np.asarray(col.is_null().to_numpy(zero_copy_only=False), dtype=bool)
             col = pc.fill_null(col.cast(pa.float64()), 0.0 if n == "volume" else 1.0)
+        elif col.null_count and n == "time":  # a null time: -1, an input-contract error
+            col = pc.fill_null(col.cast(pa.int64()), -1)
         vals[n] = col.to_numpy(zero_copy_only=False)
     return vals, nulls
 
@@ -84,43 +163,65 @@ def _as_date(x):
 def to_dense(df, codes: Sequence[str] | None = None) -> Dict:
     """Long frame -> host panel dict (see mff.synth): float32 price planes and a float64
     volume plane [D][S][240], present mask, sorted codes and dates; ``null`` (uint8
-    [D][S][240], bit i = FIELDS[i]) when a row holds a polars null (values there NaN)."""
+    [D][S][240], bit i = FIELDS[i]) when a row holds a polars null (values there NaN);
+    ``extra`` = (sd, off, rows) (see :func:`mff.synth.row_set`) for the stock-days with a
+    row off the 240-bar grid or two rows at one time -- every row of those stock-days, in
+    (time, frame) order, none of them on the grid (the host restatement of the ingest's
+    row set, :func:`listed_rows`)."""
     cols, nulls = _columns(df)
     for k in ("code", "date", "time") + FIELDS:
         if k not in cols:
             raise ValueError(f"missing column {k!r}")
     code = np.asarray(cols["code"]).astype(str)
     date = np.array([_as_date(x) for x in cols["date"]], dtype=object)
-    minute = time_to_minute(cols["time"])
-    if (minute < 0).any():
-        bad = np.asarray(cols["time"])[minute < 0][:5]
-        raise ValueError(f"bars off the 240-minute grid (time={bad.tolist()})")
+    time = np.asarray(cols["time"], dtype=np.int64)
+    minute = time_to_minute(time)
     ucodes = sorted(set(code.tolist())) if codes is None else list(codes)
     udates = sorted(set(date.tolist()))
     ci = {c: i for i, c in enumerate(ucodes)}
     di = {d: i for i, d in enumerate(udates)}
-    s = np.fromiter((ci[c] for c in code), dtype=np.int64, count=code.size)
+    s = np.fromiter((ci.get(c, -1) for c in code), dtype=np.int64, count=code.size)
     d = np.fromiter((di[x] for x in date), dtype=np.int64, count=date.size)
+    if (s < 0).any():
+        raise ValueError("stock/day index out of range")
     D, S = len(udates), len(ucodes)
-    flat = (d * S + s) * MINUTES + minute
-    if np.unique(flat).size != flat.size:
-        raise ValueError("duplicate (code, date, time) rows")
+    nb = np.zeros(code.size, np.uint8)
+    for i, k in enumerate(FIELDS):
+        if k in nulls:
+            nb |= nulls[k].astype(np.uint8) << i
+    px = [np.asarray(cols[k], dtype=np.float64) for k in FIELDS[:4]]
+    vol = np.asarray(cols["volume"], dtype=np.float64)
+    cells, off, rows, _, irr = listed_rows((s, d, time, px, vol, nb), S, D)
+    cell = d * S + s
+    grid = ~np.isin(cell, cells[irr])
+    for i in range(4):  # the engine's contract on the grid rows (nulls aside)
+        x = px[i][grid & ((nb >> i) & 1 == 0)]
+        if not (np.isfinite(x) & (x > 0)).all():
+            raise ValueError("prices must be finite and > 0")
+    x = vol[grid & ((nb >> 4) & 1 == 0)]
+    if not ((x >= 0) & (x <= 2 ** 32 - 2) & (x == np.rint(x))).all():
+        raise ValueError("volume must be integral and within [0, 2**32 - 2] shares")
+    flat = cell[grid] * MINUTES + minute[grid]
     panel = {}
     for k in FIELDS:  # prices fp32 like the device planes; volume f64 (u32 shares on the device)
         dt_ = np.float64 if k == "volume" else np.float32
         arr = np.full(D * S * MINUTES, np.nan, dtype=dt_)
-        arr[flat] = np.asarray(cols[k], dtype=np.float64).astype(dt_)
+        arr[flat] = np.asarray(cols[k], dtype=np.float64)[grid].astype(dt_)
         panel[k] = arr.reshape(D, S, MINUTES)
     pres = np.zeros(D * S * MINUTES, dtype=bool)
     pres[flat] = True
     panel["present"] = pres.reshape(D, S, MINUTES)
     if nulls:
-        nb = np.zeros(D * S * MINUTES, dtype=np.uint8)
+        nbg = np.zeros(D * S * MINUTES, dtype=np.uint8)
+        nbg[flat] = nb[grid]
         for i, k in enumerate(FIELDS):
-            if k in nulls:
-                nb[flat[nulls[k]]] |= np.uint8(1 << i)
-                panel[k].reshape(-1)[flat[nulls[k]]] = np.nan
-        panel["null"] = nb.reshape(D, S, MINUTES)
+            panel[k].reshape(-1)[flat[(nb[grid] >> i) & 1 == 1]] = np.nan
+        panel["null"] = nbg.reshape(D, S, MINUTES)
+    if irr.any():
+        keep = np.flatnonzero(irr)
+        parts = [rows[off[i]:off[i + 1]] for i in keep]
+        panel["extra"] = (cells[keep], np.concatenate([[0], np.cumsum([p.size for p in parts])]),
+                          np.concatenate(parts))
     panel["codes"] = ucodes
     panel["dates"] = udates
     return panel

@@ -81,8 +81,8 @@ def _numeric(col, dtype, fill=float("nan")):
 def _volume(col):
     """Volume column -> (values, MFF_VOLUME_* kind, null mask or None).  A null volume is
     NOT 0 shares: polars keeps it null everywhere except cal_liq_amihud_1min's
-    fill_null(0) (CM:743-744), so the row's null bit travels to mff_stage1_nulls; the
-    value under it is 0 (never read as a volume)."""
+    fill_null(0) (CM:743-744), so the row's null bit travels to the row set
+    (mff_stage1_rows); the value under it is 0 (never read as a volume)."""
     import pyarrow.compute as pc
 
     col = _one(col)
@@ -201,9 +201,11 @@ def _encode_batch(t, codes, vs, uday, pos=None):
     else:
         day = np.searchsorted(uday, dn).astype(np.int32)
         day[(day >= uday.size) | (uday[np.minimum(day, uday.size - 1)] != dn)] = -1
-    time, tnull = _numeric(t.column("time"), np.int64, fill=-1)  # a null time is off the grid
+    # a null time is -1: off the grid for the kernel, an input-contract error for the row
+    # set (_listed_rows)
+    time, tnull = _numeric(t.column("time"), np.int64, fill=-1)
     # a null price is 1.0 for the ingest kernel's contract check; its null bit (bit i of
-    # the row's byte = FIELDS[i]) keeps it out of every factor (mff_stage1_nulls)
+    # the row's byte = FIELDS[i]) lists the stock-day in the row set (mff_stage1_rows)
     px, nulls = [], []
     for k in FIELDS[:4]:
         x, isn = _numeric(t.column(k), np.float64, fill=1.0)
@@ -271,6 +273,21 @@ def encode(t, codes: Sequence[str], day_numbers: Sequence[int]):
     return cat(0), cat(1), cat(2), px, cat(4), bs[0][5], nb
 
 
+from .frames import ROWS_MAX, listed_rows  # noqa: E402  (host-only row-set restatement)
+
+
+def _cat_batches(batches):
+    """Encoded record batches of one push -> one tuple of concatenated arrays."""
+    if len(batches) == 1:
+        b = batches[0]
+        nb = b[6] if b[6] is not None else np.zeros(b[0].size, np.uint8)
+        return b[0], b[1], b[2], b[3], b[4], nb
+    cat = lambda j: np.concatenate([b[j] for b in batches])
+    px = [np.concatenate([b[3][i] for b in batches]) for i in range(4)]
+    nb = np.concatenate([b[6] if b[6] is not None else np.zeros(b[0].size, np.uint8) for b in batches])
+    return cat(0), cat(1), cat(2), px, cat(4), nb
+
+
 class PanelIngest:
     """Fill one dense device panel [5][D][S][240] + mask [D][S][8] from long tables.
 
@@ -279,12 +296,13 @@ class PanelIngest:
     counters (raising ValueError like :func:`frames.to_dense`) and returns the
     :class:`mff.engine.DevicePanel`.
 
-    Rows with a null field are ingested like any other (the null price as 1.0, the null
-    volume as 0 shares) and their (stock, day, minute, null bits) are kept on the host;
-    ``finish()`` turns them into the panel's :class:`mff.engine.NullSet` (the stock-days'
-    presence words and null bits) and clears those stock-days from the mask, so the fast
-    kernels see them ABSENT and ``mff_stage1_nulls`` computes them with polars' null
-    rules."""
+    Stock-days that do not fit the 240-bar grid -- a row with a null field, a row off the
+    grid (09:25, 15:00, end-labelled bars, seconds), two rows at one time -- go to the
+    panel's row set (:class:`mff.engine.RowSet`, computed by ``mff_stage1_rows`` with
+    polars' null rules and each row's own time): the kernel counts off-grid and duplicate
+    rows, ``finish()`` re-reads only the pushes that have such rows or nulls (their source
+    tables are kept until then), lists those stock-days with all their rows and clears them
+    from the mask, so the fast kernels see them ABSENT."""
 
     ERR_CHUNK = 64  # error-counter rows per device allocation (one row per push)
 
@@ -306,7 +324,8 @@ class PanelIngest:
         # a caller can drop exactly the bad push's cells whatever the number of pushes)
         self._err: List[torch.Tensor] = []
         self.table_cells: List[Optional[np.ndarray]] = []  # stock-day cells each push wrote
-        self._null_rows: List[tuple] = []  # (sd int64, minute int64, bits uint8) per push
+        self._src: list = []    # per push: its source table or encoded batches (row set re-read)
+        self._nulls: List[bool] = []  # per push: it holds a null field
         self.stream = torch.cuda.Stream(self.dev)
         self.stream.wait_stream(torch.cuda.current_stream(self.dev))  # zero fills first
         self.slots = [None] * slots  # (pinned, device, event)
@@ -336,7 +355,8 @@ class PanelIngest:
         return s
 
     def push(self, df) -> None:
-        self.push_encoded(encode_batches(_table(df), self.codes, self.day_numbers, self.vs, self.pos))
+        t = _table(df)
+        self.push_encoded(encode_batches(t, self.codes, self.day_numbers, self.vs, self.pos), source=t)
 
     def _cells(self, batches) -> np.ndarray:
         """The in-range (day * S + stock) cells a push writes, ascending."""
@@ -347,32 +367,27 @@ class PanelIngest:
             seen = np.zeros(self.S, dtype=bool)  # a day file: one day, mark its stocks
             for b in batches:
                 st = b[0]
-                seen[st[st >= 0]] = True
+                seen[st[(st >= 0) & (st < self.S)]] = True
             return next(iter(days)) * self.S + np.flatnonzero(seen).astype(np.int64)
         cells = []
         for b in batches:
-            ok = (b[0] >= 0) & (b[1] >= 0)
+            ok = (b[0] >= 0) & (b[1] >= 0) & (b[0] < self.S) & (b[1] < self.D)
             cells.append(b[1][ok].astype(np.int64) * self.S + b[0][ok])
         return np.unique(np.concatenate(cells)) if cells else np.zeros(0, np.int64)
 
-    def push_encoded(self, enc) -> None:
+    def push_encoded(self, enc, source=None) -> None:
         """Stage and launch one table already encoded by :func:`encode` (one tuple) or
         :func:`encode_batches` (a list of record-batch tuples: each copied straight into
-        the pinned staging slot, no concatenation)."""
+        the pinned staging slot, no concatenation).  ``source``: the pyarrow table it was
+        encoded from, re-read by ``finish()`` if the push holds rows for the row set (else
+        the encoded batches themselves are kept for that)."""
         batches = [enc] if isinstance(enc, tuple) else list(enc)
         n = int(sum(b[0].size for b in batches))
         k = len(self.table_cells)
         err = self._err_row(k)
         self.table_cells.append(self._cells(batches) if n else np.zeros(0, np.int64))
-        from .frames import time_to_minute
-        for stock, day, time, _, _, _, nbits in batches:
-            if nbits is None:
-                continue
-            r = np.flatnonzero((nbits != 0) & (stock >= 0) & (day >= 0))
-            if r.size:
-                m = time_to_minute(time[r])
-                on = m >= 0  # off-grid rows are counted as errors by the kernel
-                self._null_rows.append(((day[r].astype(np.int64) * self.S + stock[r])[on], m[on], nbits[r][on]))
+        self._src.append(source if source is not None else batches)
+        self._nulls.append(any(b[6] is not None and bool((b[6] != 0).any()) for b in batches))
         if n == 0:
             return
         kind = batches[0][5]
@@ -403,36 +418,26 @@ class PanelIngest:
     def skip_table(self, k: int) -> None:
         """Record a table that could not be pushed (its encode raised): nothing staged."""
         self.table_cells.append(np.zeros(0, dtype=np.int64))
+        self._src.append(None)
+        self._nulls.append(False)
 
-    def _null_set(self, dropped_cells: np.ndarray):
-        """Host null rows -> (sd, bits uint32 [K][5][8]) of the null-holding stock-days,
-        without the cells of dropped pushes."""
-        if not self._null_rows:
-            return None
-        sd = np.concatenate([x[0] for x in self._null_rows])
-        m = np.concatenate([x[1] for x in self._null_rows])
-        nb = np.concatenate([x[2] for x in self._null_rows])
-        if dropped_cells.size:
-            keep = ~np.isin(sd, dropped_cells)
-            sd, m, nb = sd[keep], m[keep], nb[keep]
-        if sd.size == 0:
-            return None
-        usd, inv = np.unique(sd, return_inverse=True)
-        bits = np.zeros((usd.size, 5, 8), np.uint32)
-        for i in range(5):
-            r = np.flatnonzero((nb >> i) & 1)
-            np.bitwise_or.at(bits[:, i, :], (inv[r], m[r] // 32), (np.uint32(1) << (m[r] % 32).astype(np.uint32)))
-        return usd, bits
+    def _batches(self, k: int):
+        src = self._src[k]
+        if isinstance(src, list):
+            return src
+        return encode_batches(src, self.codes, self.day_numbers, self.vs, self.pos)
 
     def finish(self, skip_bad: bool = False):
-        """Check the per-push error counters and return the DevicePanel.
+        """Check the per-push error counters, build the row set and return the DevicePanel.
 
         A push breaking the input contract raises ValueError (naming the push's index when
         there were several) unless ``skip_bad``: then the stock-day cells that push wrote
         are dropped from the panel (their presence bits cleared: ABSENT, no rows, as when
-        the reference's per-file call fails, MinuteFrequentFactorCICC.py:18-25, 95) and the
-        reasons are returned in ``panel.dropped`` {push index: message}."""
-        from .engine import DevicePanel, NullSet
+        the reference's per-file call fails, MinuteFrequentFactorCICC.py:18-25, 95) -- only
+        those cells: another table's cells of the same date stay -- and the reasons are
+        returned in ``panel.dropped`` {push index: message}."""
+        from .engine import DevicePanel, RowSet
+        from .synth import ROW_DTYPE
 
         torch.cuda.current_stream(self.dev).wait_stream(self.stream)
         npush = len(self.table_cells)
@@ -440,28 +445,56 @@ class PanelIngest:
                else np.zeros((0, 5), np.int32))  # synchronises the caller's stream
         dropped = {}
         for k in range(err.shape[0]):
-            bad = [f"{ERRORS[i]} ({int(err[k, i])} rows)" for i in range(5) if err[k, i]]
+            # off-grid and duplicate rows (counters 1, 2) are no error: the row set takes them
+            bad = [f"{ERRORS[i]} ({int(err[k, i])} rows)" for i in (0, 3, 4) if err[k, i]]
             if bad:
                 dropped[k] = "; ".join(bad)
+        listed = {}  # push -> (cells, off, rows)
+        for k in range(npush):
+            if k in dropped or not (self._nulls[k] or err[k, 1] or err[k, 2]):
+                continue
+            try:
+                cells, off, rows, _, _ = listed_rows(_cat_batches(self._batches(k)), self.S, self.D,
+                                                     counted=err[k, 1:3])
+            except ValueError as e:
+                dropped[k] = str(e)
+                continue
+            if cells.size:
+                listed[k] = (cells, off, rows)
+        # a listed stock-day's rows must come from one table
+        for k, (cells, _, _) in list(listed.items()):
+            for j in range(npush):
+                if j != k and j not in dropped and np.isin(cells, self.table_cells[j]).any():
+                    dropped[max(j, k)] = ("rows of a stock-day with nulls or rows off the grid are split "
+                                          f"across tables {min(j, k)} and {max(j, k)}")
+        for k in list(listed):
+            if k in dropped:
+                del listed[k]
         if dropped and not skip_bad:
             if npush == 1:
                 raise ValueError(dropped[0])
             raise ValueError("; ".join(f"table {k}: {m}" for k, m in sorted(dropped.items())))
+        self._src = [None] * npush  # release the source tables
         cells = [self.table_cells[k] for k in dropped if self.table_cells[k] is not None]
         dcells = np.unique(np.concatenate(cells)) if cells else np.zeros(0, np.int64)
         flat = self.mask.view(-1, 8)
         if dcells.size:
             flat[torch.as_tensor(dcells, device=self.dev)] = 0
-        nulls = None
-        ns = self._null_set(dcells)
-        if ns is not None:
-            usd, bits = ns
-            idx = torch.as_tensor(usd, device=self.dev)
-            nmask = flat[idx].cpu().numpy().view(np.uint32)  # the stock-days' real presence
-            flat[idx] = 0  # ... which only mff_stage1_nulls sees
-            nulls = NullSet.from_host(usd.astype(np.int32), nmask, bits, self.dev)
+        rs = None
+        if listed:
+            parts = [listed[k] for k in sorted(listed)]
+            sd = np.concatenate([p[0] for p in parts])
+            rows = np.concatenate([p[2] for p in parts]) if parts else np.zeros(0, ROW_DTYPE)
+            n = np.concatenate([np.diff(p[1]) for p in parts])
+            order = np.argsort(sd, kind="stable")
+            starts = np.concatenate([[0], np.cumsum(n)])[:-1]
+            rows = np.concatenate([rows[starts[i]:starts[i] + n[i]] for i in order])
+            sd, n = sd[order], n[order]
+            off = np.concatenate([[0], np.cumsum(n)])
+            flat[torch.as_tensor(sd, device=self.dev)] = 0  # only mff_stage1_rows sees them
+            rs = RowSet.from_host(sd, off, rows, self.dev)
         dates = [_EPOCH + _dt.timedelta(days=x) for x in self.day_numbers]
-        dp = DevicePanel(self.bars, self.mask, self.codes, dates, nulls=nulls)
+        dp = DevicePanel(self.bars, self.mask, self.codes, dates, rows=rs)
         dp.dropped = dropped
         return dp
 
@@ -480,10 +513,11 @@ def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None, skip_
 
     ``skip_bad`` (the reference driver's per-file error semantics,
     MinuteFrequentFactorCICC.py:18-25, 95): a table that cannot be read as a day frame or
-    breaks the input contract (include/mff.h: bars on the 240-minute grid, no duplicate
-    bars, prices finite > 0, volume integral in range) is dropped with every day it
-    touches -- its stock-days come out ABSENT -- and ``panel.dropped`` maps the table's
-    index in ``tables`` to the reason.  Otherwise the first such table raises ValueError."""
+    breaks the input contract (include/mff.h: prices finite > 0, volume integral in range,
+    non-null times; see :func:`listed_rows` for the rows off the grid) is dropped -- the
+    stock-day cells it wrote come out ABSENT, another table's cells of the same date stay
+    -- and ``panel.dropped`` maps the table's index in ``tables`` to the reason.
+    Otherwise the first such table raises ValueError."""
     from concurrent.futures import ThreadPoolExecutor
 
     raw = list(tables) if isinstance(tables, (list, tuple)) else [tables]
@@ -538,7 +572,7 @@ def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None, skip_
                 dropped[keep[j]] = msg
                 ing.skip_table(j)
             else:
-                ing.push_encoded(enc)
+                ing.push_encoded(enc, source=tabs[j])
             futs[j] = None
     with _timing.phase("read + encode + H2D + ingest"):
         dp = ing.finish(skip_bad=skip_bad)

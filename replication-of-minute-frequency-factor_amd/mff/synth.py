@@ -153,22 +153,59 @@ def unpack_mask(words: np.ndarray) -> np.ndarray:
 FIELDS = ("open", "high", "low", "close", "volume")
 
 
-def null_set(panel: Dict):
-    """The stock-days of a host panel that hold a polars null (``panel["null"]``: optional
-    uint8 [D][S][240], bit i = FIELDS[i] null on a present bar) in the layout of
-    ``mff_stage1_nulls`` (include/mff.h): (sd int32 [K] = d*S + s ascending, presence
-    words uint32 [K][8], null bits uint32 [K][5][8])."""
+ROW_DTYPE = np.dtype([("time", "<i4"), ("open", "<f4"), ("high", "<f4"), ("low", "<f4"), ("close", "<f4"),
+                      ("volume", "<u4"), ("nulls", "<u4"), ("reserved", "<u4")])  # include/mff.h MffRow
+
+
+def minute_time(m: np.ndarray) -> np.ndarray:
+    """Grid minute 0..239 -> HHMMSSmmm start label (09:30 + m, 13:00 + m - 120)."""
+    m = np.asarray(m, dtype=np.int64)
+    clock = np.where(m < 120, 570 + m, 780 + (m - 120))
+    return (clock // 60) * 10000000 + (clock % 60) * 100000
+
+
+def grid_rows(panel: Dict, d: int, s: int) -> np.ndarray:
+    """The present bars of grid stock-day (d, s) as MffRow records (minute order)."""
+    pres = panel["present"][d, s]
+    m = np.flatnonzero(pres)
+    r = np.zeros(m.size, ROW_DTYPE)
+    r["time"] = minute_time(m)
+    for k in FIELDS[:4]:
+        r[k] = np.asarray(panel[k][d, s, m], dtype=np.float32)
+    r["volume"] = volume_u32(panel["volume"][d, s, m])
+    nb = panel.get("null")
+    if nb is not None:
+        r["nulls"] = nb[d, s, m]
+    return r
+
+
+def row_set(panel: Dict):
+    """The row set of a host panel (include/mff.h): the stock-days that hold a polars null
+    (``panel["null"]``: optional uint8 [D][S][240], bit i = FIELDS[i] null on a present bar)
+    as their grid rows, plus the stock-days of ``panel["extra"]`` -- (sd [K], off [K+1],
+    rows ROW_DTYPE [R]) whose rows do not fit the grid (their ``present`` bars must be
+    empty) -- merged by d*S + s.  Returns (sd int32 [K] ascending, off int32 [K+1], rows)."""
     pres = panel["present"]
     D, S = pres.shape[:2]
+    parts = {}
     nb = panel.get("null")
-    if nb is None:
-        return (np.zeros(0, np.int32), np.zeros((0, 8), np.uint32), np.zeros((0, 5, 8), np.uint32))
-    nb = np.where(pres, nb, 0).astype(np.uint8)
-    d, s = np.nonzero((nb != 0).any(axis=2))
-    sd = (d.astype(np.int64) * S + s).astype(np.int32)
-    mask = pack_mask(pres[d, s])
-    bits = np.stack([pack_mask(((nb[d, s] >> i) & 1).astype(bool)) for i in range(5)], axis=1)
-    return sd, mask.reshape(-1, 8), bits.reshape(-1, 5, 8)
+    if nb is not None:
+        nb = np.where(pres, nb, 0).astype(np.uint8)
+        d, s = np.nonzero((nb != 0).any(axis=2))
+        for dd, ss in zip(d.tolist(), s.tolist()):
+            parts[dd * S + ss] = grid_rows(panel, dd, ss)
+    ex = panel.get("extra")
+    if ex is not None:
+        esd, eoff, erows = ex
+        for i, x in enumerate(np.asarray(esd, dtype=np.int64).tolist()):
+            if pres.reshape(-1, pres.shape[-1])[x].any():
+                raise ValueError(f"stock-day {x} is both on the grid and in panel['extra']")
+            parts[x] = np.asarray(erows[eoff[i]:eoff[i + 1]], dtype=ROW_DTYPE)
+    sd = np.array(sorted(parts), dtype=np.int64)
+    n = np.array([parts[x].size for x in sd.tolist()], dtype=np.int64)
+    off = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
+    rows = np.concatenate([parts[x] for x in sd.tolist()]) if sd.size else np.zeros(0, ROW_DTYPE)
+    return sd.astype(np.int32), off.astype(np.int32), rows
 
 
 def add_nulls(panel: Dict, seed: int = 0, rate: float = 0.002, patterns: bool = True) -> Dict:
@@ -332,3 +369,81 @@ def make_ragged_device(bars, mask, g, day_chunk: int = 50) -> None:
             for k in range(4):
                 bars[k, d0 + fd, fs, :] = px[:, None]
             bars[4, d0 + fd, fs, :] = 0.0  # the bits of 0 shares
+
+
+IRREGULAR_KINDS = ("call_0925", "close_1500", "end_labelled", "seconds", "duplicates", "dup_and_null",
+                   "lunch_1130", "sparse_offgrid")
+
+
+def irregular_day_frames(panel: Dict, seed: int = 0, per_kind: int = 2):
+    """Long day frames (pandas, one per day) of a host panel with stock-days whose rows do
+    not fit the 240-bar grid -- the reference computes with whatever ``time`` a row
+    carries (CM:18-84, 98-106, 770-815, 1212-1387).  ``per_kind`` stock-days per kind of
+    IRREGULAR_KINDS:
+      call_0925      a 09:25:00 call-auction row before the first bar
+      close_1500     a 15:00:00 closing row after the last bar
+      end_labelled   every bar labelled by its END (09:31..11:30, 13:01..15:00)
+      seconds        times with seconds / milliseconds (09:30:03.000, ...)
+      duplicates     ten bars repeated right after themselves with other values
+      dup_and_null   duplicates whose copies hold a null close / volume
+      lunch_1130     an 11:30:00 row (minute_in_trade 120, like 13:00)
+      sparse_offgrid a handful of rows, all off the grid
+    Rows of a code are in (time, frame) order (C4).  Returns a list of D frames."""
+    import pandas as pd
+
+    rng = np.random.Generator(np.random.PCG64(seed))
+    pres = panel["present"]
+    D, S = pres.shape[:2]
+    cand = [(d, s) for d in range(D) for s in range(S) if pres[d, s].sum() >= 60]
+    pick = rng.permutation(len(cand))
+    kind_of = {}
+    j = 0
+    for kind in IRREGULAR_KINDS:
+        for _ in range(per_kind):
+            if j < len(cand):
+                kind_of[cand[pick[j]]] = kind
+                j += 1
+    frames_ = []
+    for d in range(D):
+        parts = []
+        for s in range(S):
+            m = np.flatnonzero(pres[d, s])
+            if m.size == 0:
+                continue
+            t = minute_time(m)
+            cols = {k: np.asarray(panel[k][d, s, m], dtype=np.float64) for k in FIELDS}
+            kind = kind_of.get((d, s))
+            if kind == "call_0925":
+                t = np.concatenate([[92500000], t])
+                cols = {k: np.concatenate([[x[0] if k != "volume" else 12300.0], x]) for k, x in cols.items()}
+            elif kind == "close_1500":
+                t = np.concatenate([t, [150000000]])
+                cols = {k: np.concatenate([x, [x[-1] if k != "volume" else 45600.0]]) for k, x in cols.items()}
+            elif kind == "end_labelled":
+                t = t + 100000
+                t = np.where(t % 10000000 == 6000000, t - 6000000 + 10000000, t)  # hh:60 -> (hh+1):00
+            elif kind == "seconds":
+                t = t + rng.integers(0, 60, size=t.size) * 1000 + rng.integers(0, 1000, size=t.size)
+            elif kind in ("duplicates", "dup_and_null"):
+                rep = np.sort(rng.choice(m.size, size=min(10, m.size), replace=False))
+                idx = np.sort(np.concatenate([np.arange(m.size), rep]), kind="stable")
+                t = t[idx]
+                cols = {k: x[idx].copy() for k, x in cols.items()}
+                second = np.concatenate([[False], idx[1:] == idx[:-1]])
+                cols["close"][second] = np.round(cols["close"][second] * 1.01, 2).astype(np.float32)
+                cols["volume"][second] = cols["volume"][second] + 100.0
+                if kind == "dup_and_null":
+                    w = np.flatnonzero(second)
+                    cols["close"][w[::2]] = np.nan
+                    cols["volume"][w[1::2]] = np.nan
+            elif kind == "lunch_1130":
+                t = np.concatenate([t[t < 113000000], [113000000], t[t >= 113000000]])
+                at = int(np.searchsorted(minute_time(m), 113000000))
+                cols = {k: np.insert(x, at, x[max(at - 1, 0)]) for k, x in cols.items()}
+            elif kind == "sparse_offgrid":
+                keep = np.sort(rng.choice(m.size, size=7, replace=False))
+                t = t[keep] + 30000  # hh:mm:30
+                cols = {k: x[keep] for k, x in cols.items()}
+            parts.append(pd.DataFrame({"code": panel["codes"][s], "date": panel["dates"][d], "time": t, **cols}))
+        frames_.append(pd.concat(parts, ignore_index=True) if parts else None)
+    return frames_, kind_of

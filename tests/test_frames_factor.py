@@ -34,13 +34,24 @@ def test_time_grid_roundtrip_and_validation():
     assert (frames.time_to_minute(frames.minute_to_time(m)) == m).all()
     assert (frames.minute_to_time(m) == O.minute_to_time(m)).all()
     assert list(frames.time_to_minute(np.array([113000000, 150000000, 93000500]))) == [-1, -1, -1]
+    assert frames.time_to_minute(np.array([96000000]))[0] == -1  # minutes >= 60: off the grid
     df = pd.DataFrame({"code": ["A"], "date": [dt.date(2024, 1, 2)], "time": [113000000],
                        "open": [1.0], "high": [1.0], "low": [1.0], "close": [1.0], "volume": [1.0]})
-    with pytest.raises(ValueError, match="grid"):
-        frames.to_dense(df)
-    df2 = pd.concat([df.assign(time=93000000)] * 2)
-    with pytest.raises(ValueError, match="duplicate"):
-        frames.to_dense(df2)
+    # a row off the grid: the stock-day goes to the row set ("extra"), nothing on the grid
+    p = frames.to_dense(df)
+    assert not p["present"].any() and p["extra"][0].tolist() == [0]
+    assert p["extra"][2]["time"].tolist() == [113000000]
+    # two rows at one time: both kept, in frame order
+    df2 = pd.concat([df.assign(time=93000000, close=2.0), df.assign(time=93000000)])
+    p2 = frames.to_dense(df2)
+    assert not p2["present"].any() and p2["extra"][2]["close"].tolist() == [2.0, 1.0]
+    # input-contract errors of a listed stock-day
+    with pytest.raises(ValueError, match="time must be"):
+        frames.to_dense(pd.concat([df, df.assign(time=None)]))
+    with pytest.raises(ValueError, match="minute_in_trade decreases"):
+        frames.to_dense(pd.concat([df.assign(time=114500000), df.assign(time=130000000)]))
+    with pytest.raises(ValueError, match="more than 255 rows"):
+        frames.to_dense(pd.concat([df.assign(time=93000000 + 1000 * k) for k in range(256)]))
 
 
 def test_to_dense_matches_panel():

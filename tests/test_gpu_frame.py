@@ -110,15 +110,16 @@ def test_bad_day_files_dropped_mid_batch(dev, tmp_path, capsys):
         df.loc[5, "close"] = float("inf")  # a null close is a polars null, not an error
         return df
 
-    def off_grid(df):
-        df.loc[3, "time"] = 113000000  # 11:30: not a bar of the 240-minute grid
+    def null_time(df):
+        df["time"] = df["time"].astype("float64")
+        df.loc[3, "time"] = float("nan")  # a null time (a row off the grid is no error: row set)
         return df
 
     def negative_volume(df):
         df.loc[7, "volume"] = -100.0
         return df
 
-    bad_files = {1: _rewrite(folder, dates[1], inf_close), 3: _rewrite(folder, dates[3], off_grid),
+    bad_files = {1: _rewrite(folder, dates[1], inf_close), 3: _rewrite(folder, dates[3], null_time),
                  4: _rewrite(folder, dates[4], negative_volume)}
     good = [d for d in range(6) if d not in bad_files]
     names = ["doc_pdf60", "vol_return1min"]

@@ -1,5 +1,5 @@
 """GPU: rows that exist with a null field follow polars' null rules (N1-N11 / C8 of
-oracle/mff_oracle.py), for all 58 factors, through mff_stage1_nulls.
+oracle/mff_oracle.py), for all 58 factors, through the row set (mff_stage1_rows).
 
 Only cal_liq_amihud_1min fills a null volume with 0 (CM:743-744); volume.first() is null
 (CM:799, 829), the std / skew / kurtosis of volume shares skip it (CM:492-494, 694-698),
@@ -50,7 +50,7 @@ def test_golden_null_fixture(dev):
     from mff import catalog, engine
     panel, z = load("panel_null.npz")
     dp = engine.DevicePanel.from_host(panel, dev)
-    assert dp.nulls is not None and dp.nulls.K > 0
+    assert dp.rows is not None and dp.rows.K > 0
     val, state, _ = engine.compute_factors(dp)
     torch.cuda.synchronize()
     v, s = val.cpu().numpy(), state.cpu().numpy()
@@ -68,7 +68,7 @@ def test_null_panel_all_factors(dev, overlap, monkeypatch):
     monkeypatch.setattr(engine, "PDF_OVERLAP", overlap)
     panel = _null_panel(60, 3, config=51)
     dp = engine.DevicePanel.from_host(panel, dev)
-    assert dp.nulls.K >= 10
+    assert dp.rows.K >= 10
     val, state, _ = engine.compute_factors(dp)
     torch.cuda.synchronize()
     bad = _check_all(val.cpu().numpy(), state.cpu().numpy(), panel)
@@ -91,7 +91,7 @@ def test_null_subsets_and_order(dev):
 
 def test_null_rows_through_ingest_day_files(dev):
     """Long day frames with pyarrow nulls (the reference's input) through the GPU ingest:
-    the null bits reach mff_stage1_nulls; per-day semantics (one table per day file)."""
+    the null bits reach the row set (mff_stage1_rows); per-day semantics (one table per day file)."""
     import MinuteFrequentFactorCalculateMethodsCICC as CM
     from mff import catalog, frames
     panel = _null_panel(25, 3, config=53)
@@ -109,7 +109,7 @@ def test_null_rows_through_ingest_day_files(dev):
 
 def test_null_rows_multi_date_frame(dev):
     """ONE long frame holding several dates: the four over('code') factors reach across
-    days (mff_stage1_frame with the null set) and doc_pdf ranks every row of every date,
+    days (mff_stage1_frame with the row set) and doc_pdf ranks every row of every date,
     null keys unranked (N8)."""
     import MinuteFrequentFactorCalculateMethodsCICC as CM
     import mff_oracle as O

@@ -131,3 +131,30 @@ def test_merge_skips_the_sort_only_for_ordered_gpu_batches():
     old = batch(d[:1])
     got = factor._merge(old, [batch(d[1:])], presorted=True)
     assert list(got["date"]) == sorted(got["date"])
+
+
+def test_row_set_shard_matches_subpanel_rows():
+    """RowSet.shard (host re-indexing of the listed stock-days to a stock shard) equals the
+    row set of the shard's own sub-panel (nulls and rows off the grid)."""
+    import pandas as pd
+    import pyarrow as pa
+    from mff import engine, frames, synth
+    panel = synth.add_nulls(synth.make_panel(12, 3, config=71, ragged=True), seed=3, rate=0.01)
+    day_frames, _ = synth.irregular_day_frames(panel, seed=3, per_kind=1)
+    host = frames.to_dense(pa.Table.from_pandas(pd.concat(day_frames, ignore_index=True), preserve_index=False),
+                           codes=panel["codes"])
+    rs = engine.RowSet.from_host(*synth.row_set(host), "cpu")
+    S = len(panel["codes"])
+    for s0, s1 in ((0, 5), (5, 12)):
+        sub = synth.subpanel(host, stocks=slice(s0, s1))
+        if host.get("extra") is not None:
+            sd, off, rows = host["extra"]
+            keep = [i for i, x in enumerate(sd) if s0 <= x % S < s1]
+            sub["extra"] = (np.array([(sd[i] // S) * (s1 - s0) + sd[i] % S - s0 for i in keep], np.int64),
+                            np.concatenate([[0], np.cumsum([off[i + 1] - off[i] for i in keep])]).astype(np.int64),
+                            np.concatenate([rows[off[i]:off[i + 1]] for i in keep]))
+        want = synth.row_set(sub)
+        got = rs.shard(S, s0, s1).host()
+        assert got[0].tolist() == want[0].tolist() and got[1].tolist() == want[1].tolist()
+        for k in ("time", "nulls", "volume", "close"):
+            assert np.array_equal(got[2][k], want[2][k], equal_nan=True), k

@@ -128,11 +128,13 @@ def test_ingest_errors(dev):
     df = pd.DataFrame(row)
     ok = ingest.to_device_panel(df, dev)
     assert ok.mask.cpu().numpy()[0, 0, 0] == 1
+    # rows off the grid or at a duplicate time are no error: the stock-day is listed in the
+    # row set (tests/test_gpu_rows.py)
+    for irregular in (pd.concat([df] * 2), df.assign(time=113000000), df.assign(time=93000500),
+                      pd.concat([df.assign(time=93000000 + 100000 * m) for m in range(64)] * 2)):
+        dp = ingest.to_device_panel(irregular, dev)
+        assert dp.rows.K == 1 and int(dp.mask.abs().sum()) == 0
     cases = [
-        (pd.concat([df] * 2), "duplicate"),
-        (pd.concat([df.assign(time=93000000 + 100000 * m) for m in range(64)] * 2), "duplicate"),
-        (df.assign(time=113000000), "grid"),
-        (df.assign(time=93000500), "grid"),
         (df.assign(volume=1.5), "volume"),
         (df.assign(volume=2.0 ** 32 - 1), "volume"),
         (df.assign(volume=2.0 ** 40), "volume"),
