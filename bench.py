@@ -290,6 +290,52 @@ def e2e_extras(panel, days: int):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def null_extras(panel, step, k_ms: float, rates=(0.001, 0.01, 0.1), seed: int = 20251030):
+    """The row-set path at c4 (verdict r4 #4): `rate` of the stock-days carry one null field
+    (a random field of a random bar), listed from the device panel by mff_rows_from_panel
+    and computed by mff_stage1_rows (polars' null rules) inside the pass; each pass timed
+    like the headline (HIP events around compute_factors, mean of 3 after one warm pass),
+    and its ratio to the null-free pass."""
+    import torch
+    from mff import engine
+
+    dev = panel.device
+    D, S = panel.D, panel.S
+    out = {}
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    for rate in rates:
+        K = max(1, int(round(rate * S * D)))
+        sd = torch.randperm(S * D, generator=g, device=dev)[:K].sort().values.to(torch.int32)
+        m = torch.randint(0, 240, (K,), generator=g, device=dev)
+        f = torch.randint(0, 5, (K,), generator=g, device=dev)
+        bits = torch.zeros((K, 5, 8), dtype=torch.int64, device=dev)
+        bits[torch.arange(K, device=dev), f, m // 32] = torch.bitwise_left_shift(torch.ones_like(m), m % 32)
+        bits = torch.where(bits >= 2 ** 31, bits - 2 ** 32, bits).to(torch.int32)
+        mask = panel.mask.clone()
+        rs = engine.RowSet.from_panel(panel.bars, mask, sd, bits)
+        dp = engine.DevicePanel(panel.bars, mask, rows=rs, stocks_total=panel.stocks_total)
+        o = engine.compute_factors(dp)
+        del o
+        torch.cuda.synchronize()
+        ms = []
+        for _ in range(3):
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            o = engine.compute_factors(dp, events=ev)
+            del o
+            torch.cuda.synchronize()
+            ms.append(ev[0].elapsed_time(ev[1]))
+        t = float(np.mean(ms))
+        key = f"null_{rate * 100:g}pct"
+        out[key + "_stage1_ms"] = round(t, 3)
+        out[key + "_vs_null_free"] = round(t / k_ms, 4)
+        out[key + "_stock_days_per_s"] = round(S * D / (t * 1e-3))
+        out[key + "_listed"] = K
+        del dp, rs, mask, bits
+        torch.cuda.empty_cache()
+    return out
+
+
 def final_exposure_extras(val, state, days: int = 250, name: str = "vol_return1min"):
     """MinFreqFactor.cal_final_exposure(20, 'z', mode='days') (MF:187-240) on one
     factor's exposure of S stocks x `days` days taken from the pass output, as the
@@ -337,6 +383,7 @@ def main():
     ap.add_argument("--ingest-days", type=int, default=20)
     ap.add_argument("--ingest-host-days", type=int, default=4)
     ap.add_argument("--e2e-days", type=int, default=8)
+    ap.add_argument("--null-only", action="store_true", help="with --no-extras: still run the null-path extras")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -412,6 +459,8 @@ def main():
 
     extras = {}
     per_kernel = None
+    if args.no_extras and args.null_only:
+        extras.update(null_extras(panel, step, k_ms))
     if args.no_extras and args.kernel_times:
         kt = engine.stage1_launch_times(panel)
         per_kernel = {k: {"ms": round(x["ms"], 3)} for k, x in kt.items() if x["ms"] > 0}
@@ -459,6 +508,8 @@ def main():
             extras.update(ingest_extras(panel, args.ingest_days, args.ingest_host_days))
             if args.e2e_days > 0:
                 extras.update(e2e_extras(panel, args.e2e_days))
+        if rank == 0 and world == 1:
+            extras.update(null_extras(panel, step, k_ms))
         # c5: the same panel made ragged in place (suspension runs, missing bars, gap and
         # flat zero-volume stock-days), one stage-1 pass timed like the headline
         g = torch.Generator(device=dev)

@@ -117,7 +117,9 @@ size_t mff_stage1_workspace_bytes(int S, int D);
  * depend on no other launch (any stream, any time); part 10 / 11 = part 2 / 3 without them.
  * part 17 = part 1 without the exact list kernel, part 32 = that kernel alone (after part
  * 17, before the mff_pdf_* phases and before the LVL/PDF rows are read; part 2 need not
- * wait for it). */
+ * wait for it).  part 64 = part 1's prologue alone (zeroes the doc_pdf level-list counts,
+ * sets the split key, zeroes the exact-list count: mff_stage1_rows phase 1 may start after
+ * it), part 129 / 145 = part 1 / 17 without that prologue. */
 int mff_stage1_part(const float* open, const float* high, const float* low,
                     const float* close, const uint32_t* volume, const uint32_t* valid,
                     int S, int D, const int32_t* factor_ids /* host */, int nf,
@@ -135,8 +137,10 @@ int mff_stage1(const float* open, const float* high, const float* low,
  * A stock-day is listed when a row of it holds a polars null (open / high / low / close /
  * volume) or sits off the grid (a time that is not a 09:30-11:29 / 13:00-14:59 minute:
  * a 09:25 or 15:00 bar, end-labelled bars, seconds) or shares its time with another row.
- * The panel's `valid` mask holds zeros for a listed stock-day, so the grid kernels see it
- * ABSENT; the row set carries every one of its rows:
+ * The panel's `valid` mask holds zeros for a listed stock-day except bit 31 of word 7
+ * (MFF_ROWS_LISTED: bars end at 239), so the grid kernels see it ABSENT and store nothing
+ * for it -- mff_stage1_rows writes all its rows and may run on another stream at the same
+ * time; the row set carries every one of its rows:
  *   rs_sd int32 [K]     d*S + s, ascending
  *   rs_off int32 [K+1]  rows of stock-day i: rs_rows[rs_off[i] .. rs_off[i+1]), at most
  *                       MFF_ROWS_MAX, in (time, frame) order (rows at one time
@@ -146,6 +150,7 @@ int mff_stage1(const float* open, const float* high, const float* low,
  *                       volume) is null (its value is then don't-care)
  */
 #define MFF_ROWS_MAX 255
+#define MFF_ROWS_LISTED 0x80000000u /* valid[d][s][7] of a listed stock-day */
 typedef struct MffRow {
   int32_t time;
   float open, high, low, close;

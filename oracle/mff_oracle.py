@@ -275,6 +275,48 @@ def pl_shift(x: Sequence, n: int, null=None) -> List[Optional[float]]:
     return v[n:] + [None] * min(n, L)
 
 
+def pl_diff(x: Sequence, null=None) -> List[Optional[float]]:
+    """polars ``diff(1)``: x_i - x_{i-1}, null at the first element and where either side is
+    null (N1; no forward fill, unlike pct_change)."""
+    vals = _opt(x, null)
+    return [None] + [None if a is None or b is None else a - b for a, b in zip(vals[1:], vals[:-1])]
+
+
+def pl_cum_sum(x: Sequence) -> List[float]:
+    """polars ``cum_sum()`` in frame order (CM:1022, C2 level order): a running f64 sum,
+    nulls skipped (N3)."""
+    out, acc = [], 0.0
+    for v in x:
+        if v is not None:
+            acc = acc + v
+        out.append(acc)
+    return out
+
+
+def pl_rolling_window(xs: Sequence[Optional[float]], k: int, window: int, min_samples: int):
+    """S13 + N3: the non-null values of rows k-window+1 .. k (the row itself and the
+    window - 1 rows before it), or None when fewer than ``min_samples`` of them are non-null
+    (``rolling_*(window, min_samples)``; MF:205-234 call it with min_samples = window)."""
+    win = [v for v in xs[max(0, k + 1 - window):k + 1] if v is not None]
+    return win if len(win) >= min_samples else None
+
+
+def pl_rolling_mean(xs, window: int, min_samples: int) -> List[Optional[float]]:
+    out = []
+    for k in range(len(xs)):
+        w = pl_rolling_window(xs, k, window, min_samples)
+        out.append(None if w is None else _mean_exact(np.array(w, dtype=np.float64)))
+    return out
+
+
+def pl_rolling_var(xs, window: int, min_samples: int, ddof: int = 1) -> List[Optional[float]]:
+    out = []
+    for k in range(len(xs)):
+        w = pl_rolling_window(xs, k, window, min_samples)
+        out.append(None if w is None else pl_var(np.array(w, dtype=np.float64), ddof=ddof))
+    return out
+
+
 def pl_sum(x) -> float:
     """S9: sum of non-null values, empty sum 0."""
     a = _nn(x) if not isinstance(x, np.ndarray) else x
@@ -911,14 +953,11 @@ def _doc_pdf(df, p):
         for rk, x, ok, kn in zip(rank[s:e].tolist(), vd.tolist(), vok.tolist(), knull[s:e].tolist()):
             rk = None if kn else rk
             levels[rk] = levels.get(rk, 0.0) + (x if ok else 0.0)  # N3, N10
-        cum = 0.0
-        passing = []
         # C2: cum-sum in ascending rank order; the null-rank level (N10) first, where
         # sort() puts nulls (C8)
-        for rk in sorted(levels, key=lambda r: (r is not None, r if r is not None else 0.0)):
-            cum = cum + levels[rk]
-            if tot_gt(cum, p) is True:  # cum_sum() > p, S11
-                passing.append(rk)
+        order = sorted(levels, key=lambda r: (r is not None, r if r is not None else 0.0))
+        passing = [rk for rk, cum in zip(order, pl_cum_sum([levels[rk] for rk in order]))
+                   if tot_gt(cum, p) is True]  # cum_sum() > p, S11
         # .filter(...).sort().first(): null if none passes, or if the null rank passes
         # (sort() puts nulls first)
         if not passing or any(r is None for r in passing):
@@ -1272,26 +1311,23 @@ def oracle_stage2(val: np.ndarray, state: np.ndarray, N: int, method: str):
             if method == "o":  # MF:190-198
                 res = x
             else:
-                if k + 1 < N:
+                win = pl_rolling_window(xs, k, N, N)  # min_samples=N (S13)
+                if win is None:
                     res = None
                 else:
-                    win = xs[k + 1 - N : k + 1]
-                    if any(w is None for w in win):  # min_samples=N (S13)
-                        res = None
+                    w = np.array(win, dtype=np.float64)
+                    mean = _mean_exact(w)
+                    var0 = pl_var(w, ddof=0)
+                    with np.errstate(all="ignore"):
+                        sd = math.sqrt(var0) if not math.isnan(var0) else float("nan")
+                    if method == "m":  # MF:199-209
+                        res = mean
+                    elif method == "std":  # MF:228-238
+                        res = sd
+                    elif method == "z":  # MF:210-227
+                        res = None if x is None else _div(x - mean, sd)
                     else:
-                        w = np.array(win, dtype=np.float64)
-                        mean = _mean_exact(w)
-                        var0 = pl_var(w, ddof=0)
-                        with np.errstate(all="ignore"):
-                            sd = math.sqrt(var0) if not math.isnan(var0) else float("nan")
-                        if method == "m":  # MF:199-209
-                            res = mean
-                        elif method == "std":  # MF:228-238
-                            res = sd
-                        elif method == "z":  # MF:210-227
-                            res = None if x is None else _div(x - mean, sd)
-                        else:
-                            raise ValueError("Unknown method")
+                        raise ValueError("Unknown method")
             out_s[d, s] = NULLV if res is None else VALUE
             out_v[d, s] = 0.0 if res is None else res
     return out_v, out_s

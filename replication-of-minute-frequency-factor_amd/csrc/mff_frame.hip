@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void k_frame_xday(FrameArgs a) {
       const float* C = a.close + sd * NBAR;
       const uint32_t* V = a.volume + sd * NBAR;
       for (int w = 0; w < 8; ++w) {
-        uint32_t bits = mk[w];
+        uint32_t bits = w == 7 ? mk[w] & 0xFFFFu : mk[w];  // bars end at 239 (bit 255: row set)
         while (bits) {
           const int m = 32 * w + __builtin_ctz(bits);
           bits &= bits - 1u;

@@ -133,55 +133,51 @@ struct Win {  // one OLS window's statistics (ddof = 0), null flags per N11
   bool vxn, vyn, covn;
 };
 
-// CM:114-129: the window of rows [r0, r1) (minute_in_trade in (t-50, t]); var / mean
-// over the non-null lows / highs, cov over the pairs with both; exact zero for identical
-// values (C3)
-__device__ Win ols_window(const float* lo, const float* hi, const uint8_t* fl, int r0, int r1) {
+// Prefix arrays of one stock-day's rows for the 50-minute OLS windows (CM:114-129), index
+// e + 1 = through row e (index 0 = nothing): sums of the lows / highs shifted by the
+// stock-day's first non-null low / high (x - X0, y - Y0: exact f64 differences of fp32
+// values, their sums exact below 2^53), their squares, and over the rows where both are
+// non-null (the pairs of pl.cov) the shifted lows, highs and products; packed 8-bit counts
+// of the non-null lows / highs / pairs and of the value changes along each of the four
+// series (C3: a window is constant when no change falls after its first member); the
+// first non-null low / high / pair row at or after each row.
+struct OlsLds {
+  double P[7][257];   // sx, sy, sxx, syy, spx, spy, spxy
+  uint32_t cnt[257];  // nx | ny << 8 | np << 16
+  uint32_t chg[257];  // changes of x | y << 8 | pair x << 16 | pair y << 24
+  uint8_t nxt[3][256];
+  int mi[256];        // minute_in_trade per row
+};
+
+// the window of rows [r0, r1) from the prefix arrays; ddof 0; exact zero variance / cov
+// for a constant side (C3); mean = X0 + sum / n
+__device__ __forceinline__ Win ols_window(const OlsLds& L, int r0, int r1, double X0, double Y0) {
   Win w;
-  int nx = 0, ny = 0, np_ = 0;
-  double x0 = 0.0, y0 = 0.0, px0 = 0.0, py0 = 0.0, sx = 0.0, sy = 0.0, spx = 0.0, spy = 0.0;
-  bool cx = true, cy = true, cpx = true, cpy = true;
-  for (int m = r0; m < r1; ++m) {
-    const bool xo = fl[m] & 1u, yo = fl[m] & 2u;
-    const double x = (double)lo[m], y = (double)hi[m];
-    if (xo) {
-      if (nx == 0) x0 = x;
-      cx = cx && x == x0;
-      sx += x - x0;
-      ++nx;
-    }
-    if (yo) {
-      if (ny == 0) y0 = y;
-      cy = cy && y == y0;
-      sy += y - y0;
-      ++ny;
-    }
-    if (xo && yo) {
-      if (np_ == 0) { px0 = x; py0 = y; }
-      cpx = cpx && x == px0;
-      cpy = cpy && y == py0;
-      spx += x - px0;
-      spy += y - py0;
-      ++np_;
-    }
-  }
+  const uint32_t c1 = L.cnt[r1], c0 = L.cnt[r0];
+  const int nx = (int)((c1 & 0xFFu) - (c0 & 0xFFu));
+  const int ny = (int)(((c1 >> 8) & 0xFFu) - ((c0 >> 8) & 0xFFu));
+  const int np_ = (int)(((c1 >> 16) & 0xFFu) - ((c0 >> 16) & 0xFFu));
+  auto sum = [&](int j) { return L.P[j][r1] - L.P[j][r0]; };
+  // constant when no change of the series falls after its first member in the window
+  auto constant = [&](int j, int shift) {
+    const int f = L.nxt[j][r0];
+    if (f >= r1) return true;
+    return ((L.chg[r1] >> shift) & 0xFFu) == ((L.chg[f + 1] >> shift) & 0xFFu);
+  };
   w.vxn = nx == 0;
   w.vyn = ny == 0;
   w.covn = np_ == 0;
-  w.mx = nx ? x0 + sx / (double)nx : 0.0;
-  w.my = ny ? y0 + sy / (double)ny : 0.0;
-  const double mpx = np_ ? px0 + spx / (double)np_ : 0.0, mpy = np_ ? py0 + spy / (double)np_ : 0.0;
-  double axx = 0.0, ayy = 0.0, axy = 0.0;
-  for (int m = r0; m < r1; ++m) {
-    const bool xo = fl[m] & 1u, yo = fl[m] & 2u;
-    const double x = (double)lo[m], y = (double)hi[m];
-    if (xo) axx += (x - w.mx) * (x - w.mx);
-    if (yo) ayy += (y - w.my) * (y - w.my);
-    if (xo && yo) axy += (x - mpx) * (y - mpy);
+  const double sx = sum(0), sy = sum(1);
+  w.mx = nx ? X0 + sx / (double)nx : 0.0;
+  w.my = ny ? Y0 + sy / (double)ny : 0.0;
+  w.vx = (w.vxn || constant(0, 0)) ? 0.0 : (sum(2) - sx * sx / (double)nx) / (double)nx;
+  w.vy = (w.vyn || constant(1, 8)) ? 0.0 : (sum(3) - sy * sy / (double)ny) / (double)ny;
+  if (w.covn || constant(2, 16) || constant(2, 24)) {
+    w.cov = 0.0;
+  } else {
+    const double spx = sum(4), spy = sum(5);
+    w.cov = (sum(6) - spx * spy / (double)np_) / (double)np_;
   }
-  w.vx = (w.vxn || cx) ? 0.0 : axx / (double)nx;
-  w.vy = (w.vyn || cy) ? 0.0 : ayy / (double)ny;
-  w.cov = (w.covn || cpx || cpy) ? 0.0 : axy / (double)np_;
   return w;
 }
 
@@ -208,13 +204,28 @@ struct Lds {  // per wave
   uint8_t fl[256];    // bit 0 low non-null, bit 1 high non-null
 };
 
-__device__ void stock_day(const Args& a, int i, Lds& L) {
+template <uint32_t FAMS> struct LdsOf { using type = Lds; };
+template <> struct LdsOf<F_OLS> { using type = OlsLds; };
+
+template <uint32_t FAMS>
+__device__ void stock_day(const Args& a, int i, typename LdsOf<FAMS>::type& L) {
   const int lane = lane_id();
-  const uint32_t fam = a.fam;
+  const uint32_t fam = a.fam & FAMS;
   const int sdi = __builtin_amdgcn_readfirstlane(a.sd_list[i]);
   const int d = sdi / a.S;
   const size_t sd = (size_t)sdi;
   const Out out{a.val, a.state, a.row, sd, (size_t)a.D * a.S};
+  // the grid kernels store nothing for a listed stock-day (mask word 7 bit 31), so every
+  // requested row of this instance's families starts ABSENT here (one store per factor,
+  // lane = factor), drained before the values below overwrite some of them
+  if (lane < NF) {
+    const int rr = a.row[lane];
+    if (rr >= 0 && (kFamOf(lane) & fam)) {
+      a.val[(size_t)rr * out.plane + sd] = 0.0;
+      a.state[(size_t)rr * out.plane + sd] = MFF_STATE_ABSENT;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
   const int r0 = __builtin_amdgcn_readfirstlane(a.off[i]);
   int n = __builtin_amdgcn_readfirstlane(a.off[i + 1]) - r0;
   n = n < 0 ? 0 : n > MFF_ROWS_MAX ? MFF_ROWS_MAX : n;  // the host checks the cap
@@ -265,7 +276,7 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
   const Bits B = ballot4(p);
   const Bits NO = ballot4(fnO), NC = ballot4(fnC), NV = ballot4(fnV);
   // rows of a time filter, as Bits
-  auto when = [&](auto pred) {
+  auto when = [&](auto pred) __attribute__((always_inline)) {
     bool f[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) f[k] = p[k] && pred(t[k]);
@@ -283,7 +294,7 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
   if (fam & F_SEG) {
     // filter(time in [ta, tb]) -> sort by time (stable: frame order among equal times,
     // C9) -> close.last() / open.first()
-    auto seg = [&](int f, int32_t ta, int32_t tb) {
+    auto seg = [&](int f, int32_t ta, int32_t tb) __attribute__((always_inline)) {
       const Bits SB = when([&](int32_t x) { return x == ta || x == tb; });
       if (!any(SB)) return;  // filtered set empty -> absent row
       const int m0 = first_of(SB), m1 = last_of(SB);
@@ -298,19 +309,21 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
     // mmt nulls the difference
     const Bits am = when([](int32_t x) { return x <= 113000000; });
     const Bits pm = when([](int32_t x) { return !(x <= 113000000); });
-    double g[2];
-    bool gn[2];
-    int ng = 0;
-    if (any(am)) {
-      gn[ng] = test(NC, last_of(am)) || test(NO, first_of(am));
-      g[ng++] = (double)elem(c, last_of(am)) / (double)elem(o, first_of(am)) - 1.0;
+    const bool ha = any(am), hp = any(pm);
+    double gA = 0.0, gP = 0.0;
+    bool nA = false, nP = false;
+    if (ha) {
+      nA = test(NC, last_of(am)) || test(NO, first_of(am));
+      gA = (double)elem(c, last_of(am)) / (double)elem(o, first_of(am)) - 1.0;
     }
-    if (any(pm)) {
-      gn[ng] = test(NC, last_of(pm)) || test(NO, first_of(pm));
-      g[ng++] = (double)elem(c, last_of(pm)) / (double)elem(o, first_of(pm)) - 1.0;
+    if (hp) {
+      nP = test(NC, last_of(pm)) || test(NO, first_of(pm));
+      gP = (double)elem(c, last_of(pm)) / (double)elem(o, first_of(pm)) - 1.0;
     }
-    if (gn[ng - 1] || gn[0]) out.null(2);
-    else out.val1(2, g[ng - 1] - g[0]);
+    // mmt.last() - mmt.first(): one session gives g - g
+    const double gl = hp ? gP : gA, gf = ha ? gA : gP;
+    if ((hp ? nP : nA) || (ha ? nA : nP)) out.null(2);
+    else out.val1(2, gl - gf);
   }
 
   // ================================================================ MOMR / TRD returns
@@ -505,7 +518,7 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
       h20[k] = p[k] && t[k] <= 95000000;   // CM:1315, 1359, 1387
       h50[k] = p[k] && t[k] <= 102000000;  // CM:1337
     }
-    auto tail = [&](const bool (&tm)[4], int f, bool plus_one) {
+    auto tail = [&](const bool (&tm)[4], int f, bool plus_one) __attribute__((always_inline)) {
       bool tv[4], tb[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -522,7 +535,7 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
     if (any(ballot4(t20))) tail(t20, 50, true);   // trade_bottom20retRatio
     if (any(ballot4(t50))) tail(t50, 51, false);  // trade_bottom50retRatio
     // trade_top{20,50}retRatio, topNeg20, topPos20: mean over the non-null quotients (N3)
-    auto headf = [&](const bool (&hm)[4], int f_all, int f_neg, int f_pos) {
+    auto headf = [&](const bool (&hm)[4], int f_all, int f_neg, int f_pos) __attribute__((always_inline)) {
       if (!any(ballot4(hm))) return;
       bool hv[4], ha[4];
 #pragma unroll
@@ -607,7 +620,7 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
   }
 
   // ================================================================ LVL / PDF (N2, N8, N10, C8)
-  if (fam & (F_LVL | F_PDF)) {
+  if constexpr ((FAMS & (F_LVL | F_PDF)) != 0) if (fam & (F_LVL | F_PDF)) {
     // key = close.last() / close: null when the close is null or close.last() is (N2);
     // the null group sorts first (high word 0: C8), then ascending key = descending close
     const bool lastnull = test(NC, ml);
@@ -792,20 +805,86 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
   }
 
   // ================================================================ OLS CM:93-376 (N11, T1)
-  if (fam & F_OLS) {
+  if constexpr (FAMS == F_OLS) if (fam & F_OLS) {
     int mi[4];
+    bool pr[4];
+    double dx[4], dy[4];
+    const Bits BX = ballot4(okL), BY = ballot4(okH);
+    const int fx = first_of(BX), fy = first_of(BY);
+    const double X0 = fx >= 0 ? (double)elem(lo, fx) : 0.0, Y0 = fy >= 0 ? (double)elem(h, fy) : 0.0;
+    float plx[4], ply[4], ppx[4], ppy[4];
+    bool hlx[4], hly[4], hpp[4], hpq[4];
+    prev_valid(lo, okL, plx, hlx);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pr[k] = okL[k] && okH[k];
+    prev_valid(h, okH, ply, hly);
+    prev_valid(lo, pr, ppx, hpp);
+    prev_valid(h, pr, ppy, hpq);
+    double P[7][4];
+    uint32_t cnt[4], chg[4], own[3][4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       mi[k] = minute_in_trade(t[k]);
-      const int e = 4 * lane + k;
-      if (p[k]) {
-        L.lo[e] = lo[k];
-        L.hi[e] = h[k];
-        L.mi[e] = mi[k];
-        L.fl[e] = (uint8_t)((okL[k] ? 1u : 0u) | (okH[k] ? 2u : 0u));
+      dx[k] = okL[k] ? (double)lo[k] - X0 : 0.0;
+      dy[k] = okH[k] ? (double)h[k] - Y0 : 0.0;
+      P[0][k] = dx[k];
+      P[1][k] = dy[k];
+      P[2][k] = dx[k] * dx[k];
+      P[3][k] = dy[k] * dy[k];
+      P[4][k] = pr[k] ? dx[k] : 0.0;
+      P[5][k] = pr[k] ? dy[k] : 0.0;
+      P[6][k] = pr[k] ? dx[k] * dy[k] : 0.0;
+      cnt[k] = (okL[k] ? 1u : 0u) | (okH[k] ? 0x100u : 0u) | (pr[k] ? 0x10000u : 0u);
+      chg[k] = ((okL[k] && hlx[k] && lo[k] != plx[k]) ? 1u : 0u) | ((okH[k] && hly[k] && h[k] != ply[k]) ? 0x100u : 0u) |
+               ((pr[k] && hpp[k] && lo[k] != ppx[k]) ? 0x10000u : 0u) |
+               ((pr[k] && hpq[k] && h[k] != ppy[k]) ? 0x1000000u : 0u);
+      const uint32_t e = (uint32_t)(4 * lane + k);
+      own[0][k] = okL[k] ? e : 255u;
+      own[1][k] = okH[k] ? e : 255u;
+      own[2][k] = pr[k] ? e : 255u;
+    }
+#pragma unroll
+    for (int j = 0; j < 7; ++j) scan4(P[j]);
+    scan4_u32(cnt);
+    scan4_u32(chg);
+    // the first flagged row at or after each row: its own index, else the next flagged one
+    bool fl3[3][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      fl3[0][k] = okL[k];
+      fl3[1][k] = okH[k];
+      fl3[2][k] = pr[k];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      uint32_t nv[4];
+      bool hn[4];
+      next_valid(own[j], fl3[j], nv, hn);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = 4 * lane + k;
+        if (p[k]) L.nxt[j][e] = (uint8_t)(fl3[j][k] ? own[j][k] : hn[k] ? nv[k] : 255u);
       }
     }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = 4 * lane + k;
+      if (p[k]) {
+#pragma unroll
+        for (int j = 0; j < 7; ++j) L.P[j][e + 1] = P[j][k];
+        L.cnt[e + 1] = cnt[k];
+        L.chg[e + 1] = chg[k];
+        L.mi[e] = mi[k];
+      }
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < 7; ++j) L.P[j][0] = 0.0;
+      L.cnt[0] = 0u;
+      L.chg[0] = 0u;
+    }
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // rolling(index_column='minute_in_trade', period='50i') (CM:114-118): the window of
     // row r holds every row whose minute is in (m_r - 50, m_r], the rows of m_r that come
     // after r included (polars' look-behind windows consume duplicate index values: T1);
@@ -821,7 +900,7 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
         const int w0 = upper_bound(L.mi, n, mi[k] - 50);
         okw[k] = w1 - w0 >= 50;
         if (okw[k]) {
-          const Win w = ols_window(L.lo, L.hi, L.fl, w0, w1);
+          const Win w = ols_window(L, w0, w1, X0, Y0);
           // CM:131-134: when(var_x != 0) cov / var_x, otherwise mean_y / mean_x (null
           // cond or null operand: N1)
           if (!w.vxn && w.vx != 0.0) {
@@ -874,11 +953,17 @@ __device__ void stock_day(const Args& a, int i, Lds& L) {
   }
 }
 
+// one launch per family group: each instance keeps only its sections' values live
+constexpr uint32_t R_LVL = F_LVL | F_PDF;               // the close sort
+constexpr uint32_t R_ORD = F_ORD | F_ORDV;              // the volume sort
+constexpr uint32_t R_OLS = F_OLS;                       // the 50-minute windows
+constexpr uint32_t R_REST = ~(R_LVL | R_ORD | R_OLS);   // one pass over the rows
+template <uint32_t FAMS>
 __global__ __launch_bounds__(256) void k_stage1_rows(Args a) {
-  __shared__ Lds lds[WPB];
+  __shared__ typename LdsOf<FAMS>::type lds[WPB];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = gridDim.x * WPB;
-  for (int i = blockIdx.x * WPB + wave; i < a.K; i += nw) stock_day(a, i, lds[wave]);
+  for (int i = blockIdx.x * WPB + wave; i < a.K; i += nw) stock_day<FAMS>(a, i, lds[wave]);
 }
 
 // ---------------------------------------------------------------- grid stock-days -> rows
@@ -985,7 +1070,11 @@ extern "C" int mff_stage1_rows(int S, int D, const int32_t* rs_sd, const int32_t
     a.lvl_w = reinterpret_cast<uint8_t*>(base + ow);
   }
   const int blocks = (K + rws::WPB - 1) / rws::WPB < 4096 ? (K + rws::WPB - 1) / rws::WPB : 4096;
-  hipLaunchKernelGGL(rws::k_stage1_rows, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), a);
+  const hipStream_t st = as_stream(stream);
+  if (a.fam & rws::R_LVL) hipLaunchKernelGGL(rws::k_stage1_rows<rws::R_LVL>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  if (a.fam & rws::R_ORD) hipLaunchKernelGGL(rws::k_stage1_rows<rws::R_ORD>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  if (a.fam & rws::R_OLS) hipLaunchKernelGGL(rws::k_stage1_rows<rws::R_OLS>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  if (a.fam & rws::R_REST) hipLaunchKernelGGL(rws::k_stage1_rows<rws::R_REST>, dim3((unsigned)blocks), dim3(256), 0, st, a);
   MFF_LAUNCH_CHECK();
   return 0;
 }

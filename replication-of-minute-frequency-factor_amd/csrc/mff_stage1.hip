@@ -90,7 +90,9 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, uin
     const Bits B = ballot4(p);
     const int n = count(B);
     if (n == 0) {
-      if (a.pdfq && (fam & F_PDF)) {
+      // a stock-day of the row set (word 7 bit 31) is mff_stage1_rows' alone
+      const bool listed = (a.mask[sd * 8 + 7] >> 31) != 0u;
+      if (a.pdfq && (fam & F_PDF) && !listed) {
         if (lane < 5) a.pdfq[(size_t)lane * a.D * a.S + sd] = qnan();
       }
       return;  // every output stays ABSENT
@@ -708,7 +710,7 @@ __global__ __launch_bounds__(256) void k_stage1(S1Args a) {
   for (int i = threadIdx.x; i < nf * TILE; i += blockDim.x) {
     const int rrow = i / TILE, jj = i % TILE;
     const int s = s0 + jj;
-    if (s < a.S) {
+    if (s < a.S && (a.mask[((size_t)d * a.S + s) * 8 + 7] >> 31) == 0u) {  // row-set stock-days: skipped
       const size_t o_ = (size_t)rrow * plane + (size_t)d * a.S + s;
       a.val[o_] = sv[i];
       a.state[o_] = ss[i];

@@ -991,7 +991,10 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
     }
 
     // ---------------------------------------------------------------- stores
-    if (act) {
+    // a stock-day of the row set (mask word 7 bit 31, include/mff.h) is stored by
+    // mff_stage1_rows alone, which may run concurrently
+    const bool listed = act && (a.mask[sd * 8 + 7] >> 31) != 0u;
+    if (act && !listed) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int f = 16 * q + g;
@@ -1078,8 +1081,8 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
                         void* workspace, void* stream, int part) {
   clear_error();
   MFF_REQUIRE(part == 1 || part == 2 || part == 3 || part == 4 || part == 10 || part == 11 || part == 17 ||
-                  part == 32,
-              "mff_stage1_part: part=%d must be 1, 2, 3, 4, 10, 11, 17 or 32", part);
+                  part == 32 || part == 64 || part == 129 || part == 145,
+              "mff_stage1_part: part=%d must be 1, 2, 3, 4, 10, 11, 17, 32, 64, 129 or 145", part);
   MFF_REQUIRE(S > 0 && D > 0, "mff_stage1: S=%d D=%d must be positive", S, D);
   MFF_REQUIRE((long long)S * D < (1ll << 31), "mff_stage1: S*D must be < 2^31");
   MFF_REQUIRE(nf > 0 && nf <= NF, "mff_stage1: nf=%d out of range", nf);
@@ -1144,12 +1147,17 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
     return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_LVL | F_PDF, 1024,
                       st, a.lvl_count, a.lvl_key, a.lvl_w);
   }
-  if (part & 1) {  // LVL/PDF group + exact list: everything the doc_pdf phases read
-    if (a.fam & F_PDF) {
-      MFF_HIP(hipMemsetAsync(a.lvl_count, 0, (size_t)D * 8, st));
-      if (pdf_split_init(a.lvl_count, D, st) != 0) return -2;
+  if (part & 65) {  // the prologue of part 1: level-list counts, split key, exact-list count
+    if (!(part & 128)) {
+      if (a.fam & F_PDF) {
+        MFF_HIP(hipMemsetAsync(a.lvl_count, 0, (size_t)D * 8, st));
+        if (pdf_split_init(a.lvl_count, D, st) != 0) return -2;
+      }
+      MFF_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
     }
-    MFF_HIP(hipMemsetAsync(cnt, 0, sizeof(int), st));
+    if (part == 64) return 0;
+  }
+  if (part & 1) {  // LVL/PDF group + exact list: everything the doc_pdf phases read
     if (w64) {  // the wave-per-stock-day kernel for everything
       const int rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, nullptr, nullptr, ~0u, 0, st);
       if (rc != 0 || !(a.fam & F_PDF)) return rc;

@@ -34,6 +34,16 @@ def _stream(device) -> int:
 
 
 ROWS_MAX = 255  # MFF_ROWS_MAX
+ROWS_LISTED = -2 ** 31  # MFF_ROWS_LISTED: mask word 7 of a listed stock-day (int32 view)
+
+
+def mark_listed(mask: torch.Tensor, sd) -> None:
+    """Clear the mask words of the stock-days ``sd`` (d*S + s) and set their row-set flag
+    (include/mff.h MFF_ROWS_LISTED): the grid kernels see them ABSENT and store nothing."""
+    flat = mask.view(-1, 8)
+    idx = torch.as_tensor(sd, device=mask.device).long()
+    flat[idx] = 0
+    flat[idx, 7] = ROWS_LISTED
 
 
 @dataclass
@@ -102,7 +112,7 @@ class RowSet:
                                            _lib.ptr(b[4]), _lib.ptr(mask), S, D, _lib.ptr(sd), _lib.ptr(null_bits),
                                            K, _lib.ptr(off), None, _lib.ptr(rows), st), "mff_rows_from_panel")
         if clear:
-            mask.view(-1, 8)[sd.long()] = 0
+            mark_listed(mask, sd)
         return cls(sd, off, rows)
 
 
@@ -154,8 +164,9 @@ class DevicePanel:
         bars = torch.from_numpy(np.ascontiguousarray(stack_fields(panel))).to(device)
         words = pack_mask(panel["present"])
         sd, off, rows = row_set(panel)
-        if sd.size:  # the listed stock-days go to mff_stage1_rows only
+        if sd.size:  # the listed stock-days go to mff_stage1_rows only (MFF_ROWS_LISTED)
             words.reshape(-1, 8)[sd] = 0
+            words.reshape(-1, 8)[sd, 7] = np.uint32(0x80000000)
         mask = torch.from_numpy(words.view(np.int32)).to(device)
         return cls(bars, mask, list(panel["codes"]), list(panel["dates"]),
                    rows=RowSet.from_host(sd, off, rows, device))
@@ -235,7 +246,18 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
 
         if hl is not None and HL_AT == "start":
             launch_hl()
-        _lib.check(lib.mff_stage1_part(*args, 17 if EXACT_SIDE and not PDF_FIRST else 1), "mff_stage1_part(1)")
+        part1 = 17 if EXACT_SIDE and not PDF_FIRST else 1
+        rows_st = None
+        if rs is not None and ROWS_SIDE and not PDF_FIRST:
+            # the row set on its own stream right after part 1's prologue (level-list
+            # counts, split key): the grid kernels store nothing for its stock-days
+            # (MFF_ROWS_LISTED), so its kernels run beside them; the doc_pdf sort waits for it
+            _lib.check(lib.mff_stage1_part(*args, 64), "mff_stage1_part(64)")
+            rows_st = _side_stream(dev, 2)
+            rows_st.wait_stream(main)
+            rows_phase(3, rows_st)
+            part1 |= 128
+        _lib.check(lib.mff_stage1_part(*args, part1), "mff_stage1_part(1)")
         if hl is not None and HL_AT == "part1":
             launch_hl()
         if PDF_FIRST:
@@ -251,7 +273,10 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             side.wait_stream(main)
             if EXACT_SIDE:  # the exact list kernel ahead of the doc_pdf phases, off the launch stream
                 _lib.check(lib.mff_stage1_part(*(args[:-1] + [side.cuda_stream]), 32), "mff_stage1_part(32)")
-            rows_phase(1, side)
+            if rows_st is not None:
+                side.wait_stream(rows_st)  # the row set's queries and levels before the sort
+            else:
+                rows_phase(1, side)
             sorted_ev = torch.cuda.Event() if SORT_FIRST else None
             with torch.cuda.stream(side):
                 pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch,
@@ -267,7 +292,10 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             launch_hl()
         if hl is not None:
             main.wait_stream(hl)
-        rows_phase(2, main)
+        if rows_st is not None:
+            main.wait_stream(rows_st)
+        else:
+            rows_phase(2, main)
         if events is not None:  # after the doc_pdf tail on the side stream
             events[1].record(main)
         return val, state, ids
@@ -293,6 +321,10 @@ EXACT_SIDE = os.environ.get("MFF_EXACT_SIDE", "1") != "0"
 # after the sorted-group kernel and the count fills in beside the pair and set H (+1.7 %
 # pass throughput with the rank-placement sort, profiles/r03c/ab_launch_order.log)
 SORT_FIRST = os.environ.get("MFF_SORT_FIRST", "1") != "0"
+# MFF_ROWS_SIDE=1 (default): the row set's kernels (mff_stage1_rows, both phases) on their
+# own stream from the start of the pass, beside the grid kernels; 0: phase 1 before the
+# doc_pdf sort and phase 2 after the pass, on the streams of round 4 (A/B timing)
+ROWS_SIDE = os.environ.get("MFF_ROWS_SIDE", "1") != "0"
 # MFF_PDF_FIRST=1: the doc_pdf phases on the launch stream between part 1 and part 2
 PDF_FIRST = os.environ.get("MFF_PDF_FIRST", "0") != "0"
 # The high / low serial kernel (OLS, MOMH) reads only the high / low planes and writes

@@ -436,7 +436,7 @@ class PanelIngest:
         the reference's per-file call fails, MinuteFrequentFactorCICC.py:18-25, 95) -- only
         those cells: another table's cells of the same date stay -- and the reasons are
         returned in ``panel.dropped`` {push index: message}."""
-        from .engine import DevicePanel, RowSet
+        from .engine import DevicePanel, RowSet, mark_listed
         from .synth import ROW_DTYPE
 
         torch.cuda.current_stream(self.dev).wait_stream(self.stream)
@@ -491,7 +491,7 @@ class PanelIngest:
             rows = np.concatenate([rows[starts[i]:starts[i] + n[i]] for i in order])
             sd, n = sd[order], n[order]
             off = np.concatenate([[0], np.cumsum(n)])
-            flat[torch.as_tensor(sd, device=self.dev)] = 0  # only mff_stage1_rows sees them
+            mark_listed(self.mask, sd)  # only mff_stage1_rows sees them
             rs = RowSet.from_host(sd, off, rows, self.dev)
         dates = [_EPOCH + _dt.timedelta(days=x) for x in self.day_numbers]
         dp = DevicePanel(self.bars, self.mask, self.codes, dates, rows=rs)

@@ -93,8 +93,9 @@ def test_row_set_matches_host_restatement(dev):
     for i, k in enumerate(("open", "high", "low", "close", "volume")):
         ok = (rows["nulls"] >> i) & 1 == 0  # values under a null are don't-care
         assert np.array_equal(rows[k][ok], hrows[k][ok]), k
-    # the listed stock-days are ABSENT to the grid kernels
-    assert (dp.mask.view(-1, 8)[torch.as_tensor(sd, device=dev)] == 0).all()
+    # the listed stock-days are ABSENT to the grid kernels and flagged (MFF_ROWS_LISTED)
+    w = dp.mask.view(-1, 8)[torch.as_tensor(sd, device=dev)].cpu().numpy().view(np.uint32)
+    assert (w[:, :7] == 0).all() and (w[:, 7] == 0x80000000).all()
 
 
 def test_rows_from_device_panel(dev):

@@ -190,3 +190,47 @@ def test_stage3_rules():
     assert list(v[0, [0, 1, 4]]) == [3.0, 1.0, 2.0] and math.isnan(v[0, 2]) and s[0, 3] == 1
     v, s = O.oracle_stage3(val, st, "z")
     assert v[0, 0] == pytest.approx((3 - 2) / 1.0)
+
+
+# ---------------------------------------------------------------- (3) more published values
+# narwhals reproduces polars' results in its docstrings (narwhals 2.20.0,
+# /usr/local/lib/python3.10/dist-packages/narwhals/expr.py); each value below is read from
+# the cited docstring and run through the oracle's own helper.  The diff / shift examples
+# are rendered from a polars DataFrame itself; the others from narwhals' pandas backend,
+# whose missing values print as NaN (polars: null).
+def test_std_var_ddof0_published_values():
+    # expr.py:449-468 (std) and 471-490 (var): {"a": [20, 25, 60], "b": [1.5, 1, -1.4]}
+    assert round(O.pl_std(np.array([20.0, 25, 60]), ddof=0), 5) == 17.79513
+    assert round(O.pl_std(np.array([1.5, 1, -1.4]), ddof=0), 6) == 1.265789
+    assert round(O.pl_var(np.array([20.0, 25, 60]), ddof=0), 6) == 316.666667
+    assert round(O.pl_var(np.array([1.5, 1, -1.4]), ddof=0), 6) == 1.602222
+
+
+def test_shift_diff_cum_sum_published_values():
+    a = [1.0, 1, 3, 5, 5]
+    assert O.pl_shift(a, 1) == [None, 1.0, 1.0, 3.0, 5.0]    # expr.py:794-830 (polars frame)
+    assert O.pl_diff(a) == [None, 0.0, 2.0, 2.0, 0.0]         # expr.py:753-792 (polars frame)
+    assert O.pl_cum_sum(a) == [1.0, 2.0, 5.0, 10.0, 15.0]     # expr.py:722-750
+    # pct_change = diff / shift of the forward-filled series (S4, N5): on the same column
+    assert O.pl_pct_change(a) == [None, 0.0, 2.0, 2.0 / 3.0, 0.0]
+
+
+def test_rolling_window_with_null_published_values():
+    # expr.py:1905-1958 (rolling_sum), 1960-2014 (rolling_mean), 2016-2076 (rolling_var),
+    # 2078-2138 (rolling_std): {"a": [1.0, 2.0, None, 4.0]}, window_size=3, min_samples=1 --
+    # the null inside the window is skipped (N3), the window counts rows (S13)
+    xs = [1.0, 2.0, None, 4.0]
+    sums = [None if w is None else sum(w) for w in (O.pl_rolling_window(xs, k, 3, 1) for k in range(4))]
+    assert sums == [1.0, 3.0, 3.0, 6.0]
+    assert O.pl_rolling_mean(xs, 3, 1) == [1.0, 1.5, 1.5, 3.0]
+    var = O.pl_rolling_var(xs, 3, 1)
+    assert var[0] is None  # one value, ddof 1: null (S1; pandas prints NaN)
+    assert [round(v, 6) for v in var[1:]] == [0.5, 0.5, 2.0]
+    std = [None if v is None else math.sqrt(v) for v in var]
+    assert [round(v, 6) for v in std[1:]] == [0.707107, 0.707107, 1.414214]
+    # the stage-2 rule (MF:205-234, min_samples = window): any null in the window -> null
+    assert O.pl_rolling_mean(xs, 3, 3) == [None, None, None, None]
+    assert O.pl_rolling_mean([1.0, 2.0, 3.0, 4.0], 3, 3) == [None, None, 2.0, 3.0]
+    v, st = O.oracle_stage2(np.array([[1.0], [2.0], [0.0], [4.0], [5.0], [6.0]]),
+                            np.array([[2], [2], [1], [2], [2], [2]], np.uint8), 3, "m")
+    assert st[:, 0].tolist() == [1, 1, 1, 1, 1, 2] and v[5, 0] == 5.0
