@@ -228,6 +228,9 @@ int mff_stage1_frame(const float* open, const float* close, const uint32_t* volu
  *   origin_counts: day-owner side of the reduce-scatter exchange: the summed counts of
  *             the owned days at each query of q_all [R][5][D][S_all] (days [d0, d0+nd)),
  *             written in that origin layout -> out uint32 [R][5][nd][S_all] (0 for NaN);
+ *             q_sorted / counts may be the deduplicated lists [nd][M] (M <= R*5*S_all,
+ *             each day's distinct keys padded with ~0: the counts of a value sit at its
+ *             first position);
  *             one all_to_all then hands every rank its own queries' counts
  *   finalize_own: own queries [5][D][S_loc] with their counts in the same layout
  *             (2 n_less + n_eq summed over ranks) -> val/state (rank (c + 1) / 2)

@@ -949,7 +949,7 @@ int mff_pdf_origin_counts(const double* q_all, int R, int S_all, int D, int d0, 
                           const uint64_t* q_sorted, const uint32_t* counts, int M, uint32_t* out,
                           void* stream) {
   clear_error();
-  MFF_REQUIRE(R >= 1 && S_all > 0 && D > 0 && nd > 0 && d0 >= 0 && d0 + nd <= D && M == R * 5 * S_all,
+  MFF_REQUIRE(R >= 1 && S_all > 0 && D > 0 && nd > 0 && d0 >= 0 && d0 + nd <= D && M > 0 && M <= PDF_MAXM,
               "mff_pdf_origin_counts: bad sizes R=%d S=%d D=%d d0=%d nd=%d M=%d", R, S_all, D, d0, nd, M);
   MFF_REQUIRE(q_all && q_sorted && counts && out, "mff_pdf_origin_counts: NULL buffer");
   const size_t n = (size_t)R * 5 * nd * S_all;

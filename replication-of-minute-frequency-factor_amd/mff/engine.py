@@ -217,9 +217,6 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             _lib.ptr(pdfq), _lib.ptr(levels), _lib.ptr(ws), main.cuda_stream]
     rows = [ids.index(i) if i in ids else -1 for i in catalog.PDF_IDS]
     frame_pdf = frame and need_pdf and D > 1
-    if frame_pdf and comm is not None:
-        raise ValueError("frame-wide doc_pdf ranks of a multi-date frame are single-GPU; "
-                         "shard day files (per-day semantics) instead")
     rs = panel.rows
 
     def rows_phase(phase: int, stream) -> None:
@@ -302,7 +299,7 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
     _lib.check(lib.mff_stage1(*args), "mff_stage1")
     rows_phase(1, main)
     if frame_pdf:
-        pdf_ranks_frame(panel, pdfq, levels, rows, val, state)
+        pdf_ranks_frame(panel, pdfq, levels, rows, val, state, comm=comm)
     elif need_pdf:
         pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
     rows_phase(2, main)
@@ -448,8 +445,52 @@ def _pdf_ranks_frame_chunked(lib, panel, pdfq, levels, rows, val, state, chunk_d
                                             state.data_ptr() + off, st), "mff_pdf_finalize(frame chunk)")
 
 
+def _pdf_ranks_frame_sharded(lib, comm, panel, pdfq, levels, rows, val, state,
+                             chunk_days: Optional[int] = None) -> None:
+    """pdf_ranks_frame over stock shards (CM:1015-1017: `.rank()` spans every row of every
+    date and every code): per chunk of days, every rank's queries are all-gathered and
+    sorted as ONE list (on every rank: this is the drop-in surface's multi-date frame, not
+    the batched driver), each rank adds its own level keys of EVERY day of the frame to the
+    words 2 n_less + n_eq at the list's positions (mff_pdf_count_frame), the words are
+    summed over ranks (all-reduce) and each rank writes its own stock-days' ranks."""
+    D, S = panel.D, panel.S
+    dev = panel.device
+    st = _stream(dev)
+    R = comm.world_size
+    S_all = shard_width(comm, S, panel.stocks_total, dev)
+    if NBAR * S_all * R * D >= 2 ** 31:
+        raise ValueError(f"a frame of {D} dates x {S_all * R} codes is too large for one frame-wide doc_pdf rank")
+    if chunk_days is None:
+        chunk_days = max(1, PDF_MAX_QUERIES // (5 * S_all * R))
+    plane = D * S
+    for d0 in range(0, D, chunk_days):
+        d1 = min(D, d0 + chunk_days)
+        Dc = d1 - d0
+        q_own = pdfq[:, d0:d1].contiguous()  # [5][Dc][S]: one day of Dc * S stocks
+        q_all = comm.all_gather(_pad_last(q_own, S_all, float("nan")))  # [R][5][Dc][S_all]
+        M = R * 5 * Dc * S_all
+        ws = torch.empty(lib.mff_pdf_workspace_bytes(Dc * S_all, R, 1), dtype=torch.uint8, device=dev)
+        q_sorted = torch.empty((1, M), dtype=torch.int64, device=dev)
+        _lib.check(lib.mff_pdf_sort(_lib.ptr(q_all), R, Dc * S_all, 1, 0, 1, _lib.ptr(q_sorted), _lib.ptr(ws), st),
+                   "mff_pdf_sort(frame, sharded)")
+        del q_all
+        counts = torch.zeros((1, M), dtype=torch.int32, device=dev)
+        _lib.check(lib.mff_pdf_count_frame(_lib.ptr(levels), S, D, _lib.ptr(q_sorted), M, _lib.ptr(counts), st),
+                   "mff_pdf_count_frame(sharded)")
+        comm.all_reduce_sum(counts)
+        for t, r in enumerate(rows):  # one output row at a time: its chunk is contiguous
+            if r < 0:
+                continue
+            one = [-1] * 5
+            one[t] = 0
+            off = r * plane + d0 * S
+            _lib.check(lib.mff_pdf_finalize(_lib.ptr(q_own), _lib.ptr(q_sorted), _lib.ptr(counts), Dc * S, 1, 0, 1,
+                                            M, _lib.int_array(one), val.data_ptr() + 8 * off,
+                                            state.data_ptr() + off, st), "mff_pdf_finalize(frame, sharded)")
+
+
 def pdf_ranks_frame(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows: List[int], val,
-                    state, chunk_days: Optional[int] = None):
+                    state, chunk_days: Optional[int] = None, comm=None):
     """doc_pdf ranks of a multi-date frame taken as ONE reference frame: `.rank()`
     (CM:1015-1017) is outside any `.over`, so a frame holding D dates ranks every row of
     every date.  The D days' 5*S queries are sorted as one list ([5][D][S] viewed as one
@@ -459,6 +500,9 @@ def pdf_ranks_frame(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor
     (about 670 dates of 5,000 codes) the queries go in day chunks of ``chunk_days``
     (:func:`_pdf_ranks_frame_chunked`)."""
     lib = _lib.load()
+    if comm is not None:
+        _pdf_ranks_frame_sharded(lib, comm, panel, pdfq, levels, rows, val, state, chunk_days)
+        return
     D, S = panel.D, panel.S
     dev = panel.device
     st = _stream(dev)
@@ -604,7 +648,7 @@ def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern, day_batch: Optional[int] = 
     holds it:
       1. all_to_all: every rank's queries of the owner's days -> the owner, which sorts
          them (the sort is not replicated: 1/R of the days per rank);
-      2. all_gather of the sorted day lists [W][M];
+      2. all_gather of the sorted day lists, deduplicated [W][Mu];
       3. every rank counts its own level keys against each day's full list -> [W][M]
          (one word per sorted query, 2 n_less + n_eq: linear in the average rank);
       4. reduce_scatter (sum) of the counts by day block: each owner gets its days' totals;
@@ -634,17 +678,21 @@ def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern, day_batch: Optional[int] = 
         del send
         b0, b1 = blocks[rank]
         nd = b1 - b0
-        mine = torch.zeros((nd_max, M), dtype=torch.int64, device=dev)
+        mine = torch.full((nd_max, M), -1, dtype=torch.int64, device=dev)  # -1 = NaN key (~0)
         if nd > 0:
             mine[:nd] = kern.sort(recv, R, S_all, nd)
         if after_sort is not None and w0 == 0:
             after_sort()
-        gathered = comm.all_gather(mine)  # [R][nd_max][M]
-        q_sorted = torch.cat([gathered[r, :e - s] for r, (s, e) in enumerate(blocks)])  # [W][M]
+        # the distinct values of each sorted day list only (a day's queries hold long
+        # exact ties: ~20 K distinct of 25 K at c4): the lists, the counts and their
+        # reduce-scatter shrink with them; the counts of a value sit at its first position
+        mine, Mu = _dedup_sorted(comm, mine)
+        gathered = comm.all_gather(mine)  # [R][nd_max][Mu]
+        q_sorted = torch.cat([gathered[r, :e - s] for r, (s, e) in enumerate(blocks)])  # [W][Mu]
         del gathered
-        counts = kern.count(q_sorted, w0)  # [W][M], this rank's keys
+        counts = kern.count(q_sorted, w0)  # [W][Mu], this rank's keys
         del q_sorted
-        cs = torch.zeros((R, nd_max, M), dtype=torch.int32, device=dev)
+        cs = torch.zeros((R, nd_max, Mu), dtype=torch.int32, device=dev)
         for r, (s, e) in enumerate(blocks):
             cs[r, :e - s] = counts[s - w0:e - w0]
         del counts
@@ -657,6 +705,21 @@ def _pdf_ranks_sharded(comm, pdfq, S_all: int, kern, day_batch: Optional[int] = 
             own[:, s:e] = back[r, :, :e - s, :S_loc]
         del back
     kern.finalize(pdfq, own)
+
+
+def _dedup_sorted(comm, lists: torch.Tensor):
+    """Rows of ascending int64 keys (u64 total-order images, -1 = the NaN key ~0) -> the
+    distinct values of each row, left-aligned and padded with -1, at the width of the
+    largest row over all ranks (one all-reduce of a scalar).  Returns (dedup, width)."""
+    nd, M = lists.shape
+    keep = torch.ones_like(lists, dtype=torch.bool)
+    keep[:, 1:] = lists[:, 1:] != lists[:, :-1]
+    width = _agreed_max(comm, int(keep.sum(1).max().item()) if nd else 1, lists.device)
+    out = torch.full((nd, width), -1, dtype=lists.dtype, device=lists.device)
+    pos = keep.to(torch.int64).cumsum(1) - 1
+    rr = torch.arange(nd, device=lists.device).unsqueeze(1).expand(nd, M)
+    out[rr[keep], pos[keep]] = lists[keep]
+    return out, width
 
 
 def shard_width(comm, S_loc: int, stocks_total: Optional[int], dev) -> int:
@@ -724,18 +787,89 @@ def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None,
         mom_all = mom if comm is None else comm.all_gather(mom)
         _lib.check(lib.mff_xs_zscore(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(mom_all), R,
                                      _lib.ptr(ov), _lib.ptr(os_), st), "mff_xs_zscore")
-    elif kind == "rank":
-        S_all = S if comm is None else shard_width(comm, S, stocks_total, dev)
-        v_all = val if comm is None else comm.all_gather(_pad_last(val, S_all, 0.0))
-        s_all = state if comm is None else comm.all_gather(_pad_last(state, S_all, ABSENT))
+    elif kind == "rank" and comm is None:
+        _xs_rank_local(lib, val, state, ov, os_, st)
+    elif kind == "rank" and RANK_GATHER:  # round-4 form (A/B): every rank ranks every column
+        S_all = shard_width(comm, S, stocks_total, dev)
+        v_all = comm.all_gather(_pad_last(val, S_all, 0.0))
+        s_all = comm.all_gather(_pad_last(state, S_all, ABSENT))
         ws = torch.empty(lib.mff_xs_rank_workspace_bytes(rows, D, S_all, R), dtype=torch.uint8,
                          device=dev)
         _lib.check(lib.mff_xs_rank(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(v_all),
                                    _lib.ptr(s_all), R, S_all, _lib.ptr(ov), _lib.ptr(os_),
                                    _lib.ptr(ws), st), "mff_xs_rank")
+    elif kind == "rank":
+        S_all = shard_width(comm, S, stocks_total, dev)
+        ov, os_ = xs_rank_sharded(comm, val, state, S_all,
+                                  lambda v, s_, o, os2: _xs_rank_local(lib, v, s_, o, os2, _stream(dev)))
     else:
         raise ValueError(kind)
     return ov, os_
+
+
+# MFF_RANK_GATHER=1: the sharded stage-3 rank all-gathers every column to every rank (round
+# 4); default: the day-owner transpose of xs_rank_sharded
+RANK_GATHER = os.environ.get("MFF_RANK_GATHER", "0") != "0"
+
+
+def _xs_rank_local(lib, val, state, ov, os_, st) -> None:
+    """mff_xs_rank on whole days held by one rank (R = 1: the one-rank kernels,
+    k_xs_rank_day for S <= 5,120)."""
+    rows, D, S = val.shape
+    ws = torch.empty(lib.mff_xs_rank_workspace_bytes(rows, D, S, 1), dtype=torch.uint8, device=val.device)
+    _lib.check(lib.mff_xs_rank(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(val), _lib.ptr(state), 1,
+                               S, _lib.ptr(ov), _lib.ptr(os_), _lib.ptr(ws), st), "mff_xs_rank")
+
+
+def xs_rank_sharded(comm, val: torch.Tensor, state: torch.Tensor, S_all: int, rank_days):
+    """Stage-3 rank of stock-sharded rows [rows][D][S_loc] by day owners (verdict r4 #5):
+      1. all_to_all: each rank sends the owner of every day block its columns of those days
+         ([R][rows][nd_max][S_all], shards padded to S_all with ABSENT);
+      2. the owner ranks its days whole ([rows][nd][R * S_all], ``rank_days(v, s, out_v,
+         out_s)``: the one-rank kernels -- k_xs_rank_day while R * S_all <= 5,120);
+      3. all_to_all back: every rank receives its own columns' ranks of every day block.
+    Each rank moves 2 x rows x D x S_loc x 9 B (values + states, there and back) instead of
+    receiving (R - 1) x rows x D x S_all x 9 B, and ranks 1 / R of the days instead of all
+    of them.  Returns (out_val, out_state) [rows][D][S_loc]."""
+    from .dist import shard_bounds
+
+    rows, D, S_loc = val.shape
+    R, me = comm.world_size, comm.rank
+    dev = val.device
+    blocks = [shard_bounds(D, R, r) for r in range(R)]
+    nd_max = max(1, max(b - a for a, b in blocks))
+    sv = torch.zeros((R, rows, nd_max, S_all), dtype=val.dtype, device=dev)
+    ss = torch.full((R, rows, nd_max, S_all), ABSENT, dtype=state.dtype, device=dev)
+    for q, (a, b) in enumerate(blocks):
+        sv[q, :, :b - a, :S_loc] = val[:, a:b]
+        ss[q, :, :b - a, :S_loc] = state[:, a:b]
+    rv, rs = comm.all_to_all(sv), comm.all_to_all(ss)  # slice q: rank q's columns of my days
+    del sv, ss
+    a, b = blocks[me]
+    nd = b - a
+    # my days whole: columns of rank 0, then rank 1, ... (each padded to S_all)
+    fv = rv.permute(1, 2, 0, 3).reshape(rows, nd_max, R * S_all)[:, :nd].contiguous()
+    fs = rs.permute(1, 2, 0, 3).reshape(rows, nd_max, R * S_all)[:, :nd].contiguous()
+    del rv, rs
+    back_v = torch.zeros((rows, nd_max, R * S_all), dtype=val.dtype, device=dev)
+    back_s = torch.full((rows, nd_max, R * S_all), ABSENT, dtype=state.dtype, device=dev)
+    if nd > 0:
+        ov_ = torch.empty_like(fv)
+        os_ = torch.empty_like(fs)
+        rank_days(fv, fs, ov_, os_)
+        back_v[:, :nd] = ov_
+        back_s[:, :nd] = os_
+    del fv, fs
+    # slice q of the send = rank q's columns of my days
+    tv = back_v.reshape(rows, nd_max, R, S_all).permute(2, 0, 1, 3).contiguous()
+    ts = back_s.reshape(rows, nd_max, R, S_all).permute(2, 0, 1, 3).contiguous()
+    gv, gs = comm.all_to_all(tv), comm.all_to_all(ts)  # slice q: my columns of q's days
+    out_v = torch.empty_like(val)
+    out_s = torch.empty_like(state)
+    for q, (a, b) in enumerate(blocks):
+        out_v[:, a:b] = gv[q, :, :b - a, :S_loc]
+        out_s[:, a:b] = gs[q, :, :b - a, :S_loc]
+    return out_v, out_s
 
 
 def future_return(pct_val: torch.Tensor, pct_state: torch.Tensor, N: int):

@@ -284,3 +284,74 @@ def test_gloo_sharded_doc_pdf_exchange_world2(day_batch):
         ok = os_[t] == O.VALUE
         assert (state[t][ok] == 2).all(), names[t]
         assert np.array_equal(val[t][ok], ov[t][ok]), names[t]
+
+
+# --------------------------------------------------------------------------------------
+# The sharded stage-3 rank by day owners (engine.xs_rank_sharded) at world 2 and 3: the
+# real transpose code and collectives, with the oracle's rank as the stand-in for the
+# one-rank kernel on whole days, against the unsharded oracle.
+
+def _rank_rows(S, D, rows=3, seed=5):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    val = np.round(rng.normal(size=(rows, D, S)), 1)  # ties
+    state = rng.choice([0, 1, 2, 2, 2, 2], size=(rows, D, S)).astype(np.uint8)
+    val[0, 1, :] = 7.0  # an all-tied day
+    val[1, 2, ::3] = np.nan
+    return val, state
+
+
+def _np_rank_days(v, s, ov, os_):
+    import mff_oracle as O
+    for r in range(v.shape[0]):
+        a, b = O.oracle_stage3(v[r].numpy(), s[r].numpy(), "rank")
+        ov[r] = torch.from_numpy(a)
+        os_[r] = torch.from_numpy(b)
+
+
+def _xs_rank_worker(rank, world, port, resq):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "replication-of-minute-frequency-factor_amd"), os.path.join(root, "oracle")):
+        sys.path.insert(0, p)
+    from mff import dist, engine
+    comm, _ = dist.init_from_env(backend="gloo")
+    S, D = 11, 5
+    val, state = _rank_rows(S, D)
+    s0, s1 = dist.shard_bounds(S, world, rank)
+    S_all = engine.shard_width(comm, s1 - s0, S, torch.device("cpu"))
+    comm.stats = dist.CommStats()
+    ov, os_ = engine.xs_rank_sharded(comm, torch.from_numpy(val[:, :, s0:s1].copy()),
+                                     torch.from_numpy(state[:, :, s0:s1].copy()), S_all, _np_rank_days)
+    stats = comm.stats.summary()
+    comm.barrier()
+    dist_.destroy_process_group()
+    resq.put((rank, (ov.numpy(), os_.numpy(), stats)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_rank_by_day_owners(world):
+    import numpy as np
+    import mff_oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_xs_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    val, state = _rank_rows(11, 5)
+    got_v = np.concatenate([res[r][0] for r in range(world)], axis=2)
+    got_s = np.concatenate([res[r][1] for r in range(world)], axis=2)
+    for r in range(val.shape[0]):
+        ev, es = O.oracle_stage3(val[r], state[r], "rank")
+        assert np.array_equal(got_s[r], es)
+        ok = es == O.VALUE
+        assert np.array_equal(got_v[r][ok], ev[ok], equal_nan=True)
+    for r in range(world):  # two all_to_all pairs (values + states, there and back), no gather
+        assert res[r][2]["all_to_all"]["calls"] == 4 and "all_gather" not in res[r][2]

@@ -205,3 +205,40 @@ def test_all_factors_one_ingest_and_result_cache(dev, tmp_path, monkeypatch):
     assert len(reads) == 4, "a cached batch re-read its files"
     assert not bad, "\n".join(bad)
     factor.clear_result_cache()
+
+
+@pytest.mark.parametrize("R", [2, 3])
+def test_sharded_frame_doc_pdf_and_row_set(dev, R):
+    """Stock shards (threads, ThreadComm) of a ragged panel with nulls: (1) each shard's row
+    set equals RowSet.shard of the unsharded one; (2) the per-day pass matches the oracle;
+    (3) ONE multi-date frame (frame=True) ranks doc_pdf over every row of every date and
+    every shard -- queries all-gathered and sorted as one list, counts all-reduced -- exactly
+    as the unsharded oracle frame (CM:1015-1017)."""
+    import mff_oracle as O
+    from mff import catalog, dist, engine, synth
+    panel = synth.add_nulls(synth.make_panel(31, 4, config=81, ragged=True), seed=8, rate=0.01)
+    S = len(panel["codes"])
+    full = engine.DevicePanel.from_host(panel, dev)
+    ov, os_ = O.oracle_stage1(panel)
+    fx = O.oracle_frame_doc_pdf(panel)
+
+    def rank_fn(comm):
+        s0, s1 = dist.shard_bounds(S, comm.world_size, comm.rank)
+        dp = engine.DevicePanel.from_host(synth.subpanel(panel, stocks=slice(s0, s1)), dev)
+        a, b = dp.rows.host(), full.rows.shard(S, s0, s1).host()
+        same = a[0].tolist() == b[0].tolist() and a[1].tolist() == b[1].tolist() and \
+            bytes(a[2].tobytes()) == bytes(b[2].tobytes())
+        val, state, _ = engine.compute_factors(dp, comm=comm)
+        fv, fs, _ = engine.compute_factors(dp, O.FRAME_RANK_NAMES, comm=comm, frame=True)
+        torch.cuda.synchronize()
+        return same, [t.cpu().numpy() for t in (val, state, fv, fs)]
+
+    parts = dist.run_threads(R, rank_fn)
+    assert all(p[0] for p in parts)
+    cat = [np.concatenate([p[1][k] for p in parts], axis=2) for k in range(4)]
+    bad = []
+    for i, nm in enumerate(catalog.NAMES):
+        bad += compare(cat[0][i], cat[1][i], ov[i], os_[i], nm)
+    for t, nm in enumerate(O.FRAME_RANK_NAMES):
+        bad += compare(cat[2][t], cat[3][t], *fx[nm], f"{nm}/frame", rtol=0.0, atol=0.0)
+    assert not bad, "\n".join(bad[:20])
