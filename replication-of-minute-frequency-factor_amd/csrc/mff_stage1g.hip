@@ -42,13 +42,17 @@ int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, c
 int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
                   uint32_t fam, double* val, uint8_t* state, const uint32_t* ord_th, hipStream_t st);
 
-// 16 stock-days of one day per block iteration; MFF_GITER iterations per block
+// 16 stock-days of one day per block iteration; MFF_GITER iterations per block.  One:
+// with a loop, everything derived from the lane ids (lane masks, offsets, the scratch
+// address) is hoisted out of it and stays live across it -- the ORD + LVL launch then
+// took 128 VGPRs (4 waves per SIMD) against 91 (5 waves) without; measured 15.5 against
+// 16.6 ms in the pass (profiles/r05/ab_giter.txt)
 #ifndef MFF_GITER
-#define MFF_GITER 4
+#define MFF_GITER 1
 #endif
 // waves per SIMD the group kernel is built for (its LDS allows 5 at 31.7 KB per block)
 #ifndef MFF_GWAVES
-#define MFF_GWAVES 4
+#define MFF_GWAVES 5
 #endif
 #ifndef MFF_MERGE_OL
 #define MFF_MERGE_OL 1
@@ -183,7 +187,7 @@ constexpr uint32_t kGroups[2] = {G_ORD, G_LVL};
 constexpr uint32_t G_OL = G_ORD | G_LVL;
 
 template <uint32_t SET>
-// (256, 4): at most 128 VGPRs, four waves per SIMD (the LVL set would take 139 and three)
+// (256, 5): at most 102 VGPRs, five waves per SIMD
 __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
   // 2 KB per group plus 64 B of padding: the four groups of a wave start 16 banks apart,
   // so a store of 16 consecutive words per group covers the 64 banks once

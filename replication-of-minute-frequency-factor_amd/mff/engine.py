@@ -132,8 +132,9 @@ class DevicePanel:
     mask: torch.Tensor
     codes: List[str] = field(default_factory=list)
     dates: List = field(default_factory=list)
-    # ingest with skip_bad: {input table index: reason} of the tables dropped (their days
-    # hold no bars)
+    # ingest with skip_bad: {input table index: reason} of the tables dropped (the
+    # stock-day cells a dropped table wrote hold no bars; other tables' cells of the same
+    # dates keep theirs)
     dropped: dict = field(default_factory=dict)
     rows: Optional[RowSet] = None
     # stock-sharded panels: the number of stocks over all ranks (shards by

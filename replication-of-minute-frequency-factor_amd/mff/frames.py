@@ -122,8 +122,11 @@ def minute_to_time(m: np.ndarray) -> np.ndarray:
 
 def _columns(df):
     """Frame -> ({name: numpy values}, {name: null mask}) -- a null mask only for the
-    columns holding polars nulls (pyarrow nulls, pandas None / pd.NA); a float NaN is a
-    value, not a null."""
+    columns holding polars nulls: pyarrow nulls; a pandas frame goes through
+    pa.Table.from_pandas, which makes None, pd.NA AND a float NaN a null (as polars'
+    from_pandas does).  A float NaN inside an arrow table is a value (and breaks the price
+    contract).  A dict of arrays carries no null masks: give nulls as a pyarrow or pandas
+    frame."""
     if hasattr(df, "to_arrow") and not hasattr(df, "to_pandas_dtype"):
         df = df.to_arrow()
     import pyarrow as pa
@@ -339,7 +342,7 @@ def from_long(df, name: str, codes: Sequence[str] | None = None,
         x = np.asarray(arr.fill_null(0.0).to_numpy(zero_copy_only=False), dtype=np.float64)
     elif col.dtype == object:  # None / pd.NA are nulls, NaN is a value
         obj = col.to_numpy(dtype=object)
-        isnull = pd.isna(obj) & ~np.array([isinstance(v, float) for v in obj], dtype=bool)
+        isnull = pd.isna(obj) & ~np.array([isinstance(v, (float, np.floating)) for v in obj], dtype=bool)
         x = np.where(isnull, 0.0, pd.to_numeric(pd.Series(obj).where(~isnull, 0.0)).to_numpy(np.float64))
     else:  # a numpy float column: NaN is a value (no nulls)
         x = np.asarray(col.to_numpy(), dtype=np.float64)

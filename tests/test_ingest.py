@@ -171,3 +171,26 @@ def test_cal_function_through_ingest(dev):
     for name in ("vol_return1min", "doc_pdf80"):
         v, s, _, _ = frames.from_long(res[name], name, codes=panel["codes"], dates=panel["dates"])
         assert not compare(v, s, *exp[name], name), name
+
+
+@pytest.mark.gpu
+def test_skip_bad_drops_only_the_bad_tables_cells(dev):
+    """Two tables hold different stocks of the SAME date and one of them is bad: with
+    skip_bad only the stock-day cells the bad table wrote come out ABSENT; the good
+    table's cells of that date keep their bars (PanelIngest.finish clears per cell)."""
+    from mff import ingest
+    panel, _ = _frame(S=6, D=1, ragged=False, config=5)
+    df = long_frame(panel, 0)
+    good = df[df["code"].isin(panel["codes"][:3])].reset_index(drop=True)
+    bad = df[df["code"].isin(panel["codes"][3:])].reset_index(drop=True)
+    bad.loc[5, "close"] = -1.0  # breaks the price contract
+    dp = ingest.to_device_panel([good, bad], dev, codes=panel["codes"], skip_bad=True)
+    assert list(dp.dropped) == [1] and "prices" in dp.dropped[1]
+    pres = synth.unpack_mask(dp.mask.cpu().numpy().view(np.uint32))
+    assert pres[0, :3].all() and not pres[0, 3:].any()
+    ref = frames.to_dense(pa.Table.from_pandas(good, preserve_index=False), codes=panel["codes"])
+    bars = dp.bars.cpu().numpy()
+    for k, f in enumerate(frames.FIELDS[:4]):
+        assert np.array_equal(bars[k][0, :3], ref[f][0, :3]), f
+    with pytest.raises(ValueError, match="prices"):
+        ingest.to_device_panel([good, bad], dev, codes=panel["codes"])
