@@ -407,13 +407,29 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
   uint64_t nullm = 0;  // bit k: w[k] is null
   int cnt = 0;
   if (ds > 0 && method != MFF_ROLL_O) {
-    // the window after day ds-1 holds at most its last N present days: replay them
-    int dw = ds, found = 0;
+    // the window after day ds-1 holds at most its last N present days: replay them.  The
+    // backward scan loads 8 days' states at a time (one dependent round trip per 8 days:
+    // a stock listed late, ABSENT for most of the panel, scans its whole absent run in
+    // every later segment), and the replay starts at the earliest present day it saw
+    // (not at day 0 when fewer than N exist): profiles/r05/s2_absent.log
+    int dw = ds, found = 0, lo = ds;
     while (dw > 0 && found < N) {
-      --dw;
-      found += st[(size_t)dw * S] != MFF_STATE_ABSENT ? 1 : 0;
+      uint8_t b[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b[k] = st[(size_t)max(dw - 1 - k, 0) * S];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (dw > 0 && found < N) {
+          --dw;
+          if (b[k] != MFF_STATE_ABSENT) {
+            ++found;
+            lo = dw;
+          }
+        }
+      }
     }
-    for (int d = dw; d < ds; ++d) {
+    // found == N: lo = dw, the N-th present day back; else the earliest present day (ds: none)
+    for (int d = lo; d < ds; ++d) {
       const uint8_t sx = st[(size_t)d * S];
       if (sx == MFF_STATE_ABSENT) continue;
       const bool isnull = sx == MFF_STATE_NULL;

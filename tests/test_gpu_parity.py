@@ -249,14 +249,22 @@ def _random_long_panel(D, S, seed):
 def test_stage2_day_segments(dev, N, seg, monkeypatch):
     """k_stage2_reg over day segments (MFF_S2_SEG_DAYS): each segment rebuilds its window
     from the N present days before it -- segments shorter and longer than the window,
-    with absent days, nulls, NaN / inf and a constant column (exact zeros) crossing the
-    segment boundaries, against the oracle."""
+    with absent days, nulls, NaN / inf, a constant column (exact zeros) and stocks listed
+    late or present sparsely crossing the segment boundaries, against the oracle."""
     import mff_oracle as O
     from mff import engine
     monkeypatch.setenv("MFF_S2_SEG_DAYS", str(seg))
     D = 150
     val, state = _random_long_panel(D, 130, N + 7)
     state[30:70, 9] = 0  # a 40-day suspension across several segments
+    # listed late: absent for 120 days, then present (the batched backward scan crosses the
+    # whole run and finds nothing: the replay starts at the first present day); fewer than
+    # N present days before a later segment; present days only every 9th day
+    state[:120, 11] = 0
+    state[:120, 12] = 0
+    state[[40, 77, 101], 12] = 2
+    state[:, 13] = 0
+    state[::9, 13] = 2
     v = np.ascontiguousarray(val[None])
     st = np.ascontiguousarray(state[None])
     bad = []
