@@ -93,6 +93,10 @@ constexpr uint32_t kPairB = MFF_PAIR_SPLIT ? (F_SUMC | F_CORR) : kSerB;
 #ifndef MFF_SERH_VRING
 #define MFF_SERH_VRING 1
 #endif
+// set H's beta from the window's 1 / (var_x var_y) when it is computed (no f64 division)
+#ifndef MFF_SERH_BETA_MUL
+#define MFF_SERH_BETA_MUL 1
+#endif
 
 // ---- presence bits of one stock-day: 8 words, bit m%32 of word m/32 (compile-time
 // word indices only, so the array stays in registers)
@@ -336,10 +340,20 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       const double Cv = fma(-Sx * 0.02, Sy, Sxy);
       // beta = cov / var_x, or mean_y / mean_x when var_x == 0 (CM:131-134)
       const bool vz = !cx && Vx != 0.0;
-      const double beta = fdiv(vz ? (cy ? 0.0 : Cv) : y0 + Sy * 0.02, vz ? Vx : x0 + Sx * 0.02);
       const double prod = Vx * Vy;
-      if (!cx && !cy && prod != 0.0) {
+      const bool qw = !cx && !cy && prod != 0.0;
+      double beta;
+      if (MFF_SERH_BETA_MUL && qw) {
+        // cov / var_x = cov * var_y / (var_x var_y): the window's 1 / prod serves beta too
+        // (one rounding more than the quotient, no division)
         const double rp = frsq(prod);  // prod < 0: NaN, as sqrt(prod)
+        const double ip = rp * rp;     // 1 / prod
+        beta = Cv * Vy * ip;
+      } else {
+        beta = fdiv(vz ? (cy ? 0.0 : Cv) : y0 + Sy * 0.02, vz ? Vx : x0 + Sx * 0.02);
+      }
+      if (qw) {
+        const double rp = frsq(prod);  // (the same value as above: CSE)
         const double ip = rp * rp;     // 1 / prod
         const double sc = fsqrt(Cv);   // cov < 0: NaN, as cov**0.5
         sq += (Cv == 0.0 ? 0.0 : sc) * ip;  // cov**0.5 / (vx*vy) / (50^1.5)   CM:137
