@@ -432,3 +432,38 @@ def test_stage3_golden(dev):
             bad += compare(rv[0].cpu().numpy(), rs[0].cpu().numpy(), z[f"s3_{nm}_{kind}_val"],
                            z[f"s3_{nm}_{kind}_state"], f"{nm}/{kind}", atol=1e-12)
     assert not bad, "\n".join(bad)
+
+
+def test_volume_moments_match_polars_published_values(dev):
+    """shape_skewVol / shape_kurtVol (CM:690-729: skew / kurtosis of the day's volumes,
+    scale-free) on a stock-day with the five volumes of polars' own docstring example,
+    pl.Series([1, 1, 2, 10, 100]).skew() = 1.4724267269058975 and .kurtosis() =
+    0.2106571340718002 (narwhals/series.py:718-747, rendered from polars), and the same five
+    values as the day's 1-minute returns for shape_skew / shape_kurt: the grid path
+    (wave-pair kernel) and the row-set path (the same stock-day with a null high) both
+    reproduce them."""
+    from mff import catalog, synth
+    panel = synth.make_panel(8, 1, config=3)
+    bars = [0, 7, 50, 130, 200]
+    for s in (0, 1):
+        panel["present"][0, s] = False
+        panel["present"][0, s, bars] = True
+        panel["volume"][0, s, bars] = np.array([1, 1, 2, 10, 100], np.float32) * 100
+        # returns close / open - 1 = [1, 1, 2, 10, 100] / 1024 exactly (open 1.0)
+        r = np.array([1, 1, 2, 10, 100], np.float32) / 1024
+        panel["open"][0, s, bars] = 1.0
+        panel["close"][0, s, bars] = 1.0 + r
+        panel["low"][0, s, bars] = 1.0
+        panel["high"][0, s, bars] = 1.0 + r
+        for k in ("open", "high", "low", "close", "volume"):
+            panel[k][0, s][~panel["present"][0, s]] = np.nan
+    panel["null"] = np.zeros(panel["present"].shape, np.uint8)
+    panel["null"][0, 1, 7] = 2  # a null high (bit 1): stock 1 goes through the row set
+    # the same five values as 1-minute returns: shape_skew / shape_kurt (CM:518-687)
+    names = ["shape_skewVol", "shape_kurtVol", "shape_skew", "shape_kurt"]
+    gv, gs, ids = _run_stage1(panel, dev, names)
+    for s in (0, 1):
+        for row, want, tol in ((0, 1.4724267269058975, 1e-12), (1, 0.2106571340718002, 1e-11),
+                               (2, 1.4724267269058975, 1e-12), (3, 0.2106571340718002, 1e-11)):
+            assert gs[row, 0, s] == 2, (names[row], s)
+            assert abs(gv[row, 0, s] - want) <= tol * want, (names[row], s, gv[row, 0, s])

@@ -27,6 +27,14 @@ def test_polars_skew_kurt_published_values():
     assert round(O.pl_kurt(np.array([1.0, 1, 2, 10, 100])), 6) == 0.210657
 
 
+def test_polars_skew_kurt_full_precision():
+    # narwhals/series.py:718-747 (narwhals 2.20.0): rendered from a polars Series itself,
+    # pl.Series([1, 1, 2, 10, 100]).skew() / .kurtosis(), printed to full double precision
+    x = np.array([1.0, 1, 2, 10, 100])
+    assert approx(O.pl_skew(x), 1.4724267269058975, rel=4e-16)
+    assert approx(O.pl_kurt(x), 0.2106571340718002, rel=4e-15)
+
+
 def test_moment_edge_rules():
     assert O.pl_skew(np.array([])) is None           # S2 n=0 -> null
     assert math.isnan(O.pl_skew(np.array([3.0])))    # n=1 -> NaN
