@@ -467,3 +467,29 @@ def test_volume_moments_match_polars_published_values(dev):
                                (2, 1.4724267269058975, 1e-12), (3, 0.2106571340718002, 1e-11)):
             assert gs[row, 0, s] == 2, (names[row], s)
             assert abs(gv[row, 0, s] - want) <= tol * want, (names[row], s, gv[row, 0, s])
+
+
+def test_stage2_std_matches_polars_rendered_rolling_var(dev):
+    """pl.Series([1.0, 3.0, 1.0, 4.0]).rolling_var(window_size=2, min_samples=1) = [null,
+    2.0, 2.0, 4.5] (narwhals/series.py:2514-2568, rendered by polars, ddof 1): stage 2's
+    'std' over 2 present days (MF:228-238: rolling_std(N, min_samples=N, ddof=0)) is null on
+    day 0 and sqrt(var * (N - 1) / N) of those variances after it, on the register kernel
+    and the sliding kernel."""
+    import math
+    import os
+    from mff import engine
+    v = torch.tensor([1.0, 3.0, 1.0, 4.0], dtype=torch.float64, device=dev).reshape(1, 4, 1).repeat(1, 1, 3)
+    st = torch.full((1, 4, 3), 2, dtype=torch.uint8, device=dev)
+    for impl in (None, "slide"):
+        if impl:
+            os.environ["MFF_STAGE2_IMPL"] = impl
+        try:
+            rv, rs = engine.rolling(v, st, 2, "std")
+        finally:
+            os.environ.pop("MFF_STAGE2_IMPL", None)
+        torch.cuda.synchronize()
+        rv, rs = rv.cpu().numpy(), rs.cpu().numpy()
+        assert (rs[0, 0] == 1).all() and (rs[0, 1:] == 2).all(), impl
+        want = [math.sqrt(x * (2 - 1) / 2) for x in (2.0, 2.0, 4.5)]  # ddof 1 -> ddof 0
+        for d in range(3):
+            assert np.allclose(rv[0, d + 1], want[d], rtol=1e-14, atol=0), (impl, d, rv[0, d + 1])

@@ -35,6 +35,14 @@ def test_polars_skew_kurt_full_precision():
     assert approx(O.pl_kurt(x), 0.2106571340718002, rel=4e-15)
 
 
+def test_polars_rendered_std_and_rolling_var():
+    # narwhals/series.py:864-872: pl.Series([1, 2, 3]).std() = 1.0; series.py:2514-2568:
+    # pl.Series([1.0, 3.0, 1.0, 4.0]).rolling_var(window_size=2, min_samples=1) =
+    # [null, 2.0, 2.0, 4.5] (polars' own rendering: one sample at ddof 1 is null, S1)
+    assert O.pl_std(np.array([1.0, 2.0, 3.0])) == 1.0
+    assert O.pl_rolling_var([1.0, 3.0, 1.0, 4.0], 2, 1) == [None, 2.0, 2.0, 4.5]
+
+
 def test_moment_edge_rules():
     assert O.pl_skew(np.array([])) is None           # S2 n=0 -> null
     assert math.isnan(O.pl_skew(np.array([3.0])))    # n=1 -> NaN
