@@ -268,17 +268,22 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
             _lib.check(lib.mff_stage1_part(*args, 10 if hl is not None else 2), "mff_stage1_part(2)")
         else:
             side = _side_stream(dev)
-            side.wait_stream(main)
+            split = SORT_PRIO != PDF_PRIO and comm is None
+            sside = _side_stream(dev, 3) if split else side  # exact list + sort
+            sside.wait_stream(main)
             if EXACT_SIDE:  # the exact list kernel ahead of the doc_pdf phases, off the launch stream
-                _lib.check(lib.mff_stage1_part(*(args[:-1] + [side.cuda_stream]), 32), "mff_stage1_part(32)")
+                _lib.check(lib.mff_stage1_part(*(args[:-1] + [sside.cuda_stream]), 32), "mff_stage1_part(32)")
             if rows_st is not None:
-                side.wait_stream(rows_st)  # the row set's queries and levels before the sort
+                sside.wait_stream(rows_st)  # the row set's queries and levels before the sort
             else:
-                rows_phase(1, side)
+                rows_phase(1, sside)
             sorted_ev = torch.cuda.Event() if SORT_FIRST else None
-            with torch.cuda.stream(side):
+            with torch.cuda.stream(sside):
                 pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch,
-                          after_sort=(lambda: sorted_ev.record(side)) if sorted_ev is not None else None)
+                          after_sort=(lambda: sorted_ev.record(sside)) if sorted_ev is not None else None,
+                          count_stream=side if split else None)
+            if split:
+                side.wait_stream(sside)
             if sorted_ev is not None:  # part 2 after the doc_pdf sort (whole-CU workgroups)
                 main.wait_event(sorted_ev)
                 if hl is not None and HL_AT == "sort":  # set H beside the pair, after the sort
@@ -344,6 +349,10 @@ HL_AT = os.environ.get("MFF_HL_AT", "start")
 # profiles/r03e/ab_stream_priority.log; doc_pdf high instead: +0.1 %, both: +1.4 %).
 PDF_PRIO = int(os.environ.get("MFF_PDF_PRIO", "0"))
 HL_PRIO = int(os.environ.get("MFF_HL_PRIO", "-1"))
+# MFF_SORT_PRIO: when it differs from MFF_PDF_PRIO, the exact list kernel and the doc_pdf
+# sort (the short critical chain between the sorted-group kernel and the pair) run on a
+# stream of that priority and the count on the doc_pdf stream behind them
+SORT_PRIO = int(os.environ.get("MFF_SORT_PRIO", str(PDF_PRIO)))
 
 _SIDE = {}
 
@@ -351,7 +360,8 @@ _SIDE = {}
 def _side_stream(dev, which: int = 0) -> torch.cuda.Stream:
     key = (dev.index, threading.get_ident(), which)
     if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(dev, priority=HL_PRIO if which == 1 else PDF_PRIO)
+        prio = HL_PRIO if which == 1 else SORT_PRIO if which == 3 else PDF_PRIO
+        _SIDE[key] = torch.cuda.Stream(dev, priority=prio)
     return _SIDE[key]
 
 
@@ -371,10 +381,12 @@ def stage1_frame(panel: DevicePanel, ids: Sequence[int], val, state) -> None:
 
 def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows: List[int], val, state,
               comm=None,
-              day_batch: Optional[int] = None, workspace_budget: int = 2 << 30, after_sort=None):
+              day_batch: Optional[int] = None, workspace_budget: int = 2 << 30, after_sort=None,
+              count_stream=None):
     """doc_pdf frame-wide ranks (CM:1015-1017) for all days, in day batches.  ``after_sort``:
     optional callable, invoked once the first day batch's sort is enqueued (sharded: the
-    first window's sort of this rank's days)."""
+    first window's sort of this rank's days).  ``count_stream`` (one rank): the counts run
+    on that stream behind each sort instead of on the current stream."""
     lib = _lib.load()
     D, S = panel.D, panel.S
     dev = panel.device
@@ -402,10 +414,16 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
                                     _lib.ptr(ws), st), "mff_pdf_sort")
         if after_sort is not None and d0 == 0:
             after_sort()
+        cst = st
+        if count_stream is not None:
+            count_stream.wait_stream(torch.cuda.current_stream(dev))
+            q_sorted.record_stream(count_stream)
+            ws.record_stream(count_stream)
+            cst = count_stream.cuda_stream
         # single rank: count + finalize fused, no exchange
         _lib.check(lib.mff_pdf_rank_local(_lib.ptr(levels), _lib.ptr(pdfq), S, D, d0, nd,
                                           _lib.ptr(q_sorted), M,
-                                          _lib.int_array(rows), _lib.ptr(val), _lib.ptr(state), st),
+                                          _lib.int_array(rows), _lib.ptr(val), _lib.ptr(state), cst),
                    "mff_pdf_rank_local")
 
 

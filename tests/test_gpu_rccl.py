@@ -77,7 +77,7 @@ def test_rccl_engine_paths_match_unsharded(comm):
         exact = nm.startswith("doc_pdf")
         bad += compare(v1n[i], s1n[i], v0n[i], s0n[i], nm, rtol=0 if exact else 1e-6, atol=0 if exact else None)
     assert (s1n == s0n).all()
-    # stage 3: z (moments all_gather) and rank (column all_gather), vs the oracle too
+    # stage 3: z (moments all_gather) and rank (day-owner all_to_all there and back), vs the oracle too
     for kind in ("z", "rank"):
         a = _np(*engine.cross_section(v0, s0, kind))
         b = _np(*engine.cross_section(v0, s0, kind, comm=comm))
