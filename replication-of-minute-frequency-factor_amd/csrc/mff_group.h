@@ -254,6 +254,9 @@ __device__ __forceinline__ uint32_t gmin_u(uint32_t x) {
 // partners are DPP patterns inside the 16-lane row (xor 1, 2, 3 quad_perm; xor 7
 // row_half_mirror; xor 15 row_mirror; xor 8 row_ror:8) except xor 4 (ds_swizzle).
 constexpr int QP_XOR3 = 0x1B;   // quad_perm [3,2,1,0]
+#ifndef MFF_LANE_NET
+#define MFF_LANE_NET 1
+#endif
 constexpr int ROW_ROR8 = 0x128;
 
 template <int CTRL>
@@ -301,12 +304,37 @@ __device__ __forceinline__ void glocal_tail(uint32_t (&a)[K]) {
   glocal<2, false>(a);
   glocal<1, false>(a);
 }
+// the lane's 16 keys ascending by a 60-comparator network (10 layers; checked on all 2^16
+// 0-1 inputs) instead of the 80 compare-exchanges of bitonic sizes 2..16
+__device__ __forceinline__ void gsort16_lane(uint32_t (&a)[K]) {
+  constexpr int8_t net[60][2] = {
+      {0, 13}, {1, 12}, {2, 15}, {3, 14}, {4, 8}, {5, 6}, {7, 11}, {9, 10},
+      {0, 5}, {1, 7}, {2, 9}, {3, 4}, {6, 13}, {8, 14}, {10, 15}, {11, 12},
+      {0, 1}, {2, 3}, {4, 5}, {6, 8}, {7, 9}, {10, 11}, {12, 13}, {14, 15},
+      {0, 2}, {1, 3}, {4, 10}, {5, 11}, {6, 7}, {8, 9}, {12, 14}, {13, 15},
+      {1, 2}, {3, 12}, {4, 6}, {5, 7}, {8, 10}, {9, 11}, {13, 14},
+      {1, 4}, {2, 6}, {5, 8}, {7, 10}, {9, 13}, {11, 14},
+      {2, 4}, {3, 6}, {9, 12}, {11, 13},
+      {3, 5}, {6, 8}, {7, 9}, {10, 12},
+      {3, 4}, {5, 6}, {7, 8}, {9, 10}, {11, 12},
+      {6, 7}, {8, 9}};
+#pragma unroll
+  for (int i = 0; i < 60; ++i) {
+    const uint32_t x = a[net[i][0]], y = a[net[i][1]];
+    a[net[i][0]] = min(x, y);
+    a[net[i][1]] = max(x, y);
+  }
+}
 __device__ __forceinline__ void gsort256u(uint32_t (&a)[K]) {
   // sizes 2..16 inside the lane
+#if MFF_LANE_NET
+  gsort16_lane(a);
+#else
   glocal<1, true>(a);
   glocal<2, true>(a); glocal<1, false>(a);
   glocal<4, true>(a); glocal<2, false>(a); glocal<1, false>(a);
   glocal<8, true>(a); glocal<4, false>(a); glocal<2, false>(a); glocal<1, false>(a);
+#endif
   // size 32: flip with lane ^ 1
   gcross<1, 1, true>(a); glocal_tail(a);
   // size 64: flip lane ^ 3, then lane ^ 1
