@@ -57,6 +57,10 @@ int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D
 #ifndef MFF_MERGE_OL
 #define MFF_MERGE_OL 1
 #endif
+// blocks of the exact-list launch (grid-stride over the device-side list count)
+#ifndef MFF_EXACT_GRID
+#define MFF_EXACT_GRID 1024
+#endif
 
 namespace g16 {
 
@@ -1148,7 +1152,7 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
   }
   if (part == 32) {  // the exact list kernel alone (after part 17, e.g. on another stream)
     if (w64 || !(a.fam & (F_LVL | F_PDF))) return 0;
-    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_LVL | F_PDF, 1024,
+    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_LVL | F_PDF, MFF_EXACT_GRID,
                       st, a.lvl_count, a.lvl_key, a.lvl_w);
   }
   if (part & 65) {  // the prologue of part 1: level-list counts, split key, exact-list count
@@ -1173,7 +1177,7 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
       hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b);
       MFF_LAUNCH_CHECK();
       // levels of the wide days (listed by the launch above)
-      return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_PDF, 1024, st,
+      return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_PDF, MFF_EXACT_GRID, st,
                         a.lvl_count, a.lvl_key, a.lvl_w);
     }
     // ORD in the same launch when both sorted groups are requested (part 2 then skips it)
@@ -1183,7 +1187,7 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
       // exact general path for the listed stock-days (LVL + PDF only); part 17 leaves it
       // to a later part-32 call
       rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt,
-                      F_LVL | F_PDF, 1024, st, a.lvl_count, a.lvl_key, a.lvl_w);
+                      F_LVL | F_PDF, MFF_EXACT_GRID, st, a.lvl_count, a.lvl_key, a.lvl_w);
       if (rc != 0) return rc;
     }
   }
