@@ -140,17 +140,27 @@ int mff_stage1(const float* open, const float* high, const float* low,
  * The panel's `valid` mask holds zeros for a listed stock-day except bit 31 of word 7
  * (MFF_ROWS_LISTED: bars end at 239), so the grid kernels see it ABSENT and store nothing
  * for it -- mff_stage1_rows writes all its rows and may run on another stream at the same
- * time; the row set carries every one of its rows:
+ * time.  A stock-day listed only for nulls on grid bars (its rows are its present bars)
+ * may instead keep its presence bits in `valid` and carry MFF_ROWS_KEEP plus the null
+ * fields (bit MFF_ROWS_NULL_SHIFT + i: field i = open, high, low, close, volume holds a
+ * null on some bar) in word 7 AND in the `reserved` word of its first row: then a family
+ * that reads none of those fields comes from the grid kernels (its values do not depend
+ * on the null fields) and mff_stage1_rows computes only the families that read one.
+ * The row set carries every one of its rows:
  *   rs_sd int32 [K]     d*S + s, ascending
  *   rs_off int32 [K+1]  rows of stock-day i: rs_rows[rs_off[i] .. rs_off[i+1]), at most
  *                       MFF_ROWS_MAX, in (time, frame) order (rows at one time
  *                       keep their frame order), minute_in_trade (CM:98-106) non-decreasing
  *   rs_rows MffRow [rs_off[K]]  time HHMMSSmmm in [0, 240000000), prices fp32, volume u32
  *                       shares, nulls = bit i set when field i (open, high, low, close,
- *                       volume) is null (its value is then don't-care)
+ *                       volume) is null (its value is then don't-care), reserved = 0 except
+ *                       on a kept stock-day's first row (MFF_ROWS_KEEP | null fields, as in
+ *                       its `valid` word 7)
  */
 #define MFF_ROWS_MAX 255
 #define MFF_ROWS_LISTED 0x80000000u /* valid[d][s][7] of a listed stock-day */
+#define MFF_ROWS_KEEP 0x40000000u   /* grid bars kept; only the families reading a null field listed */
+#define MFF_ROWS_NULL_SHIFT 24      /* bits 24..28: the fields holding a null (with MFF_ROWS_KEEP) */
 typedef struct MffRow {
   int32_t time;
   float open, high, low, close;

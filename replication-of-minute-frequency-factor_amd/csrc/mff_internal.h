@@ -5,6 +5,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include "../../include/mff.h"
+
 namespace mff {
 
 // thread-local last error (mff_last_error)
@@ -87,6 +89,21 @@ __host__ __device__ constexpr uint32_t kFamOf(int f) {
        : f < 24 ? F_MOMR : f < 27 ? F_MOMV : f == 27 ? F_SUMC : f < 33 ? F_SUMV : f < 39 ? F_CORR
        : f < 42 ? F_LVL : f < 47 ? F_PDF : f < 50 ? F_ORDV : f < 52 ? F_TRD : f < 54 ? F_SUMV : F_TRD;
 }
+
+// Row set (include/mff.h): the families mff_stage1_rows computes for a stock-day with
+// row-set flags `fl` (valid word 7, or its first row's `reserved`): every family, unless
+// the grid bars are kept (MFF_ROWS_KEEP) -- then those reading a field that holds a null
+// (the fields each family's grid kernel loads: open, high, low, close, volume)
+__host__ __device__ constexpr uint32_t rows_fams(uint32_t fl) {
+  const uint32_t nb = (fl >> MFF_ROWS_NULL_SHIFT) & 31u;
+  return !(fl & MFF_ROWS_KEEP) ? ~0u
+         : ((nb & 1u) ? (F_SEG | F_ORD | F_MOMR | F_TRD) : 0u) |
+           ((nb & 6u) ? (F_OLS | F_MOMH) : 0u) |
+           ((nb & 8u) ? (F_SEG | F_ORD | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD) : 0u) |
+           ((nb & 16u) ? (F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD) : 0u);
+}
+// the families a grid kernel must not store for a stock-day whose valid word 7 is w7
+__host__ __device__ constexpr uint32_t grid_skip(uint32_t w7) { return (w7 & MFF_ROWS_LISTED) ? rows_fams(w7) : 0u; }
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 

@@ -3,7 +3,9 @@
 // The dense panel holds a stock-day as 240 bars on the start-labelled grid 09:30-11:29,
 // 13:00-14:59.  Two kinds of stock-day do not fit it, and the ingest lists them in the
 // panel's row set (include/mff.h MffRow: every row of the stock-day, in (time, frame)
-// order, C4) with their mask words cleared, so the fast kernels see them ABSENT:
+// order, C4) with their mask words cleared, so the fast kernels see them ABSENT (a
+// stock-day listed only for nulls on grid bars may instead keep them, MFF_ROWS_KEEP: then
+// this kernel computes only its families that read a null field, rows_fams):
 //  * rows that exist with a null open / high / low / close / volume.  That is not a
 //    missing bar: the reference's expressions decide what a null does (SURVEY §8(c)
 //    S1-S13 plus the null rules N1-N11 / C8 of oracle/mff_oracle.py), and only
@@ -210,14 +212,22 @@ template <> struct LdsOf<F_OLS> { using type = OlsLds; };
 template <uint32_t FAMS>
 __device__ void stock_day(const Args& a, int i, typename LdsOf<FAMS>::type& L) {
   const int lane = lane_id();
-  const uint32_t fam = a.fam & FAMS;
   const int sdi = __builtin_amdgcn_readfirstlane(a.sd_list[i]);
   const int d = sdi / a.S;
   const size_t sd = (size_t)sdi;
+  const int r0 = __builtin_amdgcn_readfirstlane(a.off[i]);
+  int n = __builtin_amdgcn_readfirstlane(a.off[i + 1]) - r0;
+  n = n < 0 ? 0 : n > MFF_ROWS_MAX ? MFF_ROWS_MAX : n;  // the host checks the cap
+  // this stock-day's families (include/mff.h): every one, or for a kept stock-day (its
+  // first row's flags) those reading a field that holds a null -- the grid kernels store
+  // the others from its grid bars
+  const uint32_t fam = a.fam & FAMS &
+                       rows_fams(n > 0 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)a.rows[r0].reserved) : 0u);
+  if (!fam) return;
   const Out out{a.val, a.state, a.row, sd, (size_t)a.D * a.S};
-  // the grid kernels store nothing for a listed stock-day (mask word 7 bit 31), so every
-  // requested row of this instance's families starts ABSENT here (one store per factor,
-  // lane = factor), drained before the values below overwrite some of them
+  // the grid kernels store nothing for these families of a listed stock-day (mask word 7),
+  // so every requested row of them starts ABSENT here (one store per factor, lane =
+  // factor), drained before the values below overwrite some of them
   if (lane < NF) {
     const int rr = a.row[lane];
     if (rr >= 0 && (kFamOf(lane) & fam)) {
@@ -226,9 +236,6 @@ __device__ void stock_day(const Args& a, int i, typename LdsOf<FAMS>::type& L) {
     }
   }
   __builtin_amdgcn_s_waitcnt(0);
-  const int r0 = __builtin_amdgcn_readfirstlane(a.off[i]);
-  int n = __builtin_amdgcn_readfirstlane(a.off[i + 1]) - r0;
-  n = n < 0 ? 0 : n > MFF_ROWS_MAX ? MFF_ROWS_MAX : n;  // the host checks the cap
   if (n == 0) {  // nothing to compute: every output stays ABSENT
     if ((fam & F_PDF) && a.pdfq && lane < 5) a.pdfq[(size_t)lane * a.D * a.S + sd] = qnan();
     return;

@@ -45,6 +45,7 @@ struct S1Args {
   int S, D, nf;
   uint32_t fam;
   int8_t row[NF];          // output row of each factor id, -1 = not requested
+  uint32_t rowfam[NF];     // family of each output row (tile mode: the row set's skip)
 };
 
 struct Out {
@@ -77,9 +78,12 @@ struct Out {
 __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, uint32_t* vw, bool emit_levels = false) {
   const int lane = lane_id();
   const bool lv = lane < 60;
-  const uint32_t fam = a.fam;
   {
     const size_t sd = (size_t)d * a.S + s;
+    // the row set's families of this stock-day are mff_stage1_rows' alone (include/mff.h:
+    // every family when its mask words are zero, else a kept stock-day's families that
+    // read a field holding a null)
+    const uint32_t fam = a.fam & ~grid_skip(a.mask[sd * 8 + 7]);
 
     // ---- presence
     const uint32_t mw = lv ? a.mask[sd * 8 + (lane >> 3)] : 0u;
@@ -90,9 +94,7 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, uin
     const Bits B = ballot4(p);
     const int n = count(B);
     if (n == 0) {
-      // a stock-day of the row set (word 7 bit 31) is mff_stage1_rows' alone
-      const bool listed = (a.mask[sd * 8 + 7] >> 31) != 0u;
-      if (a.pdfq && (fam & F_PDF) && !listed) {
+      if (a.pdfq && (fam & F_PDF)) {
         if (lane < 5) a.pdfq[(size_t)lane * a.D * a.S + sd] = qnan();
       }
       return;  // every output stays ABSENT
@@ -710,7 +712,8 @@ __global__ __launch_bounds__(256) void k_stage1(S1Args a) {
   for (int i = threadIdx.x; i < nf * TILE; i += blockDim.x) {
     const int rrow = i / TILE, jj = i % TILE;
     const int s = s0 + jj;
-    if (s < a.S && (a.mask[((size_t)d * a.S + s) * 8 + 7] >> 31) == 0u) {  // row-set stock-days: skipped
+    // the row set's families: mff_stage1_rows' (include/mff.h)
+    if (s < a.S && !(grid_skip(a.mask[((size_t)d * a.S + s) * 8 + 7]) & a.rowfam[rrow])) {
       const size_t o_ = (size_t)rrow * plane + (size_t)d * a.S + s;
       a.val[o_] = sv[i];
       a.state[o_] = ss[i];
@@ -738,6 +741,7 @@ int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, c
   for (int i = 0; i < NF; ++i) a.row[i] = -1;
   for (int r = 0; r < nf; ++r) {
     a.row[ids[r]] = (int8_t)r;
+    a.rowfam[r] = kFactorFamily[ids[r]];
     a.fam |= kFactorFamily[ids[r]];
   }
   a.fam &= fam_mask;

@@ -27,6 +27,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "../../include/mff.h"
 #include "mff_group.h"
 #include "mff_fmath.h"
@@ -824,7 +826,8 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
         // and its doc_pdf levels; list entry flagged by the top bit)
         const bool wide = cmx - cmn >= (1u << 24);  // uniform inside the group
         if (wide) {
-          if (g == 0) {
+          // (not a kept row-set stock-day whose LVL / PDF come from mff_stage1_rows)
+          if (g == 0 && !(grid_skip(a.mask[sd * 8 + 7]) & (F_LVL | F_PDF))) {
             const int idx = atomicAdd(a.fb_count, 1);
             a.fb_list[idx] = (int)((uint32_t)sd | 0x80000000u);
           }
@@ -943,7 +946,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
           lds_fence();
         }
         if (!fast && !wide && (fam & (a.fam_exact))) {
-          if (g == 0) {
+          if (g == 0 && !(grid_skip(a.mask[sd * 8 + 7]) & (F_LVL | F_PDF))) {
             const int idx = atomicAdd(a.fb_count, 1);
             a.fb_list[idx] = (int)sd;
           }
@@ -965,6 +968,12 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
     // from its back; one u64 counter holds both counts (A low, B high), so the
     // reservation stays one atomic.  Levels are in descending close order (keys
     // ascending), so a group's list-A levels are its first gA.  Issued before the result stores, the reservation used after them.
+    // Row set (include/mff.h): the families mff_stage1_rows computes for this stock-day
+    // (mask word 7): none, or every one (its mask words are zero: n == 0 above), or for a
+    // kept stock-day the families that read a field holding a null -- their stores, and
+    // with doc_pdf its levels and queries, are left to mff_stage1_rows
+    const uint32_t skip = act ? grid_skip(a.mask[sd * 8 + 7]) : 0u;
+    if (skip & F_PDF) emitL = 0u;
     const bool emit = a.lvl_key != nullptr;  // uniform
     uint32_t lpreA = 0u, lpreB = 0u, gA = 0u;
     uint64_t lwb = 0ull;
@@ -999,22 +1008,25 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
     }
 
     // ---------------------------------------------------------------- stores
-    // a stock-day of the row set (mask word 7 bit 31, include/mff.h) is stored by
-    // mff_stage1_rows alone, which may run concurrently
-    const bool listed = act && (a.mask[sd * 8 + 7] >> 31) != 0u;
-    if (act && !listed) {
+    // the row set's families are stored by mff_stage1_rows alone, which may run
+    // concurrently (a kept stock-day: the family test, behind a wave-uniform branch)
+    if (act && skip != ~0u) {
+      auto store = [&](auto kept) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int f = 16 * q + g;
-        if (f < NF) {
-          const int row = a.row[f];
-          if (row >= 0) {
-            a.val[(size_t)row * plane + sd] = R.r[q];
-            a.state[(size_t)row * plane + sd] = (uint8_t)((R.st >> (8 * q)) & 0xFFu);
+        for (int q = 0; q < 4; ++q) {
+          const int f = 16 * q + g;
+          if (f < NF) {
+            const int row = a.row[f];
+            if (row >= 0 && (!decltype(kept)::value || !(kFamOf(f) & skip))) {
+              a.val[(size_t)row * plane + sd] = R.r[q];
+              a.state[(size_t)row * plane + sd] = (uint8_t)((R.st >> (8 * q)) & 0xFFu);
+            }
           }
         }
-      }
-      if (a.pdfq && g < 5) {
+      };
+      if (__builtin_amdgcn_ballot_w64(skip != 0u) == 0ull) store(std::false_type());
+      else store(std::true_type());
+      if (a.pdfq && g < 5 && !(skip & F_PDF)) {
         a.pdfq[(size_t)g * plane + sd] = qv;
       }
     }

@@ -177,10 +177,13 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   const bool act = sd0 + tix < plane;
   const size_t sd = act ? sd0 + tix : plane - 1;
 
-  bool listed = false;  // a stock-day of the row set: stored by mff_stage1_rows alone
+  // the row set's families of this stock-day (include/mff.h: every one when its mask
+  // words are zero, a kept stock-day's families reading a null field) are stored by
+  // mff_stage1_rows alone
+  uint32_t skip = 0u;
   auto put = [&](int f, double x, uint32_t st) {
     const int r = a.row[f];
-    if (r >= 0 && !listed) {
+    if (r >= 0 && !(kFamOf(f) & skip)) {
       a.val[(size_t)r * plane + sd] = x;
       a.state[(size_t)r * plane + sd] = (uint8_t)st;
     }
@@ -196,7 +199,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     M.w[0] = m0.x; M.w[1] = m0.y; M.w[2] = m0.z; M.w[3] = m0.w;
     M.w[4] = m1.x; M.w[5] = m1.y; M.w[6] = m1.z; M.w[7] = m1.w;
   }
-  listed = (M.w[7] >> 31) != 0u;  // include/mff.h: word 7 bit 31 (bars end at 239)
+  skip = grid_skip(M.w[7]);  // include/mff.h: word 7 bits 24..31 (bars end at 239)
   const int n = M.count_in(0, NBAR - 1);
   // suspended stock-days (n == 0) walk bar 0 as a stand-in and store ABSENT at the end
   const int fb = max(M.first_in(0, NBAR - 1), 0);

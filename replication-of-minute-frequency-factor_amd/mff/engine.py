@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib, catalog
-from .synth import ROW_DTYPE, pack_mask, row_set, stack_fields
+from .synth import ROW_DTYPE, ROWS_KEEP, ROWS_NULL_SHIFT, pack_mask, row_set, stack_fields
 
 ABSENT, NULL, VALUE = 0, 1, 2
 VOLUME_MAX = 2 ** 32 - 2  # MFF_VOLUME_MAX: u32 shares per bar (all-ones = absent sort key)
@@ -37,13 +37,31 @@ ROWS_MAX = 255  # MFF_ROWS_MAX
 ROWS_LISTED = -2 ** 31  # MFF_ROWS_LISTED: mask word 7 of a listed stock-day (int32 view)
 
 
-def mark_listed(mask: torch.Tensor, sd) -> None:
+def _i32(x: torch.Tensor) -> torch.Tensor:
+    """u32 values held in int64 -> their int32 bit pattern."""
+    return torch.where(x >= 2 ** 31, x - 2 ** 32, x).to(torch.int32)
+
+
+def mark_listed(mask: torch.Tensor, sd, flags=None) -> None:
     """Clear the mask words of the stock-days ``sd`` (d*S + s) and set their row-set flag
-    (include/mff.h MFF_ROWS_LISTED): the grid kernels see them ABSENT and store nothing."""
+    (include/mff.h MFF_ROWS_LISTED): the grid kernels see them ABSENT and store nothing.
+    ``flags`` (optional, [K]): a stock-day whose flags hold MFF_ROWS_KEEP keeps its
+    presence bits and gets LISTED | its flags in word 7 -- the grid kernels then store the
+    families that read none of its null fields (the same flags must be in its first row's
+    ``reserved``: mff_stage1_rows computes the others)."""
     flat = mask.view(-1, 8)
     idx = torch.as_tensor(sd, device=mask.device).long()
-    flat[idx] = 0
-    flat[idx, 7] = ROWS_LISTED
+    if flags is None:
+        flat[idx] = 0
+        flat[idx, 7] = ROWS_LISTED
+        return
+    fl = torch.as_tensor(flags, device=mask.device).to(torch.int64) & 0xFFFFFFFF
+    keep = (fl & ROWS_KEEP) != 0
+    w = flat[idx].clone()
+    w[~keep] = 0
+    w7 = w[:, 7].to(torch.int64) & 0xFFFF  # bars 224..239
+    w[:, 7] = _i32(torch.where(keep, w7 | (fl & 0x7FFF0000), torch.zeros_like(w7)) | 0x80000000)
+    flat[idx] = w
 
 
 @dataclass
@@ -91,10 +109,14 @@ class RowSet:
 
     @classmethod
     def from_panel(cls, bars: torch.Tensor, mask: torch.Tensor, sd: torch.Tensor,
-                   null_bits: Optional[torch.Tensor] = None, clear: bool = True) -> "RowSet":
+                   null_bits: Optional[torch.Tensor] = None, clear: bool = True,
+                   keep: bool = True) -> "RowSet":
         """List the grid stock-days ``sd`` (int32 device tensor, ascending) of a device panel
         as rows (mff_rows_from_panel), with optional null bits int32 [K][5][8]; ``clear``:
-        zero their mask words (the grid kernels then see them ABSENT)."""
+        mark them in the mask (mark_listed): ``keep`` -- a stock-day with a null on a present
+        bar keeps its grid bars and only the families reading a null field come from its
+        rows (MFF_ROWS_KEEP in word 7 and its first row); every other one is zeroed (the
+        grid kernels see it ABSENT)."""
         lib = _lib.load()
         D, S = int(bars.shape[1]), int(bars.shape[2])
         K = int(sd.numel())
@@ -111,8 +133,18 @@ class RowSet:
         _lib.check(lib.mff_rows_from_panel(_lib.ptr(b[0]), _lib.ptr(b[1]), _lib.ptr(b[2]), _lib.ptr(b[3]),
                                            _lib.ptr(b[4]), _lib.ptr(mask), S, D, _lib.ptr(sd), _lib.ptr(null_bits),
                                            K, _lib.ptr(off), None, _lib.ptr(rows), st), "mff_rows_from_panel")
+        flags = None
+        if keep and null_bits is not None and K > 0:
+            pres = mask.view(-1, 8)[sd.long()].to(torch.int64) & 0xFFFFFFFF  # before marking
+            nb = (null_bits.view(K, 5, 8).to(torch.int64) & 0xFFFFFFFF) & pres[:, None, :]
+            fields = ((nb != 0).any(dim=2).to(torch.int64) << torch.arange(5, device=dev)).sum(dim=1)
+            has = (fields != 0) & (off[1:] > off[:-1])
+            flags = torch.where(has, ROWS_KEEP | (fields << ROWS_NULL_SHIFT), torch.zeros_like(fields))
+            if bool(has.any()):
+                first = off[:-1].long()[has]
+                rows.view(torch.int32).view(-1, 8)[first, 7] = _i32(flags[has])
         if clear:
-            mark_listed(mask, sd)
+            mark_listed(mask, sd, flags)
         return cls(sd, off, rows)
 
 
@@ -165,9 +197,15 @@ class DevicePanel:
         bars = torch.from_numpy(np.ascontiguousarray(stack_fields(panel))).to(device)
         words = pack_mask(panel["present"])
         sd, off, rows = row_set(panel)
-        if sd.size:  # the listed stock-days go to mff_stage1_rows only (MFF_ROWS_LISTED)
-            words.reshape(-1, 8)[sd] = 0
-            words.reshape(-1, 8)[sd, 7] = np.uint32(0x80000000)
+        if sd.size:  # the listed stock-days go to mff_stage1_rows (MFF_ROWS_LISTED / KEEP)
+            w = words.reshape(-1, 8)
+            n = np.diff(off)
+            fl = np.where(n > 0, rows["reserved"][np.minimum(off[:-1], max(len(rows) - 1, 0))], 0)
+            fl = fl.astype(np.uint32) if len(rows) else np.zeros(len(sd), np.uint32)
+            keep = (fl & ROWS_KEEP) != 0
+            w[sd[~keep]] = 0
+            w[sd[keep], 7] = (w[sd[keep], 7] & np.uint32(0xFFFF)) | (fl[keep] & np.uint32(0x7FFF0000))
+            w[sd, 7] |= np.uint32(0x80000000)
         mask = torch.from_numpy(words.view(np.int32)).to(device)
         return cls(bars, mask, list(panel["codes"]), list(panel["dates"]),
                    rows=RowSet.from_host(sd, off, rows, device))

@@ -437,7 +437,7 @@ class PanelIngest:
         those cells: another table's cells of the same date stay -- and the reasons are
         returned in ``panel.dropped`` {push index: message}."""
         from .engine import DevicePanel, RowSet, mark_listed
-        from .synth import ROW_DTYPE
+        from .synth import ROW_DTYPE, ROWS_KEEP, keep_flags
 
         torch.cuda.current_stream(self.dev).wait_stream(self.stream)
         npush = len(self.table_cells)
@@ -454,11 +454,15 @@ class PanelIngest:
             if k in dropped or not (self._nulls[k] or err[k, 1] or err[k, 2]):
                 continue
             try:
-                cells, off, rows, _, _ = listed_rows(_cat_batches(self._batches(k)), self.S, self.D,
-                                                     counted=err[k, 1:3])
+                cells, off, rows, _, irregular = listed_rows(_cat_batches(self._batches(k)), self.S, self.D,
+                                                             counted=err[k, 1:3])
             except ValueError as e:
                 dropped[k] = str(e)
                 continue
+            # a stock-day listed only for nulls (its rows on the grid at distinct minutes: the
+            # kernel wrote them all, nulls filled) keeps its grid bars (MFF_ROWS_KEEP)
+            for i in np.flatnonzero(~np.asarray(irregular, dtype=bool)):
+                rows["reserved"][off[i]] = keep_flags(rows["nulls"][off[i]:off[i + 1]])
             if cells.size:
                 listed[k] = (cells, off, rows)
         # a listed stock-day's rows must come from one table
@@ -491,7 +495,10 @@ class PanelIngest:
             rows = np.concatenate([rows[starts[i]:starts[i] + n[i]] for i in order])
             sd, n = sd[order], n[order]
             off = np.concatenate([[0], np.cumsum(n)])
-            mark_listed(self.mask, sd)  # only mff_stage1_rows sees them
+            flags = np.where(n > 0, rows["reserved"][np.minimum(off[:-1], max(len(rows) - 1, 0))], 0)
+            flags = np.where(flags & ROWS_KEEP, flags, 0).astype(np.int64)
+            # only mff_stage1_rows sees them (a kept one: its families that read a null field)
+            mark_listed(self.mask, sd, torch.as_tensor(flags, device=self.dev))
             rs = RowSet.from_host(sd, off, rows, self.dev)
         dates = [_EPOCH + _dt.timedelta(days=x) for x in self.day_numbers]
         dp = DevicePanel(self.bars, self.mask, self.codes, dates, rows=rs)

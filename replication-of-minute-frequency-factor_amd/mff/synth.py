@@ -155,6 +155,16 @@ FIELDS = ("open", "high", "low", "close", "volume")
 
 ROW_DTYPE = np.dtype([("time", "<i4"), ("open", "<f4"), ("high", "<f4"), ("low", "<f4"), ("close", "<f4"),
                       ("volume", "<u4"), ("nulls", "<u4"), ("reserved", "<u4")])  # include/mff.h MffRow
+# include/mff.h MFF_ROWS_KEEP / MFF_ROWS_NULL_SHIFT: a stock-day listed only for nulls on its
+# grid bars keeps them; only the families reading a null field come from its rows
+ROWS_KEEP = 0x40000000
+ROWS_NULL_SHIFT = 24
+
+
+def keep_flags(nulls: np.ndarray) -> int:
+    """MFF_ROWS_KEEP | the null fields of a grid stock-day's rows (their ``nulls`` words)."""
+    nb = int(np.bitwise_or.reduce(np.asarray(nulls, dtype=np.uint32))) & 31 if len(nulls) else 0
+    return ROWS_KEEP | (nb << ROWS_NULL_SHIFT) if nb else 0
 
 
 def minute_time(m: np.ndarray) -> np.ndarray:
@@ -179,12 +189,15 @@ def grid_rows(panel: Dict, d: int, s: int) -> np.ndarray:
     return r
 
 
-def row_set(panel: Dict):
+def row_set(panel: Dict, keep: bool = True):
     """The row set of a host panel (include/mff.h): the stock-days that hold a polars null
     (``panel["null"]``: optional uint8 [D][S][240], bit i = FIELDS[i] null on a present bar)
     as their grid rows, plus the stock-days of ``panel["extra"]`` -- (sd [K], off [K+1],
     rows ROW_DTYPE [R]) whose rows do not fit the grid (their ``present`` bars must be
-    empty) -- merged by d*S + s.  Returns (sd int32 [K] ascending, off int32 [K+1], rows)."""
+    empty) -- merged by d*S + s.  ``keep``: a null stock-day's first row carries
+    MFF_ROWS_KEEP and its null fields (keep_flags), so it keeps its grid bars and only the
+    families reading a null field come from its rows.  Returns (sd int32 [K] ascending,
+    off int32 [K+1], rows)."""
     pres = panel["present"]
     D, S = pres.shape[:2]
     parts = {}
@@ -193,7 +206,10 @@ def row_set(panel: Dict):
         nb = np.where(pres, nb, 0).astype(np.uint8)
         d, s = np.nonzero((nb != 0).any(axis=2))
         for dd, ss in zip(d.tolist(), s.tolist()):
-            parts[dd * S + ss] = grid_rows(panel, dd, ss)
+            r = grid_rows(panel, dd, ss)
+            if keep:
+                r["reserved"][0] = keep_flags(r["nulls"])
+            parts[dd * S + ss] = r
     ex = panel.get("extra")
     if ex is not None:
         esd, eoff, erows = ex

@@ -78,6 +78,53 @@ def test_null_panel_all_factors(dev, overlap, rows_side, monkeypatch):
     assert not bad, "\n".join(bad)
 
 
+@pytest.mark.parametrize("field", range(5))
+def test_kept_stock_days_one_null_field(dev, field):
+    """A stock-day listed only for nulls on its grid bars keeps them (include/mff.h
+    MFF_ROWS_KEEP): word 7 holds LISTED | KEEP | the null field and its presence bits stay;
+    the grid kernels store the families that read none of its null fields and
+    mff_stage1_rows the others.  Nulls in one field at a time: all 58 factors against the
+    oracle, and against the same stock-days listed whole (every family from their rows,
+    RowSet.from_panel keep=False) -- the families left to the grid kernels do not depend
+    on the null field."""
+    from mff import catalog, engine, synth
+    panel = synth.make_panel(40, 3, config=55, ragged=True)
+    pres = panel["present"]
+    rng = np.random.default_rng(10 + field)
+    nb = np.where(pres & (rng.random(pres.shape) < 0.004), np.uint8(1 << field), np.uint8(0))
+    panel["null"] = nb
+    k = synth.FIELDS[field]
+    panel[k] = np.asarray(panel[k], dtype=np.float64)
+    panel[k][nb != 0] = np.nan
+    dp = engine.DevicePanel.from_host(panel, dev)
+    assert dp.rows is not None and dp.rows.K >= 10
+    sd = dp.rows.sd.long()
+    w = dp.mask.view(-1, 8)[sd].cpu().numpy().view(np.uint32)
+    assert (w[:, 7] >> 16 == (0xC000 | (1 << (8 + field)))).all()
+    assert (w[:, :7] != 0).any(axis=1).all()  # the presence bits stay
+    val, state, _ = engine.compute_factors(dp)
+    torch.cuda.synchronize()
+    bad = _check_all(val.cpu().numpy(), state.cpu().numpy(), panel)
+    assert not bad, "\n".join(bad)
+    # the same stock-days listed whole
+    bars = torch.from_numpy(np.ascontiguousarray(synth.stack_fields(panel))).to(dev)
+    mask = torch.from_numpy(synth.pack_mask(pres).view(np.int32)).to(dev)
+    hsd = dp.rows.sd.cpu().numpy()
+    d, s = hsd // pres.shape[1], hsd % pres.shape[1]
+    bits = np.stack([synth.pack_mask(((nb[d, s] >> i) & 1).astype(bool)) for i in range(5)], axis=1)
+    rs = engine.RowSet.from_panel(bars, mask, dp.rows.sd, torch.from_numpy(bits.view(np.int32).reshape(-1, 5, 8)).to(dev),
+                                  keep=False)
+    wz = mask.view(-1, 8)[sd].cpu().numpy().view(np.uint32)
+    assert (wz[:, :7] == 0).all() and (wz[:, 7] == 0x80000000).all()
+    whole = engine.compute_factors(engine.DevicePanel(bars, mask, list(panel["codes"]), list(panel["dates"]), rows=rs))
+    torch.cuda.synchronize()
+    bad = []
+    for i, nm in enumerate(catalog.NAMES):
+        bad += compare(val[i].cpu().numpy(), state[i].cpu().numpy(), whole[0][i].cpu().numpy(),
+                       whole[1][i].cpu().numpy(), nm)
+    assert not bad, "\n".join(bad)
+
+
 def test_null_subsets_and_order(dev):
     """A factor subset in another row order (the null kernel's row map) and a subset
     without doc_pdf (phase 1 skipped)."""

@@ -93,9 +93,16 @@ def test_row_set_matches_host_restatement(dev):
     for i, k in enumerate(("open", "high", "low", "close", "volume")):
         ok = (rows["nulls"] >> i) & 1 == 0  # values under a null are don't-care
         assert np.array_equal(rows[k][ok], hrows[k][ok]), k
-    # the listed stock-days are ABSENT to the grid kernels and flagged (MFF_ROWS_LISTED)
+    # the listed stock-days with a row off the grid or at a duplicate time are ABSENT to the
+    # grid kernels (MFF_ROWS_LISTED alone); those listed only for nulls keep their grid bars
+    # and carry MFF_ROWS_KEEP with their null fields, in word 7 and on their first row
     w = dp.mask.view(-1, 8)[torch.as_tensor(sd, device=dev)].cpu().numpy().view(np.uint32)
-    assert (w[:, :7] == 0).all() and (w[:, 7] == 0x80000000).all()
+    fl = rows["reserved"][off[:-1]]
+    kept = (fl & synth.ROWS_KEEP) != 0
+    assert kept.any() and (~kept).any()
+    assert (w[~kept, :7] == 0).all() and (w[~kept, 7] == 0x80000000).all()
+    assert (w[kept, 7] >> 16 == (0x8000 | (fl[kept] >> 16))).all() and (w[kept, :7] != 0).any(axis=1).all()
+    assert (fl == hrows["reserved"][hoff[:-1]]).all()
 
 
 def test_rows_from_device_panel(dev):

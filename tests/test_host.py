@@ -158,3 +158,41 @@ def test_row_set_shard_matches_subpanel_rows():
         assert got[0].tolist() == want[0].tolist() and got[1].tolist() == want[1].tolist()
         for k in ("time", "nulls", "volume", "close"):
             assert np.array_equal(got[2][k], want[2][k], equal_nan=True), k
+
+
+def test_kept_stock_day_flags():
+    """A stock-day listed only for nulls on its grid bars (include/mff.h MFF_ROWS_KEEP): its
+    first row's `reserved` and its mask word 7 carry LISTED | KEEP | the null fields, and
+    its presence bits stay; a stock-day with rows off the grid is zeroed as before; and
+    engine.mark_listed / the kernels' family rule agree (synth.keep_flags, rows_fams)."""
+    import torch
+    from mff import engine, synth
+    panel = synth.make_panel(10, 2, config=72, ragged=True)
+    pres = panel["present"]
+    nb = np.zeros(pres.shape, np.uint8)
+    d0, s0 = np.argwhere(pres.any(axis=2))[0]
+    bars = np.flatnonzero(pres[d0, s0])
+    nb[d0, s0, bars[3]] = 16  # a null volume
+    nb[d0, s0, bars[7]] = 2   # a null high
+    panel["null"] = nb
+    for i, k in enumerate(synth.FIELDS):
+        panel[k] = np.asarray(panel[k], dtype=np.float64)
+        panel[k][(nb >> i) & 1 == 1] = np.nan
+    sd, off, rows = synth.row_set(panel)
+    S = pres.shape[1]
+    assert sd.tolist() == [d0 * S + s0]
+    fl = int(rows["reserved"][off[0]])
+    assert fl == synth.ROWS_KEEP | (18 << synth.ROWS_NULL_SHIFT)
+    assert (rows["reserved"][off[0] + 1:off[1]] == 0).all()
+    dp = engine.DevicePanel.from_host(panel, "cpu")
+    w = dp.mask.view(-1, 8)[int(sd[0])].numpy().view(np.uint32)
+    want = synth.pack_mask(pres[d0, s0][None])[0]
+    assert (w[:7] == want[:7]).all() and w[7] == (want[7] | 0x80000000 | fl)
+    assert not synth.row_set(panel, keep=False)[2]["reserved"].any()
+    # mark_listed: kept (flags) and whole (no flags) side by side
+    mask = torch.from_numpy(synth.pack_mask(pres).view(np.int32).copy())
+    other = int(np.argwhere(pres.reshape(-1, 240).any(axis=1)).ravel()[-1])
+    engine.mark_listed(mask, [int(sd[0]), other], torch.tensor([fl, 0]))
+    m = mask.view(-1, 8).numpy().view(np.uint32)
+    assert (m[int(sd[0])] == w).all()
+    assert (m[other, :7] == 0).all() and m[other, 7] == 0x80000000
