@@ -37,6 +37,17 @@ ROWS_MAX = 255  # MFF_ROWS_MAX
 ROWS_LISTED = -2 ** 31  # MFF_ROWS_LISTED: mask word 7 of a listed stock-day (int32 view)
 
 
+def first_row_flags(off: np.ndarray, rows: np.ndarray) -> np.ndarray:
+    """uint32 [K]: the row-set flags of each listed stock-day (its first row's `reserved`,
+    include/mff.h MFF_ROWS_KEEP; 0 for a stock-day without rows)."""
+    off = np.asarray(off, dtype=np.int64)
+    fl = np.zeros(len(off) - 1, np.uint32)
+    has = off[1:] > off[:-1]
+    if has.any():
+        fl[has] = rows["reserved"][off[:-1][has]]
+    return fl
+
+
 def _i32(x: torch.Tensor) -> torch.Tensor:
     """u32 values held in int64 -> their int32 bit pattern."""
     return torch.where(x >= 2 ** 31, x - 2 ** 32, x).to(torch.int32)
@@ -199,9 +210,7 @@ class DevicePanel:
         sd, off, rows = row_set(panel)
         if sd.size:  # the listed stock-days go to mff_stage1_rows (MFF_ROWS_LISTED / KEEP)
             w = words.reshape(-1, 8)
-            n = np.diff(off)
-            fl = np.where(n > 0, rows["reserved"][np.minimum(off[:-1], max(len(rows) - 1, 0))], 0)
-            fl = fl.astype(np.uint32) if len(rows) else np.zeros(len(sd), np.uint32)
+            fl = first_row_flags(off, rows)
             keep = (fl & ROWS_KEEP) != 0
             w[sd[~keep]] = 0
             w[sd[keep], 7] = (w[sd[keep], 7] & np.uint32(0xFFFF)) | (fl[keep] & np.uint32(0x7FFF0000))

@@ -436,7 +436,7 @@ class PanelIngest:
         the reference's per-file call fails, MinuteFrequentFactorCICC.py:18-25, 95) -- only
         those cells: another table's cells of the same date stay -- and the reasons are
         returned in ``panel.dropped`` {push index: message}."""
-        from .engine import DevicePanel, RowSet, mark_listed
+        from .engine import DevicePanel, RowSet, first_row_flags, mark_listed
         from .synth import ROW_DTYPE, ROWS_KEEP, keep_flags
 
         torch.cuda.current_stream(self.dev).wait_stream(self.stream)
@@ -495,8 +495,8 @@ class PanelIngest:
             rows = np.concatenate([rows[starts[i]:starts[i] + n[i]] for i in order])
             sd, n = sd[order], n[order]
             off = np.concatenate([[0], np.cumsum(n)])
-            flags = np.where(n > 0, rows["reserved"][np.minimum(off[:-1], max(len(rows) - 1, 0))], 0)
-            flags = np.where(flags & ROWS_KEEP, flags, 0).astype(np.int64)
+            flags = first_row_flags(off, rows).astype(np.int64)
+            flags = np.where(flags & ROWS_KEEP, flags, 0)
             # only mff_stage1_rows sees them (a kept one: its families that read a null field)
             mark_listed(self.mask, sd, torch.as_tensor(flags, device=self.dev))
             rs = RowSet.from_host(sd, off, rows, self.dev)
