@@ -1125,9 +1125,17 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
     a.row[id] = (int8_t)r;
     a.fam |= kFactorFamily[id];
   }
-  const uint32_t use[5] = {F_SEG | F_ORD | F_MOMR | F_TRD, F_OLS | F_MOMH, F_OLS | F_MOMH,
-                           F_SEG | F_ORD | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD,
-                           F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD};
+  constexpr uint32_t use[5] = {F_SEG | F_ORD | F_MOMR | F_TRD, F_OLS | F_MOMH, F_OLS | F_MOMH,
+                               F_SEG | F_ORD | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD,
+                               F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD};
+  // a kept row-set stock-day's null field sends exactly the families that read it to
+  // mff_stage1_rows (include/mff.h MFF_ROWS_KEEP; rows_fams in mff_internal.h)
+  static_assert(rows_fams(MFF_ROWS_KEEP | (1u << MFF_ROWS_NULL_SHIFT)) == use[0], "open");
+  static_assert(rows_fams(MFF_ROWS_KEEP | (2u << MFF_ROWS_NULL_SHIFT)) == use[1], "high");
+  static_assert(rows_fams(MFF_ROWS_KEEP | (4u << MFF_ROWS_NULL_SHIFT)) == use[2], "low");
+  static_assert(rows_fams(MFF_ROWS_KEEP | (8u << MFF_ROWS_NULL_SHIFT)) == use[3], "close");
+  static_assert(rows_fams(MFF_ROWS_KEEP | (16u << MFF_ROWS_NULL_SHIFT)) == use[4], "volume");
+  static_assert(rows_fams(MFF_ROWS_LISTED) == ~0u && grid_skip(0u) == 0u, "listed whole / not listed");
   for (int f = 0; f < 5; ++f)
     MFF_REQUIRE(!(a.fam & use[f]) || fld[f] != nullptr, "mff_stage1: field plane %d required", f);
   MFF_REQUIRE(!(a.fam & F_PDF) || (pdf_query != nullptr && pdf_levels != nullptr),
