@@ -125,6 +125,22 @@ def test_kept_stock_days_one_null_field(dev, field):
     assert not bad, "\n".join(bad)
 
 
+def test_kept_stock_days_w64_impl(dev, monkeypatch):
+    """MFF_STAGE1_IMPL=w64 (the wave-per-stock-day kernel for every family, tile mode) on a
+    null panel whose listed stock-days keep their grid bars: its tile stores skip a kept
+    stock-day's row-set families (S1Args.rowfam) -- all 58 factors against the oracle."""
+    from mff import engine
+    monkeypatch.setenv("MFF_STAGE1_IMPL", "w64")
+    panel = _null_panel(40, 2, config=56)
+    dp = engine.DevicePanel.from_host(panel, dev)
+    w = dp.mask.view(-1, 8)[dp.rows.sd.long()].cpu().numpy().view(np.uint32)
+    assert ((w[:, 7] & 0x40000000) != 0).sum() >= 5  # kept stock-days
+    val, state, _ = engine.compute_factors(dp)
+    torch.cuda.synchronize()
+    bad = _check_all(val.cpu().numpy(), state.cpu().numpy(), panel)
+    assert not bad, "\n".join(bad)
+
+
 def test_null_subsets_and_order(dev):
     """A factor subset in another row order (the null kernel's row map) and a subset
     without doc_pdf (phase 1 skipped)."""
