@@ -16,6 +16,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--stocks", type=int, default=5000)
 ap.add_argument("--days", type=int, default=250)
 ap.add_argument("--rate", type=float, default=0.1)
+ap.add_argument("--whole", action="store_true", help="list the stock-days whole (every family from rows)")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 S, D = args.stocks, args.days
@@ -29,7 +30,7 @@ f = torch.randint(0, 5, (K,), generator=g, device=dev)
 bits = torch.zeros((K, 5, 8), dtype=torch.int64, device=dev)
 bits[torch.arange(K, device=dev), f, m // 32] = torch.bitwise_left_shift(torch.ones_like(m), m % 32)
 bits = torch.where(bits >= 2 ** 31, bits - 2 ** 32, bits).to(torch.int32)
-rs = engine.RowSet.from_panel(bars, mask, sd, bits)
+rs = engine.RowSet.from_panel(bars, mask, sd, bits, keep=not args.whole)
 lib = _lib.load()
 ids = list(range(58))
 val = torch.empty((58, D, S), dtype=torch.float64, device=dev)
@@ -51,7 +52,7 @@ def run(sel, phase):
                                    _lib.ptr(pdfq), _lib.ptr(levels), phase, st.cuda_stream), "rows")
 
 
-print(f"K = {K} listed stock-days ({args.rate:.1%} of {S} x {D})")
+print(f"K = {K} listed stock-days ({args.rate:.1%} of {S} x {D}){' listed whole' if args.whole else ' (kept)'}")
 for name, sel, phase in sets:
     run(sel, phase)
     torch.cuda.synchronize()

@@ -39,6 +39,7 @@
 #include <string.h>
 
 #include "../../include/mff.h"
+#include "mff_fmath.h"
 #include "mff_internal.h"
 #include "mff_w64.h"
 #include "mff_wave.h"
@@ -169,16 +170,19 @@ __device__ __forceinline__ Win ols_window(const OlsLds& L, int r0, int r1, doubl
   w.vxn = nx == 0;
   w.vyn = ny == 0;
   w.covn = np_ == 0;
+  // tolerance-only statistics: the counts' reciprocals (mff_fmath.h) instead of divisions;
+  // a constant side's exact zero comes from its flag (C3), not from the arithmetic
+  const double rx = frcp((double)max(nx, 1)), ry = frcp((double)max(ny, 1)), rp = frcp((double)max(np_, 1));
   const double sx = sum(0), sy = sum(1);
-  w.mx = nx ? X0 + sx / (double)nx : 0.0;
-  w.my = ny ? Y0 + sy / (double)ny : 0.0;
-  w.vx = (w.vxn || constant(0, 0)) ? 0.0 : (sum(2) - sx * sx / (double)nx) / (double)nx;
-  w.vy = (w.vyn || constant(1, 8)) ? 0.0 : (sum(3) - sy * sy / (double)ny) / (double)ny;
+  w.mx = nx ? X0 + sx * rx : 0.0;
+  w.my = ny ? Y0 + sy * ry : 0.0;
+  w.vx = (w.vxn || constant(0, 0)) ? 0.0 : (sum(2) - sx * sx * rx) * rx;
+  w.vy = (w.vyn || constant(1, 8)) ? 0.0 : (sum(3) - sy * sy * ry) * ry;
   if (w.covn || constant(2, 16) || constant(2, 24)) {
     w.cov = 0.0;
   } else {
     const double spx = sum(4), spy = sum(5);
-    w.cov = (sum(6) - spx * spy / (double)np_) / (double)np_;
+    w.cov = (sum(6) - spx * spy * rp) * rp;
   }
   return w;
 }
@@ -912,17 +916,19 @@ __device__ void stock_day(const Args& a, int i, typename LdsOf<FAMS>::type& L) {
           // cond or null operand: N1)
           if (!w.vxn && w.vx != 0.0) {
             okb[k] = !w.covn;
-            beta[k] = w.cov / w.vx;
+            beta[k] = fdiv(w.cov, w.vx);
           } else {
             okb[k] = !w.vxn && !w.vyn;
-            beta[k] = w.my / w.mx;
+            beta[k] = fdiv(w.my, w.mx);
           }
           const double prod = w.vx * w.vy;
           okq[k] = !w.vxn && !w.vyn && prod != 0.0 && !w.covn;
           if (okq[k]) {
-            q[k] = sqrt(w.cov) / prod;      // cov**0.5 / (vx*vy)   CM:137
-            cs[k] = (w.cov * w.cov) / prod;  // cov**2 / (vx*vy)     CM:212
-            cr[k] = w.cov / sqrt(prod);      // cov / (vx*vy)**0.5   CM:261
+            // one refined rsqrt of the product serves all three (prod < 0: NaN, as sqrt)
+            const double rs = frsq(prod), ip = rs * rs;
+            q[k] = (w.cov == 0.0 ? 0.0 : fsqrt(w.cov)) * ip;  // cov**0.5 / (vx*vy)   CM:137
+            cs[k] = w.cov * w.cov * ip;                        // cov**2 / (vx*vy)     CM:212
+            cr[k] = w.cov * rs;                                // cov / (vx*vy)**0.5   CM:261
           }
           if (!okb[k]) beta[k] = 0.0;
         }
