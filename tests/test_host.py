@@ -196,3 +196,18 @@ def test_kept_stock_day_flags():
     m = mask.view(-1, 8).numpy().view(np.uint32)
     assert (m[int(sd[0])] == w).all()
     assert (m[other, :7] == 0).all() and m[other, 7] == 0x80000000
+
+
+def test_python_mirrors_of_header_constants():
+    """The host-side mirrors of include/mff.h's constants (row set flags, caps, states)
+    equal the header's values."""
+    from mff import engine
+    txt = open(HEADER).read()
+    defs = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"#define (MFF_\w+) (0x[0-9A-Fa-f]+|\d+)u?\b", txt)}
+    assert defs["MFF_ROWS_LISTED"] == engine.ROWS_LISTED & 0xFFFFFFFF
+    assert defs["MFF_ROWS_KEEP"] == synth.ROWS_KEEP
+    assert defs["MFF_ROWS_NULL_SHIFT"] == synth.ROWS_NULL_SHIFT
+    assert defs["MFF_ROWS_MAX"] == engine.ROWS_MAX
+    assert synth.ROW_DTYPE.itemsize == 32  # MffRow
+    # the kept flags leave the presence bits of bars 224..239 (word 7 bits 0..15) alone
+    assert (synth.ROWS_KEEP | (31 << synth.ROWS_NULL_SHIFT) | defs["MFF_ROWS_LISTED"]) & 0xFFFF == 0
