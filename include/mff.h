@@ -103,7 +103,7 @@ int mff_ingest_rows(const int32_t* stock, const int32_t* day, const int64_t* tim
  * (filled and counted by the call itself), in two lists split at a key the library sets
  * per call (the mean median doc_pdf query of earlier calls on the device; 1.0 before
  * any: any key gives the same ranks): the keys below it from the front of the day's
- * S*240 slots, the others from the back, with the per-day counts (u32 pairs A, B = one
+ * S*256 slots (at most 255 levels per stock-day: MFF_ROWS_MAX), the others from the back, with the per-day counts (u32 pairs A, B = one
  * u64 counter per day) and the split key u64 in front.
  * workspace: mff_stage1_workspace_bytes(S, D) bytes of device scratch (the list of
  * stock-days the exact general path finishes; zeroed by the call itself).

@@ -80,7 +80,11 @@ does (``DayFrame.time``; the time filters CM:18-84, 770-815, 1212-1387 and
   duplicate minute share one window.
 * C9 ``sort(by=[code, date, time])`` (CM:19, 34, 70, 85) keeps rows at one time in frame
   order (polars' sort is not promised stable; the build takes the stable order).
-Neither is pinned by a polars run.
+* T2 the same ``rolling()`` rejects an index that decreases inside a group (a row inside
+  the 11:30-13:00 break before an afternoon row): the whole ``cal_mmt_ols_*`` call raises
+  (:class:`RollingUnsorted`), so the driver drops that day file for the five OLS factors
+  only (MF:18-25, 95); the other 53 calls on the file are unaffected.
+None of these is pinned by a polars run.
 """
 from __future__ import annotations
 
@@ -491,8 +495,15 @@ def _ols_windows(df: DayFrame, s: int, e: int):
     return cache[(s, e)]
 
 
+class RollingUnsorted(ValueError):
+    """polars' rolling() on an index column that is not sorted inside a group (T2)."""
+
+
 def _ols_windows_calc(df: DayFrame, s: int, e: int):
     mins = _minute_in_trade(df.time[s:e])
+    if (np.diff(mins) < 0).any():  # T2: the whole call raises (CM:114-118)
+        raise RollingUnsorted("rolling(): index column 'minute_in_trade' is not sorted within a group "
+                              "(CM:114-118)")
     x = df.low[s:e]
     y = df.high[s:e]
     xok = ~df.null["low"][s:e]
@@ -1191,7 +1202,10 @@ def oracle_stage1(panel, names: Sequence[str] = None):
     for d in range(D):
         df = day_frame_from_panel(panel, d)
         for fi, nm in enumerate(names):
-            res = ORACLE_FUNCS[nm](df)
+            try:
+                res = ORACLE_FUNCS[nm](df)
+            except RollingUnsorted:  # T2: the call on this day frame raises -> no rows (MF:18-25)
+                continue
             for code, x in res.items():
                 s = code_index[code]
                 if x is None:

@@ -1,5 +1,5 @@
 # Round-3 stage-1 profile (GPU box): headline bench line, overlapped pass kernel trace
-# (per-pass timeline), and the launches one at a time (MFF_PDF_OVERLAP=0 MFF_HL_STREAM=0:
+# (per-pass timeline), and the launches one at a time (MFF_STAGE1_SERIAL=1:
 # standalone per-kernel durations).  usage: bash profiles/gpu_r3_prof.sh TAG
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -13,7 +13,7 @@ export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/overlap -o trace --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-extras --steps 4 --warmup 1 > $OUT/overlap.log 2>&1 || { echo PROF_FAILED; tail -20 $OUT/overlap.log; exit 1; }
 python3 $R/profiles/pass_span.py $OUT/overlap $OUT/pass_spans.csv > $OUT/pass_timeline.log 2>&1 || true
-export MFF_PDF_OVERLAP=0 MFF_HL_STREAM=0
+export MFF_STAGE1_SERIAL=1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/serial -o trace --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-extras --steps 4 --warmup 1 > $OUT/serial.log 2>&1 || { echo PROF2_FAILED; tail -20 $OUT/serial.log; exit 1; }
 find $OUT -name "*kernel_trace.csv" -delete
 tail -8 $OUT/pass_timeline.log

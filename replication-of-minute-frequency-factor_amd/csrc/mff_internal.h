@@ -43,6 +43,12 @@ void clear_error();
 // counter (list A count low, list B high), then the u64 split key of this pass's lists
 // at pdf_koff(D) (keys below it in list A)
 __host__ __device__ inline size_t pdf_koff(int D) { return (size_t)8 * (size_t)D; }
+// level-list slots per day: one level per distinct close of a stock-day, at most its rows
+// -- 240 grid bars, or MFF_ROWS_MAX = 255 rows of a row-set stock-day (the host rejects
+// more) -- so S x 256 slots hold lists A and B of any day; a multiple of 16 entries, so
+// every day's keys start 128-B and its weight bytes 16-B aligned (the count's vector loads)
+__host__ __device__ inline size_t pdf_day_cap(int S) { return (size_t)S * 256; }
+static_assert(MFF_ROWS_MAX <= 256, "pdf_day_cap holds MFF_ROWS_MAX levels per stock-day");
 __device__ inline uint64_t pdf_split_key(const uint32_t* lvl_count, int D) {
   return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(lvl_count) + pdf_koff(D));
 }

@@ -407,7 +407,7 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
     // takes UNR consecutive entries (chunk c = entries [UNR c, UNR c + UNR)): the keys as
     // four 16-B loads and the bars as one 8-B load (a wave reads 4 KB of keys
     // contiguously) instead of UNR strided key and byte loads.  Every day's list starts
-    // 64-B aligned (pdf_levels_split: S x 240 entries per day), so the vector loads are
+    // 64-B aligned (pdf_day_cap: S x 256 entries per day), so the vector loads are
     // aligned; the last partial chunk loads entry by entry.
     static_assert(UNR == 8 || UNR == 16, "chunk loads assume 8 or 16 entries");
     int s = 0, e = 0, s8 = 0;  // the list being read: entries [s, e), chunks from s8 = s rounded down
@@ -893,7 +893,7 @@ static void pdf_levels_args(PdfArgs& a, const void* pdf_levels, int S, int D) {
   a.lvl_count = reinterpret_cast<const uint32_t*>(base);
   a.lvl_key = reinterpret_cast<const uint64_t*>(base + ok);
   a.lvl_w = reinterpret_cast<const uint8_t*>(base + ow);
-  a.cap = (size_t)S * NBAR;
+  a.cap = pdf_day_cap(S);
 }
 
 int mff_pdf_count(const void* pdf_levels, int S_loc, int D, int d0, int nd,

@@ -479,7 +479,7 @@ __device__ void stock_day_w64(const S1Args& a, int d, int s, const Out& out, uin
         }
         idxA += (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)base);
         idxB += (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(base >> 32));
-        const size_t cap = (size_t)a.S * NBAR;
+        const size_t cap = pdf_day_cap(a.S);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (lend[k]) {

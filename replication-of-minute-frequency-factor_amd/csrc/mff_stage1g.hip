@@ -56,13 +56,8 @@ int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D
 #ifndef MFF_GWAVES
 #define MFF_GWAVES 5
 #endif
-#ifndef MFF_MERGE_OL
-#define MFF_MERGE_OL 1
-#endif
 // blocks of the exact-list launch (grid-stride over the device-side list count)
-#ifndef MFF_EXACT_GRID
-#define MFF_EXACT_GRID 1024
-#endif
+constexpr int kExactGrid = 1024;
 
 namespace g16 {
 
@@ -1040,7 +1035,7 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)lwb);
       const uint32_t baseA = (uint32_t)wb + lpreA, baseB = (uint32_t)(wb >> 32) + lpreB;
       const uint32_t* lc = reinterpret_cast<const uint32_t*>(scr) + NBAR;
-      const size_t capd = (size_t)a.S * NBAR;
+      const size_t capd = pdf_day_cap(a.S);
       uint64_t* kd = a.lvl_key + (size_t)d * capd;
       uint8_t* wd = a.lvl_w + (size_t)d * capd;
       for (int l = g; l < (int)emitL; l += 16) {
@@ -1068,14 +1063,14 @@ extern "C" size_t mff_stage1_workspace_bytes(int S, int D) {
 }
 
 namespace mff {
-// doc_pdf level side channel: counts u32 [D] | keys u64 [D][S*240] | bars u8 [D][S*240]
+// doc_pdf level side channel: counts u32 [D] | keys u64 [D][S*256] | bars u8 [D][S*256]
 // (a day holds at most one level per bar of every stock)
 // level buffer: per day the entry counts of list A and list B (u32 pairs, A first: one
 // u64 counter per day) and the split key (u64, pdf_koff), then
-// the keys u64 [D][S * 240] and the bars u8 [D][S * 240]; list A (keys below the split
-// key) fills a day's S * 240 slots from the front, list B from the back
+// the keys u64 [D][S * 256] and the bars u8 [D][S * 256] (pdf_day_cap); list A (keys below
+// the split key) fills a day's slots from the front, list B from the back
 size_t pdf_levels_split(int S, int D, size_t* off_key, size_t* off_w) {
-  const size_t cap = (size_t)S * (size_t)D * NBAR;
+  const size_t cap = pdf_day_cap(S) * (size_t)D;
   *off_key = (pdf_koff(D) + 8 + 255) & ~(size_t)255;
   *off_w = *off_key + cap * 8;
   return *off_w + cap;
@@ -1172,7 +1167,7 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
   }
   if (part == 32) {  // the exact list kernel alone (after part 17, e.g. on another stream)
     if (w64 || !(a.fam & (F_LVL | F_PDF))) return 0;
-    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_LVL | F_PDF, MFF_EXACT_GRID,
+    return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_LVL | F_PDF, kExactGrid,
                       st, a.lvl_count, a.lvl_key, a.lvl_w);
   }
   if (part & 65) {  // the prologue of part 1: level-list counts, split key, exact-list count
@@ -1197,17 +1192,17 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
       hipLaunchKernelGGL(g16::k_stage1g<g16::G_LVL>, dim3((unsigned)nblk), dim3(256), 0, st, b);
       MFF_LAUNCH_CHECK();
       // levels of the wide days (listed by the launch above)
-      return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_PDF, MFF_EXACT_GRID, st,
+      return launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt, F_PDF, kExactGrid, st,
                         a.lvl_count, a.lvl_key, a.lvl_w);
     }
     // ORD in the same launch when both sorted groups are requested (part 2 then skips it)
-    int rc = group_launch(MFF_MERGE_OL && (a.fam & g16::G_ORD) && (a.fam & (F_LVL | F_PDF)) ? 2 : 1);
+    int rc = group_launch((a.fam & g16::G_ORD) && (a.fam & (F_LVL | F_PDF)) ? 2 : 1);
     if (rc != 0) return rc;
     if ((a.fam & (F_LVL | F_PDF)) && !(part & 16)) {
       // exact general path for the listed stock-days (LVL + PDF only); part 17 leaves it
       // to a later part-32 call
       rc = launch_w64(fld, valid, S, D, factor_ids, nf, val, state, pdf_query, a.fb_list, cnt,
-                      F_LVL | F_PDF, MFF_EXACT_GRID, st, a.lvl_count, a.lvl_key, a.lvl_w);
+                      F_LVL | F_PDF, kExactGrid, st, a.lvl_count, a.lvl_key, a.lvl_w);
       if (rc != 0) return rc;
     }
   }
@@ -1217,7 +1212,7 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
     return launch_serial(fld, valid, S, D, a.row, a.fam & kHL, val, state, a.ord_th, st);
   }
   if ((part & 2) && !w64) {  // the ORD sort (thresholds) before the serial kernels (products)
-    if (!(MFF_MERGE_OL && (a.fam & g16::G_ORD) && (a.fam & (F_LVL | F_PDF)))) {
+    if (!((a.fam & g16::G_ORD) && (a.fam & (F_LVL | F_PDF)))) {
       const int rc = group_launch(0);
       if (rc != 0) return rc;
     }

@@ -82,21 +82,6 @@ constexpr uint32_t kPairB = MFF_PAIR_SPLIT ? (F_SUMC | F_CORR) : kSerB;
 #ifndef MFF_SERH_FAST
 #define MFF_SERH_FAST 1
 #endif
-#ifndef MFF_CAPTURE_BRANCH
-#define MFF_CAPTURE_BRANCH 0
-#endif
-#ifndef MFF_PAIR_QREAD
-#define MFF_PAIR_QREAD 0
-#endif
-// set H's lag chunk (c-3, the bars leaving the 50-bar windows) from a register ring of the
-// last three chunks instead of a second LDS-DMA of chunk c-3
-#ifndef MFF_SERH_VRING
-#define MFF_SERH_VRING 1
-#endif
-// set H's beta from the window's 1 / (var_x var_y) when it is computed (no f64 division)
-#ifndef MFF_SERH_BETA_MUL
-#define MFF_SERH_BETA_MUL 1
-#endif
 
 // ---- presence bits of one stock-day: 8 words, bit m%32 of word m/32 (compile-time
 // word indices only, so the array stays in registers)
@@ -346,7 +331,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       const double prod = Vx * Vy;
       const bool qw = !cx && !cy && prod != 0.0;
       double beta;
-      if (MFF_SERH_BETA_MUL && qw) {
+      if (qw) {
         // cov / var_x = cov * var_y / (var_x var_y): the window's 1 / prod serves beta too
         // (one rounding more than the quotient, no division)
         const double rp = frsq(prod);  // prod < 0: NaN, as sqrt(prod)
@@ -390,13 +375,12 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         const bool up = pk & (r > 0.0), dn = pk & (r < 0.0);  // r is finite (no NaN case)
         nu += up ? 1 : 0;
         ndn += dn ? 1 : 0;
-        // first up / down member of each lane: a wave-uniform branch, taken only while
-        // some lane still meets its first one (the first few bars), not a select per bar
+        // first up / down member of each lane
         const bool cu = up & !hu, cd = dn & !hd;
-        if (MFF_CAPTURE_BRANCH ? __builtin_amdgcn_ballot_w64(cu | cd) != 0ull : true) {
-          xu = cu ? r : xu;
-          xd = cd ? r : xd;
-        }
+        // (selects: a wave-uniform branch taken only while some lane meets its first one
+        // measured much slower here, round 3)
+        xu = cu ? r : xu;
+        xd = cd ? r : xd;
         hu |= up;
         hd |= dn;
         const double eu = up ? r - xu : 0.0, ed = dn ? r - xd : 0.0;
@@ -476,8 +460,8 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
           // first pair: the shifts, behind a wave-uniform branch taken only while some
           // lane meets its second non-zero-volume row (set B bounds the wave pair: its
           // walk 16.9 ms vs set A's 15.6 with both waves on one set; the branch instead of
-          // six selects per bar: pair 16.2 -> 15.8 ms.  Set A's capture stays select-based,
-          // MFF_CAPTURE_BRANCH: its branch form measured much slower)
+          // six selects per bar: pair 16.2 -> 15.8 ms.  Set A's capture stays select-based:
+          // its branch form measured much slower)
           if (__builtin_amdgcn_ballot_w64(nzc == 1) != 0ull) {
             if (nzc == 1) { x5 = pcz; y5 = pvz; x6 = c; }
           }
@@ -540,14 +524,14 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     // chunk is in flight while this one is used.  The image is [row][quad] with the quad
     // slot XOR-swizzled by (row >> 2) & 3 on the SOURCE address (the DMA destination is
     // lane-linear), so each lane's ds_read_b128 of its own row is bank-conflict free.
-    // OLS also stages chunk c-3 (its bars 2..15 are the bars 50 back of bars 0..13 of
-    // chunk c; bars 14, 15 of chunk c-4 are carried in registers).
+    // OLS keeps the last three chunks in registers (RG): bars 2..15 of chunk c-3 are the
+    // bars 50 back of bars 0..13 of chunk c; bars 14, 15 of chunk c-4 are carried.  (A
+    // second LDS-DMA of chunk c-3 instead cost 18 % of set H, round 4.)
     constexpr uint32_t PLM = PAIR ? kPairPlanes : kPlanes(SET);
     constexpr int NP = __builtin_popcount(PLM);
     constexpr bool LAG = (SET & F_OLS) != 0u;
     static_assert(!(PAIR && LAG), "the pair form covers sets A and B");
-    constexpr bool VRING = LAG && MFF_SERH_VRING;
-    constexpr int NB = LAG && !VRING ? 2 * NP : NP;  // images: the planes, then their lag copies
+    constexpr int NB = NP;  // images: one per plane
     // chunk = CQ quads (4*CQ bars) per stock-day; the lag sets use 8-bar chunks so the
     // staged registers (NB*CQ float4) leave room for a third wave per SIMD
     constexpr int CQ = PAIR ? 4 : (SET == kSerB || SET == kSerAB) ? 2 : 4, BC = 4 * CQ;
@@ -605,10 +589,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       return x;
     };
     Q4 carry;  // lag bars BC-2, BC-1 of chunk c-1-LAGC (in .z .w)
-    // VRING: chunks c-3, c-2, c-1 of the planes (slot 0 = the lag chunk of chunk c)
-    float4 RG[VRING ? LAGC : 1][NP][CQ];
+    // LAG: chunks c-3, c-2, c-1 of the planes (slot 0 = the lag chunk of chunk c)
+    float4 RG[LAG ? LAGC : 1][NP][CQ];
 #pragma unroll
-    for (int j = 0; j < (VRING ? LAGC : 1); ++j)
+    for (int j = 0; j < (LAG ? LAGC : 1); ++j)
 #pragma unroll
       for (int ii = 0; ii < NP; ++ii)
 #pragma unroll
@@ -618,31 +602,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     uint32_t pw1 = 0u, pw2 = 0u;  // mask words w-1, w-2
     auto step = [&](auto full, float4(*sb)[64 * CQ], int c, int h, uint32_t bits, uint32_t lbits) {
       float4 X[NB][CQ];
-      if constexpr (PAIR && MFF_PAIR_QREAD) {
-        // as below, but the DMA of chunk c+1 goes out first and the chunk is read one quad
-        // ahead of its use (two quads of registers staged instead of four)
-        sb = (c & 1) ? pb1 : pb0;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (c + 1 < NBAR / BC) dma((c & 1) ? pb0 : pb1, c + 1, 0);
-        float4 Y[2][NB];
-#pragma unroll
-        for (int ii = 0; ii < NB; ++ii) Y[0][ii] = sb[ii][CQ * lane + (0 ^ sw)];
-#pragma unroll
-        for (int k = 0; k < CQ; ++k) {
-          if (k + 1 < CQ) {
-#pragma unroll
-            for (int ii = 0; ii < NB; ++ii) Y[(k + 1) & 1][ii] = sb[ii][CQ * lane + ((k + 1) ^ sw)];
-          }
-          float4 Z[NB][CQ];
-#pragma unroll
-          for (int ii = 0; ii < NB; ++ii) Z[ii][0] = Y[k & 1][ii];
-          __builtin_amdgcn_sched_barrier(0);
-          quad(full, BC * c + 4 * k, bits >> (BC * h + 4 * k), 0u, toq(Z, 0, 0), one4, one4, one4, one4);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        return;
-      } else if constexpr (PAIR) {
+      if constexpr (PAIR) {
         // chunk c is in buffer c & 1: this wave's half has landed (vmcnt 0), the
         // partner's half after the barrier; read it, then fetch chunk c+1 into the other
         // buffer (both waves finished reading it at chunk c-1, before this barrier)
@@ -681,26 +641,19 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         // the reads have returned before the DMA refills the buffers
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
-      if (!PAIR && c + NBUF < NBAR / BC) {
-        dma(sb, c + NBUF, 0);
-        if (LAG && !VRING && c + 1 >= LAGC) dma(sb, c + 1 - LAGC, NP);
-      }
+      if (!PAIR && c + NBUF < NBAR / BC) dma(sb, c + NBUF, 0);
 #pragma unroll
       for (int k = 0; k < CQ; ++k) {
         const Q4 x = toq(X, 0, k);
-        if constexpr (VRING) {
+        if constexpr (LAG) {
           const Q4 l1 = toq(RG[0], 0, k);
           const Q4 l0 = k > 0 ? toq(RG[0], 0, k - 1) : carry;
-          quad(full, BC * c + 4 * k, bits >> (BC * h + 4 * k), lbits >> (BC * h + 4 * k), x, l0.h, l0.l, l1.h, l1.l);
-        } else if constexpr (LAG) {
-          const Q4 l1 = toq(X, NP, k);
-          const Q4 l0 = k > 0 ? toq(X, NP, k - 1) : carry;
           quad(full, BC * c + 4 * k, bits >> (BC * h + 4 * k), lbits >> (BC * h + 4 * k), x, l0.h, l0.l, l1.h, l1.l);
         } else {
           quad(full, BC * c + 4 * k, bits >> (BC * h + 4 * k), 0u, x, one4, one4, one4, one4);
         }
       }
-      if constexpr (VRING) {
+      if constexpr (LAG) {
         carry = toq(RG[0], 0, CQ - 1);
 #pragma unroll
         for (int j = 0; j + 1 < LAGC; ++j)
@@ -712,8 +665,6 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         for (int ii = 0; ii < NP; ++ii)
 #pragma unroll
           for (int k = 0; k < CQ; ++k) RG[LAGC - 1][ii][k] = X[ii][k];
-      } else if constexpr (LAG) {
-        carry = toq(X, NP, CQ - 1);
       }
     };
     auto walk = [&](auto full) {

@@ -89,6 +89,10 @@ FIELDS = {
 }
 
 PDF_IDS = [ID[f"doc_pdf{p}"] for p in (60, 70, 80, 90, 95)]
+# the five calls built on rolling(index_column='minute_in_trade') (CM:114-118): a frame
+# whose minute_in_trade decreases inside a stock-day makes exactly these calls raise
+OLS_NAMES = [n for n in NAMES if FAMILY[n] == "OLS"]
+OLS_IDS = [ID[n] for n in OLS_NAMES]
 
 
 def resolve(names: Sequence[str] | None) -> List[int]:

@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib, catalog
-from .synth import ROW_DTYPE, ROWS_KEEP, ROWS_NULL_SHIFT, pack_mask, row_set, stack_fields
+from .synth import ROW_DTYPE, ROWS_KEEP, ROWS_NULL_SHIFT, ols_unsorted_cells, pack_mask, row_set, stack_fields
 
 ABSENT, NULL, VALUE = 0, 1, 2
 VOLUME_MAX = 2 ** 32 - 2  # MFF_VOLUME_MAX: u32 shares per bar (all-ones = absent sort key)
@@ -184,6 +184,13 @@ class DevicePanel:
     # dist.shard_bounds), so the exchange's padded shard width is known without a
     # collective; None = agree on it with one all-reduce
     stocks_total: Optional[int] = None
+    # T2 (oracle/mff_oracle.py): the cells (int64 d*S + s, on the device) of every frame
+    # whose minute_in_trade decreases inside a stock-day -- the reference's five
+    # cal_mmt_ols_* calls raise on such a frame (rolling(), CM:114-118), so their rows of
+    # the whole frame come out ABSENT; the other 53 factors are computed as usual
+    ols_drop: Optional[torch.Tensor] = None
+    # {input table index: (factor names, reason)} of those frames (ingest)
+    partial: dict = field(default_factory=dict)
 
     @property
     def D(self) -> int:
@@ -216,8 +223,15 @@ class DevicePanel:
             w[sd[keep], 7] = (w[sd[keep], 7] & np.uint32(0xFFFF)) | (fl[keep] & np.uint32(0x7FFF0000))
             w[sd, 7] |= np.uint32(0x80000000)
         mask = torch.from_numpy(words.view(np.int32)).to(device)
-        return cls(bars, mask, list(panel["codes"]), list(panel["dates"]),
-                   rows=RowSet.from_host(sd, off, rows, device))
+        dp = cls(bars, mask, list(panel["codes"]), list(panel["dates"]),
+                 rows=RowSet.from_host(sd, off, rows, device))
+        bad = ols_unsorted_cells(panel)
+        if bad.size:  # T2, one reference frame per day: every cell of those days
+            D, S = panel["present"].shape[:2]
+            days = np.unique(bad // S)
+            cells = (days[:, None] * S + np.arange(S)[None, :]).reshape(-1)
+            dp.ols_drop = torch.from_numpy(cells.astype(np.int64)).to(device)
+        return dp
 
 
 def validate_host_panel(panel) -> None:
@@ -280,126 +294,91 @@ def compute_factors(panel: DevicePanel, names: Optional[Sequence[str]] = None, c
 
     if events is not None:
         events[0].record(main)
-    if need_pdf and PDF_OVERLAP and not frame_pdf:
-        # part 1 (sorted families: doc_pdf levels + queries), then the doc_pdf rank on a
-        # side stream while part 2 (the serial families) runs on the launch stream
-        hl = _side_stream(dev, 1) if HL_STREAM else None
-
-        def launch_hl():  # the high / low serial kernel on its own stream
-            hl.wait_stream(main)
-            _lib.check(lib.mff_stage1_part(*(args[:-1] + [hl.cuda_stream]), 4), "mff_stage1_part(4)")
-
-        if hl is not None and HL_AT == "start":
-            launch_hl()
-        part1 = 17 if EXACT_SIDE and not PDF_FIRST else 1
+    if need_pdf and not frame_pdf and not SERIAL:
+        # Three streams.  Set H (OLS, MOMH: high / low only, its own rows only) from the
+        # start on a high-priority stream: its blocks fill the registers the other
+        # launches leave.  The sorted-group kernel (ORD thresholds, doc_pdf queries and
+        # level lists) on the launch stream; then, on the doc_pdf side stream, the exact
+        # list (LVL / PDF of the listed stock-days) and the doc_pdf sort, after which the
+        # wave pair (which reads the ORD thresholds) starts on the launch stream while the
+        # doc_pdf count runs beside it.  The row set's kernels (ABSENT to every grid
+        # launch: MFF_ROWS_LISTED) run on their own stream from the level-list prologue on;
+        # the sort waits for their queries and levels.  (Launch orders, priorities and
+        # stream splits measured equal or slower are in DESIGN.md §5.)
+        hl = _side_stream(dev, 1)
+        hl.wait_stream(main)
+        _lib.check(lib.mff_stage1_part(*(args[:-1] + [hl.cuda_stream]), 4), "mff_stage1_part(4)")
+        part1 = 17
         rows_st = None
-        if rs is not None and ROWS_SIDE and not PDF_FIRST:
-            # the row set on its own stream right after part 1's prologue (level-list
-            # counts, split key): the grid kernels store nothing for its stock-days
-            # (MFF_ROWS_LISTED), so its kernels run beside them; the doc_pdf sort waits for it
+        if rs is not None:
             _lib.check(lib.mff_stage1_part(*args, 64), "mff_stage1_part(64)")
             rows_st = _side_stream(dev, 2)
             rows_st.wait_stream(main)
             rows_phase(3, rows_st)
             part1 |= 128
         _lib.check(lib.mff_stage1_part(*args, part1), "mff_stage1_part(1)")
-        if hl is not None and HL_AT == "part1":
-            launch_hl()
-        if PDF_FIRST:
-            # the doc_pdf phases (whole-CU workgroups) on the launch stream before part 2:
-            # behind the wave-pair kernel they only get CUs its blocks have drained
-            rows_phase(1, main)
-            pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
-            if hl is not None and HL_AT == "pdf":
-                launch_hl()
-            _lib.check(lib.mff_stage1_part(*args, 10 if hl is not None else 2), "mff_stage1_part(2)")
-        else:
-            side = _side_stream(dev)
-            split = SORT_PRIO != PDF_PRIO and comm is None
-            sside = _side_stream(dev, 3) if split else side  # exact list + sort
-            sside.wait_stream(main)
-            if EXACT_SIDE:  # the exact list kernel ahead of the doc_pdf phases, off the launch stream
-                _lib.check(lib.mff_stage1_part(*(args[:-1] + [sside.cuda_stream]), 32), "mff_stage1_part(32)")
-            if rows_st is not None:
-                sside.wait_stream(rows_st)  # the row set's queries and levels before the sort
-            else:
-                rows_phase(1, sside)
-            sorted_ev = torch.cuda.Event() if SORT_FIRST else None
-            with torch.cuda.stream(sside):
-                pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch,
-                          after_sort=(lambda: sorted_ev.record(sside)) if sorted_ev is not None else None,
-                          count_stream=side if split else None)
-            if split:
-                side.wait_stream(sside)
-            if sorted_ev is not None:  # part 2 after the doc_pdf sort (whole-CU workgroups)
-                main.wait_event(sorted_ev)
-                if hl is not None and HL_AT == "sort":  # set H beside the pair, after the sort
-                    hl.wait_event(sorted_ev)
-                    _lib.check(lib.mff_stage1_part(*(args[:-1] + [hl.cuda_stream]), 4), "mff_stage1_part(4)")
-            _lib.check(lib.mff_stage1_part(*args, 10 if hl is not None else 2), "mff_stage1_part(2)")
-            main.wait_stream(side)
-        if hl is not None and HL_AT == "pdf" and not PDF_FIRST:
-            launch_hl()
-        if hl is not None:
-            main.wait_stream(hl)
+        side = _side_stream(dev)
+        side.wait_stream(main)
+        _lib.check(lib.mff_stage1_part(*(args[:-1] + [side.cuda_stream]), 32), "mff_stage1_part(32)")
+        if rows_st is not None:
+            side.wait_stream(rows_st)  # the row set's queries and levels before the sort
+        sorted_ev = torch.cuda.Event()
+        with torch.cuda.stream(side):
+            pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch,
+                      after_sort=lambda: sorted_ev.record(side))
+        main.wait_event(sorted_ev)  # the pair after the doc_pdf sort
+        _lib.check(lib.mff_stage1_part(*args, 10), "mff_stage1_part(2)")
+        main.wait_stream(side)
+        main.wait_stream(hl)
         if rows_st is not None:
             main.wait_stream(rows_st)
-        else:
-            rows_phase(2, main)
-        if events is not None:  # after the doc_pdf tail on the side stream
-            events[1].record(main)
-        return val, state, ids
-    _lib.check(lib.mff_stage1(*args), "mff_stage1")
-    rows_phase(1, main)
-    if frame_pdf:
-        pdf_ranks_frame(panel, pdfq, levels, rows, val, state, comm=comm)
-    elif need_pdf:
-        pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
-    rows_phase(2, main)
-    if events is not None:
+    else:
+        _lib.check(lib.mff_stage1(*args), "mff_stage1")
+        rows_phase(1, main)
+        if frame_pdf:
+            pdf_ranks_frame(panel, pdfq, levels, rows, val, state, comm=comm)
+        elif need_pdf:
+            pdf_ranks(panel, pdfq, levels, rows, val, state, comm=comm, day_batch=pdf_day_batch)
+        rows_phase(2, main)
+    drop_ols(panel, ids, val, state, comm)
+    if events is not None:  # after the doc_pdf tail on the side stream
         events[1].record(main)
     return val, state, ids
 
 
-# MFF_PDF_OVERLAP=0: doc_pdf after the whole stage-1 pass on one stream (A/B timing)
-PDF_OVERLAP = os.environ.get("MFF_PDF_OVERLAP", "1") != "0"
-# MFF_EXACT_SIDE=1 (default): the exact list kernel (LVL/PDF of the listed stock-days) runs on
-# the doc_pdf side stream, so part 2 starts right after the sorted-group kernel
-EXACT_SIDE = os.environ.get("MFF_EXACT_SIDE", "1") != "0"
-# MFF_SORT_FIRST=1 (default since round 3): part 2 waits for the doc_pdf sort (which
-# otherwise gets CUs only as the wave-pair kernel's blocks drain), so the sort runs right
-# after the sorted-group kernel and the count fills in beside the pair and set H (+1.7 %
-# pass throughput with the rank-placement sort, profiles/r03c/ab_launch_order.log)
-SORT_FIRST = os.environ.get("MFF_SORT_FIRST", "1") != "0"
-# MFF_ROWS_SIDE=1 (default): the row set's kernels (mff_stage1_rows, both phases) on their
-# own stream from the start of the pass, beside the grid kernels; 0: phase 1 before the
-# doc_pdf sort and phase 2 after the pass, on the streams of round 4 (A/B timing)
-ROWS_SIDE = os.environ.get("MFF_ROWS_SIDE", "1") != "0"
-# MFF_PDF_FIRST=1: the doc_pdf phases on the launch stream between part 1 and part 2
-PDF_FIRST = os.environ.get("MFF_PDF_FIRST", "0") != "0"
-# The high / low serial kernel (OLS, MOMH) reads only the high / low planes and writes
-# only its own rows, so it runs on a third stream from the start of the pass: its blocks
-# (180 VGPRs, 2 waves per SIMD) fill the VGPRs the sorted-group kernel (128, 4 waves)
-# leaves and the gaps of the doc_pdf phases (+2 % pass throughput, profiles/r02/).
-# MFF_HL_STREAM=0: launch order of round 1 (A/B timing).
-HL_STREAM = os.environ.get("MFF_HL_STREAM", "1") != "0"
-# MFF_HL_AT: when that stream's launch is issued: "start" (default), "part1" (after the
-# sorted-group launch), "pdf" (after the doc_pdf phases), "sort" (after the doc_pdf sort,
-# beside the pair)
-HL_AT = os.environ.get("MFF_HL_AT", "start")
+def drop_ols(panel: DevicePanel, ids: Sequence[int], val, state, comm=None) -> None:
+    """T2: the five OLS rows of every frame whose minute_in_trade decreases inside a
+    stock-day come out ABSENT for the whole frame (``panel.ols_drop``): the reference's
+    cal_mmt_ols_* call raises on that frame and the driver drops it (MF:18-25, 95).  Stock
+    shards (``comm``): a day frame spans every shard, so the days holding such a
+    stock-day on any rank are agreed by one all-reduce (max) of a [D] flag vector."""
+    rows = [r for r, i in enumerate(ids) if i in catalog.OLS_IDS]
+    if not rows:
+        return
+    cells = panel.ols_drop
+    if comm is not None:
+        bad = torch.zeros(panel.D, dtype=torch.int32, device=panel.device)
+        if cells is not None and cells.numel():
+            bad[cells // panel.S] = 1
+        comm.all_reduce_max(bad)
+        for r in rows:
+            state[r].masked_fill_(bad[:, None] != 0, ABSENT)
+            val[r].masked_fill_(bad[:, None] != 0, 0.0)
+        return
+    if cells is None or cells.numel() == 0:
+        return
+    for r in rows:
+        state[r].view(-1)[cells] = ABSENT
+        val[r].view(-1)[cells] = 0.0
 
-# Stream priorities of the side streams (torch / HIP: lower = higher priority; 0 is the
-# default): MFF_PDF_PRIO for the doc_pdf rank phases, MFF_HL_PRIO for the high / low kernel.
-# The high / low stream runs at high priority (-1) by default since round 3: its blocks
-# are then dispatched ahead of the doc_pdf and pair blocks, so its long walk no longer
-# ends last, and the doc_pdf sort / count fill the gaps around it (+1.8 % pass, c4,
-# profiles/r03e/ab_stream_priority.log; doc_pdf high instead: +0.1 %, both: +1.4 %).
-PDF_PRIO = int(os.environ.get("MFF_PDF_PRIO", "0"))
-HL_PRIO = int(os.environ.get("MFF_HL_PRIO", "-1"))
-# MFF_SORT_PRIO: when it differs from MFF_PDF_PRIO, the exact list kernel and the doc_pdf
-# sort (the short critical chain between the sorted-group kernel and the pair) run on a
-# stream of that priority and the count on the doc_pdf stream behind them
-SORT_PRIO = int(os.environ.get("MFF_SORT_PRIO", str(PDF_PRIO)))
+
+# MFF_STAGE1_SERIAL=1: every stage-1 launch on the launch stream, one after another (the
+# standalone per-kernel durations of profiles/gpu_r3_prof.sh; results are identical,
+# tests/test_gpu_schedules.py)
+SERIAL = os.environ.get("MFF_STAGE1_SERIAL", "0") != "0"
+# the high / low stream runs at high priority: its blocks are dispatched ahead of the pair's
+# and the doc_pdf count's, so its long walk does not end last (+1.8 % pass, round 3)
+HL_PRIO = -1
 
 _SIDE = {}
 
@@ -407,8 +386,7 @@ _SIDE = {}
 def _side_stream(dev, which: int = 0) -> torch.cuda.Stream:
     key = (dev.index, threading.get_ident(), which)
     if key not in _SIDE:
-        prio = HL_PRIO if which == 1 else SORT_PRIO if which == 3 else PDF_PRIO
-        _SIDE[key] = torch.cuda.Stream(dev, priority=prio)
+        _SIDE[key] = torch.cuda.Stream(dev, priority=HL_PRIO if which == 1 else 0)
     return _SIDE[key]
 
 
@@ -428,12 +406,10 @@ def stage1_frame(panel: DevicePanel, ids: Sequence[int], val, state) -> None:
 
 def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows: List[int], val, state,
               comm=None,
-              day_batch: Optional[int] = None, workspace_budget: int = 2 << 30, after_sort=None,
-              count_stream=None):
+              day_batch: Optional[int] = None, workspace_budget: int = 2 << 30, after_sort=None):
     """doc_pdf frame-wide ranks (CM:1015-1017) for all days, in day batches.  ``after_sort``:
     optional callable, invoked once the first day batch's sort is enqueued (sharded: the
-    first window's sort of this rank's days).  ``count_stream`` (one rank): the counts run
-    on that stream behind each sort instead of on the current stream."""
+    first window's sort of this rank's days)."""
     lib = _lib.load()
     D, S = panel.D, panel.S
     dev = panel.device
@@ -461,16 +437,10 @@ def pdf_ranks(panel: DevicePanel, pdfq: torch.Tensor, levels: torch.Tensor, rows
                                     _lib.ptr(ws), st), "mff_pdf_sort")
         if after_sort is not None and d0 == 0:
             after_sort()
-        cst = st
-        if count_stream is not None:
-            count_stream.wait_stream(torch.cuda.current_stream(dev))
-            q_sorted.record_stream(count_stream)
-            ws.record_stream(count_stream)
-            cst = count_stream.cuda_stream
         # single rank: count + finalize fused, no exchange
         _lib.check(lib.mff_pdf_rank_local(_lib.ptr(levels), _lib.ptr(pdfq), S, D, d0, nd,
                                           _lib.ptr(q_sorted), M,
-                                          _lib.int_array(rows), _lib.ptr(val), _lib.ptr(state), cst),
+                                          _lib.int_array(rows), _lib.ptr(val), _lib.ptr(state), st),
                    "mff_pdf_rank_local")
 
 
@@ -855,15 +825,6 @@ def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None,
                                      _lib.ptr(ov), _lib.ptr(os_), st), "mff_xs_zscore")
     elif kind == "rank" and comm is None:
         _xs_rank_local(lib, val, state, ov, os_, st)
-    elif kind == "rank" and RANK_GATHER:  # round-4 form (A/B): every rank ranks every column
-        S_all = shard_width(comm, S, stocks_total, dev)
-        v_all = comm.all_gather(_pad_last(val, S_all, 0.0))
-        s_all = comm.all_gather(_pad_last(state, S_all, ABSENT))
-        ws = torch.empty(lib.mff_xs_rank_workspace_bytes(rows, D, S_all, R), dtype=torch.uint8,
-                         device=dev)
-        _lib.check(lib.mff_xs_rank(_lib.ptr(val), _lib.ptr(state), rows, D, S, _lib.ptr(v_all),
-                                   _lib.ptr(s_all), R, S_all, _lib.ptr(ov), _lib.ptr(os_),
-                                   _lib.ptr(ws), st), "mff_xs_rank")
     elif kind == "rank":
         S_all = shard_width(comm, S, stocks_total, dev)
         ov, os_ = xs_rank_sharded(comm, val, state, S_all,
@@ -871,11 +832,6 @@ def cross_section(val: torch.Tensor, state: torch.Tensor, kind: str, comm=None,
     else:
         raise ValueError(kind)
     return ov, os_
-
-
-# MFF_RANK_GATHER=1: the sharded stage-3 rank all-gathers every column to every rank (round
-# 4); default: the day-owner transpose of xs_rank_sharded
-RANK_GATHER = os.environ.get("MFF_RANK_GATHER", "0") != "0"
 
 
 def _xs_rank_local(lib, val, state, ov, os_, st) -> None:

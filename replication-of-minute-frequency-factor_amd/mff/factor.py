@@ -503,8 +503,10 @@ def _batch_key(folder_path, files, device):
 
 
 def _batch_results(files, folder_path, device):
-    """(val [58][D][S], state, codes, dates, {file name: error}) of one batch of day files
-    (all 58 factors, per-day semantics), from the cache or computed."""
+    """((val [58][D][S], state, codes, dates), {file name: error}, {file name: (factor names,
+    error)}) of one batch of day files (all 58 factors, per-day semantics), from the cache
+    or computed.  The third dict: files on which only those factors' calls fail (T2: the
+    five OLS calls on a decreasing minute_in_trade, CM:114-118; their rows are ABSENT)."""
     global _RESULTS, _RESULTS_BYTES
     from collections import OrderedDict
 
@@ -518,14 +520,15 @@ def _batch_results(files, folder_path, device):
     # column from the files' dictionary pages) and encode them while earlier files move
     # to the device; a file that cannot be read is reported like any other bad file
     paths = [os.path.join(folder_path, f) for f in files]
-    errors, res = {}, None
+    errors, res, partial = {}, None, {}
     try:  # one reference call per file (per-day semantics); a bad file drops its day only
-        v, s, _, codes, dates, dropped = compute_dense(paths, None, device, per_day=True, skip_bad=True)
+        v, s, _, codes, dates, dropped, part = compute_dense(paths, None, device, per_day=True, skip_bad=True)
         res = (v, s, codes, dates)
+        partial = {files[k]: x for k, x in sorted(part.items())}
     except NoTables as e:
         dropped = e.dropped
     errors.update({files[k]: msg for k, msg in dropped.items()})
-    out = (res, dict(sorted(errors.items())))
+    out = (res, dict(sorted(errors.items())), partial)
     nbytes = 0 if res is None else res[0].nbytes + res[1].nbytes
     if key is not None and not errors and res is not None and _RESULTS_BYTES + nbytes <= _cache_cap():
         if _RESULTS is None:
@@ -539,7 +542,11 @@ def _gpu_batches(files, folder_path, names, batch_days, device, strict=False):
     """{name: [long frames of each batch]} over the day files, batch_days at a time."""
     out = {nm: [] for nm in names}
     for b0 in range(0, len(files), batch_days):
-        res, errors = _batch_results(files[b0:b0 + batch_days], folder_path, device)
+        res, errors, partial = _batch_results(files[b0:b0 + batch_days], folder_path, device)
+        errors = dict(errors)  # (the cached entry stays as it is)
+        for f, (fns, msg) in partial.items():  # only those calls fail on the file (MF:20-25)
+            errors.update({f: msg for nm in names if nm in fns})
+        errors = dict(sorted(errors.items()))
         for f, msg in errors.items():
             if strict:
                 raise ValueError(f"{f}: {msg}")

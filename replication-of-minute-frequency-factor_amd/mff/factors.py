@@ -37,8 +37,11 @@ FRAME_RANK = ("doc_pdf60", "doc_pdf70", "doc_pdf80", "doc_pdf90", "doc_pdf95")
 def compute_dense(df, names: Sequence[str] | None = None, device=None, per_day: bool | None = None,
                   skip_bad: bool = False):
     """Long frame(s) -> the dense stage-1 result on the host: (val f64 [nf][D][S], state u8
-    [nf][D][S], names, codes, dates, dropped {table index: reason}).  Semantics as
-    :func:`compute_long`."""
+    [nf][D][S], names, codes, dates, dropped {table index: reason}, partial {table index:
+    (factor names, reason)}).  Semantics as :func:`compute_long`; ``partial`` lists the
+    tables on which only some reference calls fail (T2: a decreasing minute_in_trade makes
+    the five cal_mmt_ols_* calls raise, CM:114-118) -- those factors' rows of the table
+    are ABSENT, the others computed."""
     import torch
 
     from . import engine, ingest
@@ -54,7 +57,7 @@ def compute_dense(df, names: Sequence[str] | None = None, device=None, per_day: 
             engine.stage1_frame(dp, ids, val, state)
         torch.cuda.synchronize(dp.device)
     with _timing.phase("D2H"):
-        return val.cpu().numpy(), state.cpu().numpy(), names, dp.codes, dp.dates, dp.dropped
+        return val.cpu().numpy(), state.cpu().numpy(), names, dp.codes, dp.dates, dp.dropped, dp.partial
 
 
 def to_long_frames(val, state, names, codes, dates) -> Dict:
@@ -82,10 +85,20 @@ def compute_long(df, names: Sequence[str] | None = None, device=None, per_day: b
     A table that breaks the input contract (include/mff.h) raises ValueError, unless
     ``skip_bad``: then its days are dropped (no rows), as the reference driver drops a
     day file whose call raised (MinuteFrequentFactorCICC.py:18-25, 95), and ``errors``
-    (a dict, if given) receives {table index: reason}."""
-    v, s, names, codes, dates, dropped = compute_dense(df, names, device, per_day, skip_bad)
+    (a dict, if given) receives {table index: reason}.  A table on which only some of the
+    requested calls fail (a minute_in_trade decreasing inside a stock-day: the five OLS
+    calls, CM:114-118) raises likewise when one of them is requested, unless
+    ``skip_bad``: then those factors get no rows for the table, every other factor is
+    computed, and ``errors`` receives the reason naming the factors."""
+    v, s, names, codes, dates, dropped, partial = compute_dense(df, names, device, per_day, skip_bad)
+    failed = {k: (tuple(n for n in fns if n in names), msg) for k, (fns, msg) in partial.items()}
+    failed = {k: x for k, x in failed.items() if x[0]}
+    if failed and not skip_bad:
+        raise ValueError("; ".join(f"{', '.join('cal_' + n for n in fns)}: {msg}" for fns, msg in failed.values()))
     if errors is not None:
         errors.update(dropped)
+        for k, (fns, msg) in failed.items():
+            errors.setdefault(k, f"{', '.join('cal_' + n for n in fns)}: {msg}")
     return to_long_frames(v, s, names, codes, dates)
 
 

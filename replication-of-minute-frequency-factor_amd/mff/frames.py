@@ -40,19 +40,26 @@ def time_to_minute(time: np.ndarray) -> np.ndarray:
     return np.where(ok, m, -1)
 
 
+OLS_UNSORTED = ("minute_in_trade decreases inside a stock-day (a row inside the 11:30-13:00 break "
+                "before an afternoon row): rolling(index_column='minute_in_trade') (CM:114-118) "
+                "rejects the frame")
+
+
 def listed_rows(cols, S: int, D: int, counted=None):
     """The row set of one table (include/mff.h): the stock-days with a null field, a row off
     the 240-bar grid (a time that is not a 09:30-11:29 / 13:00-14:59 minute start) or two
     rows at one time, and all their rows in (time, frame) order (C4: rows at one time keep
     the push's order).  Returns (cells int64 [K] = d*S + s ascending, off int64 [K+1], rows
     ROW_DTYPE [R], internal duplicate rows, irregular bool [K] = the stock-day has a row off
-    the grid or a duplicate time, not only nulls).  ``cols``: (stock, day, time, 4 price
-    arrays, volume, null bits uint8) per row (ingest's encoding).  ``counted``: the kernel's (off-grid, duplicate)
-    counts for the push; more duplicates there than inside the push = rows of another
-    table at the same (code, date, time).  Raises ValueError on an input-contract error of
-    a listed stock-day (include/mff.h: a null or out-of-day time, more than MFF_ROWS_MAX
-    rows, minute_in_trade decreasing -- a row inside the lunch break before an afternoon
-    row, which the reference's rolling() rejects as unsorted -- or a bad price / volume)."""
+    the grid or a duplicate time, not only nulls, unsorted bool [K] = its minute_in_trade
+    decreases).  ``cols``: (stock, day, time, 4 price arrays, volume, null bits uint8) per
+    row (ingest's encoding).  ``counted``: the kernel's (off-grid, duplicate) counts for the
+    push; more duplicates there than inside the push = rows of another table at the same
+    (code, date, time).  Raises ValueError on an input-contract error of a listed stock-day
+    (include/mff.h: a null or out-of-day time, more than MFF_ROWS_MAX rows, or a bad price /
+    volume).  A stock-day whose minute_in_trade decreases (a row inside the lunch break
+    before an afternoon row) is no contract error: the reference's rolling() rejects that
+    frame, so only its five OLS calls fail (T2; the caller drops them for the table)."""
     from .synth import ROW_DTYPE
 
     stock, day, time, px, vol, nb = cols
@@ -79,7 +86,7 @@ def listed_rows(cols, S: int, D: int, counted=None):
     listed = np.unique(np.concatenate([cell[offg], dupc, cell[ok & (nb != 0)]]))
     irregular = np.isin(listed, np.concatenate([cell[offg], dupc]))
     if listed.size == 0:
-        return listed, np.zeros(1, np.int64), np.zeros(0, ROW_DTYPE), ndup, irregular
+        return listed, np.zeros(1, np.int64), np.zeros(0, ROW_DTYPE), ndup, irregular, np.zeros(0, bool)
     sel = np.flatnonzero(ok & np.isin(cell, listed))
     t = time[sel]
     if ((t < 0) | (t >= TIME_END)).any():
@@ -91,9 +98,9 @@ def listed_rows(cols, S: int, D: int, counted=None):
         raise ValueError(f"a stock-day with nulls or rows off the grid holds more than {ROWS_MAX} rows")
     te = (time[idx] // 10000000) * 60 + (time[idx] % 10000000) // 100000
     mi = np.where(te < 720, te - 570, te - 660)
-    if ((np.diff(mi) < 0) & (c[1:] == c[:-1])).any():
-        raise ValueError("minute_in_trade decreases inside a stock-day (a row inside the 11:30-13:00 "
-                         "break before an afternoon row): the reference's rolling() rejects it")
+    down = np.flatnonzero((np.diff(mi) < 0) & (c[1:] == c[:-1]))
+    unsorted = np.zeros(listed.size, bool)
+    unsorted[np.searchsorted(listed, c[down])] = True
     rows = np.zeros(idx.size, ROW_DTYPE)
     rows["time"] = time[idx]
     nbi = nb[idx]
@@ -110,7 +117,7 @@ def listed_rows(cols, S: int, D: int, counted=None):
     rows["volume"] = np.where(vn, v, 0.0).astype(np.uint32)
     rows["nulls"] = nbi
     off = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)
-    return listed, off, rows, ndup, irregular
+    return listed, off, rows, ndup, irregular, unsorted
 
 
 
@@ -170,7 +177,8 @@ def to_dense(df, codes: Sequence[str] | None = None) -> Dict:
     ``extra`` = (sd, off, rows) (see :func:`mff.synth.row_set`) for the stock-days with a
     row off the 240-bar grid or two rows at one time -- every row of those stock-days, in
     (time, frame) order, none of them on the grid (the host restatement of the ingest's
-    row set, :func:`listed_rows`)."""
+    row set, :func:`listed_rows`); ``ols_unsorted`` (int64 cells d*S + s) when some of
+    them have a decreasing minute_in_trade (T2)."""
     cols, nulls = _columns(df)
     for k in ("code", "date", "time") + FIELDS:
         if k not in cols:
@@ -194,7 +202,7 @@ def to_dense(df, codes: Sequence[str] | None = None) -> Dict:
             nb |= nulls[k].astype(np.uint8) << i
     px = [np.asarray(cols[k], dtype=np.float64) for k in FIELDS[:4]]
     vol = np.asarray(cols["volume"], dtype=np.float64)
-    cells, off, rows, _, irr = listed_rows((s, d, time, px, vol, nb), S, D)
+    cells, off, rows, _, irr, uns = listed_rows((s, d, time, px, vol, nb), S, D)
     cell = d * S + s
     grid = ~np.isin(cell, cells[irr])
     for i in range(4):  # the engine's contract on the grid rows (nulls aside)
@@ -225,6 +233,8 @@ def to_dense(df, codes: Sequence[str] | None = None) -> Dict:
         parts = [rows[off[i]:off[i + 1]] for i in keep]
         panel["extra"] = (cells[keep], np.concatenate([[0], np.cumsum([p.size for p in parts])]),
                           np.concatenate(parts))
+    if uns.any():  # T2: the frame's five OLS calls raise (mff.synth.ols_unsorted_days)
+        panel["ols_unsorted"] = cells[uns]
     panel["codes"] = ucodes
     panel["dates"] = udates
     return panel

@@ -25,7 +25,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 import torch
 
-from . import _lib, _timing
+from . import _lib, _timing, catalog
 
 FIELDS = ("open", "high", "low", "close", "volume")
 ERRORS = ("stock/day index out of range", "bars off the 240-minute grid",
@@ -273,7 +273,7 @@ def encode(t, codes: Sequence[str], day_numbers: Sequence[int]):
     return cat(0), cat(1), cat(2), px, cat(4), bs[0][5], nb
 
 
-from .frames import ROWS_MAX, listed_rows  # noqa: E402  (host-only row-set restatement)
+from .frames import OLS_UNSORTED, ROWS_MAX, listed_rows  # noqa: E402  (host-only row-set restatement)
 
 
 def _cat_batches(batches):
@@ -450,25 +450,30 @@ class PanelIngest:
             if bad:
                 dropped[k] = "; ".join(bad)
         listed = {}  # push -> (cells, off, rows)
+        partial = {}  # push -> (factor names, reason): T2, only its OLS calls fail
         for k in range(npush):
             if k in dropped or not (self._nulls[k] or err[k, 1] or err[k, 2]):
                 continue
             try:
-                cells, off, rows, _, irregular = listed_rows(_cat_batches(self._batches(k)), self.S, self.D,
-                                                             counted=err[k, 1:3])
+                cells, off, rows, _, irregular, unsorted = listed_rows(_cat_batches(self._batches(k)), self.S,
+                                                                       self.D, counted=err[k, 1:3])
             except ValueError as e:
                 dropped[k] = str(e)
                 continue
+            if unsorted.any():
+                partial[k] = (tuple(catalog.OLS_NAMES), OLS_UNSORTED)
             # a stock-day listed only for nulls (its rows on the grid at distinct minutes: the
             # kernel wrote them all, nulls filled) keeps its grid bars (MFF_ROWS_KEEP)
             for i in np.flatnonzero(~np.asarray(irregular, dtype=bool)):
                 rows["reserved"][off[i]] = keep_flags(rows["nulls"][off[i]:off[i + 1]])
             if cells.size:
                 listed[k] = (cells, off, rows)
-        # a listed stock-day's rows must come from one table
+        # a listed stock-day's rows must come from one table (the later table of a split is
+        # dropped; the tables already dropped for a contract error are not compared)
+        bad_before = set(dropped)
         for k, (cells, _, _) in list(listed.items()):
             for j in range(npush):
-                if j != k and j not in dropped and np.isin(cells, self.table_cells[j]).any():
+                if j != k and j not in bad_before and np.isin(cells, self.table_cells[j]).any():
                     dropped[max(j, k)] = ("rows of a stock-day with nulls or rows off the grid are split "
                                           f"across tables {min(j, k)} and {max(j, k)}")
         for k in list(listed):
@@ -484,6 +489,19 @@ class PanelIngest:
         flat = self.mask.view(-1, 8)
         if dcells.size:
             flat[torch.as_tensor(dcells, device=self.dev)] = 0
+            # a cell a dropped table wrote is ABSENT for every family: no listing of a kept
+            # table may keep it (its grid bars are gone, so a kept listing would mix the
+            # grid's ABSENT with row-computed families)
+            for k, (cells, off, rows) in list(listed.items()):
+                hit = np.isin(cells, dcells)
+                if hit.any():
+                    keep = np.flatnonzero(~hit)
+                    parts = [rows[off[i]:off[i + 1]] for i in keep]
+                    noff = np.concatenate([[0], np.cumsum([p.size for p in parts])]).astype(np.int64)
+                    nrows = np.concatenate(parts) if parts else np.zeros(0, ROW_DTYPE)
+                    listed[k] = (cells[keep], noff, nrows)
+                    if not keep.size:
+                        del listed[k]
         rs = None
         if listed:
             parts = [listed[k] for k in sorted(listed)]
@@ -503,6 +521,10 @@ class PanelIngest:
         dates = [_EPOCH + _dt.timedelta(days=x) for x in self.day_numbers]
         dp = DevicePanel(self.bars, self.mask, self.codes, dates, rows=rs)
         dp.dropped = dropped
+        dp.partial = {k: v for k, v in partial.items() if k not in dropped}
+        if dp.partial:  # the whole frame of each such table (its cells)
+            cells = np.unique(np.concatenate([self.table_cells[k] for k in dp.partial]))
+            dp.ols_drop = torch.as_tensor(cells, dtype=torch.int64, device=self.dev)
         return dp
 
 
@@ -586,6 +608,7 @@ def to_device_panel(tables, device, codes: Optional[Sequence[str]] = None, skip_
     for j, msg in dp.dropped.items():
         dropped[keep[j]] = msg
     dp.dropped = dict(sorted(dropped.items()))
+    dp.partial = {keep[j]: v for j, v in sorted(dp.partial.items())}
     return dp
 
 

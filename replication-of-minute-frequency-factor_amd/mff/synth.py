@@ -189,6 +189,50 @@ def grid_rows(panel: Dict, d: int, s: int) -> np.ndarray:
     return r
 
 
+ROWS_MAX = 255  # include/mff.h MFF_ROWS_MAX
+TIME_END = 240000000
+VOLUME_MAX = 2 ** 32 - 2  # include/mff.h MFF_VOLUME_MAX
+
+
+def minute_in_trade(time: np.ndarray) -> np.ndarray:
+    """CM:98-106 on HHMMSSmmm times (Int64 truncation of the minute, then the session
+    offset)."""
+    t = np.asarray(time, dtype=np.int64)
+    te = (t // 10000000) * 60 + (t % 10000000) // 100000
+    return np.where(te < 720, te - 570, te - 660)
+
+
+def check_rows(r: np.ndarray) -> None:
+    """The input contract of one listed stock-day's rows (include/mff.h; the checks of
+    mff.frames.listed_rows): at most MFF_ROWS_MAX rows, times in [0, 24:00) in ascending
+    order, non-null prices finite and > 0, non-null volumes integral u32 shares.  (A
+    decreasing minute_in_trade is no contract error: T2, :func:`ols_unsorted_cells`.)"""
+    if r.size > ROWS_MAX:
+        raise ValueError(f"a listed stock-day holds {r.size} rows, more than {ROWS_MAX}")
+    t = r["time"].astype(np.int64)
+    if ((t < 0) | (t >= TIME_END)).any() or (np.diff(t) < 0).any():
+        raise ValueError("a listed stock-day's rows must be in time order within [0, 240000000)")
+    nb = r["nulls"].astype(np.uint32)
+    for i, k in enumerate(FIELDS[:4]):
+        x = r[k][(nb >> i) & 1 == 0].astype(np.float64)
+        if not (np.isfinite(x) & (x > 0)).all():
+            raise ValueError("prices must be finite and > 0")
+    if (r["volume"][(nb >> 4) & 1 == 0] > VOLUME_MAX).any():
+        raise ValueError(f"volume must be within [0, {VOLUME_MAX}] shares")
+
+
+def ols_unsorted_cells(panel: Dict) -> np.ndarray:
+    """The stock-days (d*S + s) of ``panel["extra"]`` whose minute_in_trade decreases (T2:
+    the reference's rolling() rejects their frame, CM:114-118)."""
+    ex = panel.get("extra")
+    if ex is None:
+        return np.zeros(0, np.int64)
+    esd, eoff, erows = ex
+    out = [int(x) for i, x in enumerate(np.asarray(esd, dtype=np.int64).tolist())
+           if (np.diff(minute_in_trade(erows["time"][eoff[i]:eoff[i + 1]])) < 0).any()]
+    return np.asarray(out, dtype=np.int64)
+
+
 def row_set(panel: Dict, keep: bool = True):
     """The row set of a host panel (include/mff.h): the stock-days that hold a polars null
     (``panel["null"]``: optional uint8 [D][S][240], bit i = FIELDS[i] null on a present bar)
@@ -214,9 +258,12 @@ def row_set(panel: Dict, keep: bool = True):
     if ex is not None:
         esd, eoff, erows = ex
         for i, x in enumerate(np.asarray(esd, dtype=np.int64).tolist()):
+            if not 0 <= x < D * S:
+                raise ValueError(f"stock-day {x} of panel['extra'] is outside the {D} x {S} panel")
             if pres.reshape(-1, pres.shape[-1])[x].any():
                 raise ValueError(f"stock-day {x} is both on the grid and in panel['extra']")
             parts[x] = np.asarray(erows[eoff[i]:eoff[i + 1]], dtype=ROW_DTYPE)
+            check_rows(parts[x])
     sd = np.array(sorted(parts), dtype=np.int64)
     n = np.array([parts[x].size for x in sd.tolist()], dtype=np.int64)
     off = np.concatenate([[0], np.cumsum(n)]).astype(np.int64)

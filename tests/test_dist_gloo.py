@@ -269,7 +269,7 @@ def test_gloo_sharded_doc_pdf_exchange_world2(day_batch):
     val = np.concatenate([res[0][0], res[1][0]], axis=2)
     state = np.concatenate([res[0][1], res[1][1]], axis=2)
     # the exchange is accounted per collective (bench.py's N > 1 line), and the launch
-    # stream's SORT_FIRST hook fired once, after the first window's sort
+    # stream's after-sort hook (the pair waits for it) fired once, after the first window's sort
     windows = 1 if day_batch is None else 3
     for r in (0, 1):
         st, nsort = res[r][2], res[r][3]

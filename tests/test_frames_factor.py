@@ -48,8 +48,12 @@ def test_time_grid_roundtrip_and_validation():
     # input-contract errors of a listed stock-day
     with pytest.raises(ValueError, match="time must be"):
         frames.to_dense(pd.concat([df, df.assign(time=None)]))
-    with pytest.raises(ValueError, match="minute_in_trade decreases"):
-        frames.to_dense(pd.concat([df.assign(time=114500000), df.assign(time=130000000)]))
+    # a decreasing minute_in_trade is no contract error (T2): the stock-day is listed and
+    # marked, only the frame's five OLS calls fail
+    p3 = frames.to_dense(pd.concat([df.assign(time=114500000), df.assign(time=130000000)]))
+    assert p3["extra"][0].tolist() == [0] and p3["ols_unsorted"].tolist() == [0]
+    assert synth.ols_unsorted_cells(p3).tolist() == [0]
+    assert "ols_unsorted" not in frames.to_dense(pd.concat([df.assign(time=112900000), df.assign(time=130000000)]))
     with pytest.raises(ValueError, match="more than 255 rows"):
         frames.to_dense(pd.concat([df.assign(time=93000000 + 1000 * k) for k in range(256)]))
 

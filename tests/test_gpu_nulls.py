@@ -60,15 +60,14 @@ def test_golden_null_fixture(dev):
     assert not bad, "\n".join(bad)
 
 
-@pytest.mark.parametrize("overlap,rows_side", [(True, True), (True, False), (False, True)])
-def test_null_panel_all_factors(dev, overlap, rows_side, monkeypatch):
+@pytest.mark.parametrize("serial", [False, True])
+def test_null_panel_all_factors(dev, serial, monkeypatch):
     """Every factor on a ragged panel with nulls: the overlapped pass with the row set's
     kernels on their own stream beside the grid kernels (MFF_ROWS_LISTED keeps the grid
-    kernels off its rows), the same with the row-set phases before the doc_pdf sort and
-    after the pass, and the one-stream serial pass."""
+    kernels off its rows), and the one-stream serial pass (the row-set phases before the
+    doc_pdf sort and after the pass)."""
     from mff import engine
-    monkeypatch.setattr(engine, "PDF_OVERLAP", overlap)
-    monkeypatch.setattr(engine, "ROWS_SIDE", rows_side)
+    monkeypatch.setattr(engine, "SERIAL", serial)
     panel = _null_panel(60, 3, config=51)
     dp = engine.DevicePanel.from_host(panel, dev)
     assert dp.rows.K >= 10

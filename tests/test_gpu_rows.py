@@ -133,9 +133,9 @@ def test_rows_from_device_panel(dev):
 
 def test_row_set_contract_errors(dev):
     """Input-contract errors of a listed stock-day raise (or drop the table with skip_bad):
-    a null time, more than MFF_ROWS_MAX rows, minute_in_trade decreasing (a lunch-break row
-    before an afternoon row), rows of one listed stock-day in two tables, a duplicate time
-    across two tables."""
+    a null time, more than MFF_ROWS_MAX rows, rows of one listed stock-day in two tables, a
+    duplicate time across two tables.  (A decreasing minute_in_trade is not one: T2,
+    test_unsorted_minute_fails_only_the_ols_calls.)"""
     from mff import ingest
     row = {"code": ["A"], "date": [dt.date(2024, 1, 2)], "time": [93000000],
            "open": [1.0], "high": [1.0], "low": [1.0], "close": [1.0], "volume": [100.0]}
@@ -143,7 +143,6 @@ def test_row_set_contract_errors(dev):
     cases = [
         (pd.concat([df.assign(time=92500000), df.assign(time=None)]), "time must be"),
         (pd.concat([df.assign(time=93000000 + 1000 * k) for k in range(256)]), "more than 255 rows"),
-        (pd.concat([df.assign(time=114500000), df.assign(time=130000000)]), "minute_in_trade decreases"),
     ]
     for bad, msg in cases:
         with pytest.raises(ValueError, match=msg):
@@ -158,3 +157,56 @@ def test_row_set_contract_errors(dev):
     # an off-grid row is no error: the stock-day is listed
     dp = ingest.to_device_panel(pd.concat([df, df.assign(time=150000000)]), dev)
     assert dp.rows.K == 1 and dp.rows.host()[2]["time"].tolist() == [93000000, 150000000]
+
+
+def test_unsorted_minute_fails_only_the_ols_calls(dev, capsys):
+    """T2 (verdict r5 #4): a stock-day with an 11:45 row before its 13:00 row has a
+    decreasing minute_in_trade, which rolling(index_column='minute_in_trade') rejects
+    (CM:114-118): on that day file the reference's five cal_mmt_ols_* calls raise and the
+    driver drops the file for those factors only (MF:18-25, 95).  The other 53 factors of
+    the day -- that stock-day included, from its rows -- equal the oracle; the five OLS rows
+    of the whole day are absent and the error is reported; the other days are untouched."""
+    import MinuteFrequentFactorCalculateMethodsCICC as CM
+    import mff_oracle as O
+    from mff import catalog, engine, frames, ingest, synth
+    from test_frames_factor import long_frame
+    panel = synth.make_panel(24, 3, config=65)
+    full = long_frame(panel)
+    d1 = panel["dates"][1]
+    code = panel["codes"][5]
+    extra = full[(full["code"] == code) & (full["date"] == d1) & (full["time"] == 130000000)].copy()
+    assert len(extra) == 1
+    extra["time"] = 114500000  # inside the 11:30-13:00 break: minute_in_trade 135 > 120
+    df = pd.concat([full, extra], ignore_index=True).sort_values(["date", "code", "time"], kind="stable")
+    tabs = [pa.Table.from_pandas(g.reset_index(drop=True), preserve_index=False)
+            for _, g in df.groupby("date", sort=True)]
+    host = frames.to_dense(pa.concat_tables(tabs), codes=panel["codes"])
+    assert synth.ols_unsorted_cells(host).tolist() == [1 * 24 + 5]
+    ov, os_ = O.oracle_stage1(host)
+    ols = catalog.OLS_IDS
+    assert (os_[ols][:, 1] == 0).all() and (os_[ols][:, 0] != 0).any() and (os_[ols][:, 2] != 0).any()
+    assert os_[catalog.ID["mmt_pm"], 1, 5] != 0  # the stock-day's other factors exist
+    # (a) the host panel path: one frame per day
+    dp = engine.DevicePanel.from_host(host, dev)
+    val, state, ids = engine.compute_factors(dp)
+    torch.cuda.synchronize()
+    bad = []
+    for i, nm in enumerate(catalog.NAMES):
+        kw = {"rtol": 0, "atol": 0} if nm.startswith("doc_pdf") else {}
+        bad += compare(val[i].cpu().numpy(), state[i].cpu().numpy(), ov[i], os_[i], nm, **kw)
+    assert not bad, "\n".join(bad)
+    # (b) the ingest of day tables: the table of day 1 is reported for the OLS calls only
+    dp = ingest.to_device_panel(tabs, dev, codes=panel["codes"])
+    assert dp.dropped == {} and list(dp.partial) == [1]
+    assert dp.partial[1][0] == tuple(catalog.OLS_NAMES) and "minute_in_trade" in dp.partial[1][1]
+    errors = {}
+    res = CM.compute_long(tabs, skip_bad=True, errors=errors)
+    assert list(errors) == [1] and "cal_mmt_ols_qrs" in errors[1]
+    bad = _check_long(res, catalog.NAMES, host, lambda i, nm: (ov[i], os_[i]))
+    assert not bad, "\n".join(bad)
+    # (c) the drop-in calls on the day-1 frame: OLS raises like the reference, others work
+    day1 = tabs[1].to_pandas()
+    with pytest.raises(ValueError, match="minute_in_trade"):
+        CM.cal_mmt_ols_qrs(day1)
+    got = CM.cal_mmt_pm(day1)
+    assert len(got) == int((os_[catalog.ID["mmt_pm"], 1] != 0).sum())

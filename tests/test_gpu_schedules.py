@@ -1,10 +1,10 @@
-"""The stage-1 pass under every launch order `engine.compute_factors` offers.
-
-The knobs (engine.py: MFF_EXACT_SIDE, MFF_PDF_OVERLAP, MFF_PDF_FIRST, MFF_SORT_FIRST,
-MFF_HL_STREAM, MFF_HL_AT) only move the same launches between streams, so every
-schedule must reproduce the default pass bit for bit (values, NaN pattern, states) on
-the ragged golden panel, whose exact-list stock-days (wide days, doc_pdf ties) make the
-side-stream ordering of the exact kernel matter.
+"""The stage-1 pass in its two schedules: the overlapped three-stream pass
+(`engine.compute_factors`, the default) and every launch on one stream
+(MFF_STAGE1_SERIAL=1, the standalone-kernel profile of profiles/gpu_r3_prof.sh).  They
+only move the same launches between streams, so both must give the same pass bit for bit
+(values, NaN pattern, states) on the ragged golden panel, whose exact-list stock-days
+(wide days, doc_pdf ties) make the side-stream ordering of the exact kernel matter, and on
+a panel with a row set (nulls and off-grid rows: the row set's own stream).
 """
 import numpy as np
 import pytest
@@ -29,25 +29,19 @@ def _pass(dev, panel):
     return val.cpu().numpy(), state.cpu().numpy()
 
 
-SCHEDULES = [
-    {"EXACT_SIDE": False},
-    {"PDF_OVERLAP": False},
-    {"PDF_FIRST": True},
-    {"SORT_FIRST": False},
-    {"HL_STREAM": False},
-    {"HL_AT": "part1"},
-    {"PDF_FIRST": True, "HL_AT": "pdf"},
-]
-
-
-@pytest.mark.parametrize("knobs", SCHEDULES, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
-def test_schedule_matches_default(dev, monkeypatch, knobs):
+def _panels():
     from golden.make_golden import load
+    from mff import synth
+    yield load("panel_ragged.npz")[0]
+    yield synth.add_nulls(synth.make_panel(40, 3, config=66, ragged=True), seed=3, rate=0.01)
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_serial_schedule_matches_overlapped(dev, monkeypatch, which):
     from mff import engine
-    panel, _ = load("panel_ragged.npz")
+    panel = list(_panels())[which]
     v0, s0 = _pass(dev, panel)
-    for name, value in knobs.items():
-        monkeypatch.setattr(engine, name, value)
+    monkeypatch.setattr(engine, "SERIAL", True)
     v1, s1 = _pass(dev, panel)
     assert np.array_equal(s0, s1)
     assert np.array_equal(np.isnan(v0), np.isnan(v1))
