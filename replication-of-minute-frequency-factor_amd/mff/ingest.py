@@ -489,19 +489,12 @@ class PanelIngest:
         flat = self.mask.view(-1, 8)
         if dcells.size:
             flat[torch.as_tensor(dcells, device=self.dev)] = 0
-            # a cell a dropped table wrote is ABSENT for every family: no listing of a kept
-            # table may keep it (its grid bars are gone, so a kept listing would mix the
-            # grid's ABSENT with row-computed families)
-            for k, (cells, off, rows) in list(listed.items()):
-                hit = np.isin(cells, dcells)
-                if hit.any():
-                    keep = np.flatnonzero(~hit)
-                    parts = [rows[off[i]:off[i + 1]] for i in keep]
-                    noff = np.concatenate([[0], np.cumsum([p.size for p in parts])]).astype(np.int64)
-                    nrows = np.concatenate(parts) if parts else np.zeros(0, ROW_DTYPE)
-                    listed[k] = (cells[keep], noff, nrows)
-                    if not keep.size:
-                        del listed[k]
+            # the grid bars of those cells are gone (a kept table's bars of a shared cell
+            # too): a kept table's listing of such a cell computes every family from its own
+            # rows (MFF_ROWS_KEEP cleared), never the grid's ABSENT beside row-computed ones
+            for k, (cells, off, rows) in listed.items():
+                hit = np.flatnonzero(np.isin(cells, dcells) & (off[1:] > off[:-1]))
+                rows["reserved"][off[hit]] = 0
         rs = None
         if listed:
             parts = [listed[k] for k in sorted(listed)]

@@ -154,6 +154,27 @@ def test_row_set_contract_errors(dev):
     # skip_bad drops the later table only
     dp = ingest.to_device_panel([df.assign(time=92500000), df.assign(time=93100000)], dev, skip_bad=True)
     assert list(dp.dropped) == [1] and dp.rows.K == 1
+    # a stock-day listed only for a null (kept: its grid bars stay) whose cell a dropped
+    # table shares: computed from the kept table's own rows alone, as if the dropped table
+    # were absent (no kept listing over a cell whose grid bars were cleared)
+    import MinuteFrequentFactorCalculateMethodsCICC as CM
+    t0 = pa.Table.from_pandas(pd.concat([df.assign(time=93000000 + 100000 * k, volume=100.0 + k)
+                                         for k in range(6)]), preserve_index=False)
+    t0 = t0.set_column(t0.column_names.index("volume"), "volume",
+                       pa.array([None, 101.0, 102.0, 103.0, 104.0, 105.0], pa.float64()))
+    t1 = pa.Table.from_pandas(df.assign(time=93600000), preserve_index=False)
+    errors = {}
+    a = CM.compute_long([t0, t1], skip_bad=True, errors=errors)
+    b = CM.compute_long([t0])
+    assert list(errors) == [1]
+    from mff import frames
+    codes, dates = ["A"], [dt.date(2024, 1, 2)]
+    bad = []
+    for nm in a:
+        va, sa, _, _ = frames.from_long(a[nm], nm, codes=codes, dates=dates)
+        vb, sb, _, _ = frames.from_long(b[nm], nm, codes=codes, dates=dates)
+        bad += compare(va, sa, vb, sb, nm)
+    assert not bad, "\n".join(bad)
     # an off-grid row is no error: the stock-day is listed
     dp = ingest.to_device_panel(pd.concat([df, df.assign(time=150000000)]), dev)
     assert dp.rows.K == 1 and dp.rows.host()[2]["time"].tolist() == [93000000, 150000000]
