@@ -336,6 +336,141 @@ def null_extras(panel, step, k_ms: float, rates=(0.001, 0.01, 0.1), seed: int = 
     return out
 
 
+def rank_share_extras(panel, val, state, R: int = 8, reps: int = 3):
+    """One rank's share of the c4 pass at N = R, timed on one GPU (verdict r5 #5; no
+    collective runs: the exchanges' bytes are DESIGN §6's table).  Rank 0 of R owns stocks
+    shard_bounds(S, R, 0) (625 at R = 8) of every day and the day block shard_bounds(D, R, 0)
+    (313 days).  Timed, each alone on the launch stream (median of `reps`):
+      * the stage-1 grid kernels on the shard panel (engine.stage1_launch_times: group,
+        exact list, set H, wave pair; 1/R of the stock-days);
+      * doc_pdf step 1: the owner's sort of its 313 days at full width (R x 5 x S_loc
+        queries per day, [R][5][nd][S_loc] as the all_to_all delivers them);
+      * step 3: the count of the shard's OWN level keys against EVERY day's full sorted,
+        deduplicated list ([D][Mu], Mu ~ 20 K distinct of 25 K queries) -- its list reads
+        shrink with R, its per-(day, slice) setup and per-position output do not;
+      * step 5: the owner's origin lookup of its days, and the finalize of the rank's own
+        queries;
+      * stage 3: the z-score moments + z of the shard ([58][D][S_loc], R moment sets) and
+        the day-owner rank of 313 whole days at full width ([58][313][S]).
+    The full-width lists are the real c4 day lists (the 5,000-stock panel's queries)."""
+    import torch
+    from mff import _lib, catalog, dist, engine
+
+    lib = _lib.load()
+    dev = panel.device
+    S, D = panel.S, panel.D
+    s0, s1 = dist.shard_bounds(S, R, 0)
+    d0, d1 = dist.shard_bounds(D, R, 0)
+    S_loc, nd = s1 - s0, d1 - d0
+    st = torch.cuda.current_stream(dev)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st)
+            fn()
+            b.record(st)
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b))
+        return round(float(np.median(ts)), 3)
+
+    out = {"R": R, "S_loc": S_loc, "owner_days": nd}
+    shard = engine.DevicePanel(panel.bars[:, :, s0:s1].contiguous(), panel.mask[:, s0:s1].contiguous(),
+                               stocks_total=S)
+    kt = engine.stage1_launch_times(shard)
+    out["stage1_kernels_ms"] = {k: round(x["ms"], 3) for k, x in kt.items()
+                                if k in ("k_stage1g<ORD|ORDV|LVL|PDF>", "k_stage1 (exact list)",
+                                         "k_stage1s<OLS|MOMH>", "k_stage1s_pair")}
+
+    def pdf_side(p):
+        """doc_pdf queries [5][D][S] and level lists of panel p (the group launch only)."""
+        ids = catalog.PDF_IDS
+        v = torch.empty((5, p.D, p.S), dtype=torch.float64, device=dev)
+        s_ = torch.empty((5, p.D, p.S), dtype=torch.uint8, device=dev)
+        q = torch.empty((5, p.D, p.S), dtype=torch.float64, device=dev)
+        lv = torch.empty(lib.mff_pdf_levels_bytes(p.S, p.D), dtype=torch.uint8, device=dev)
+        ws = torch.empty(lib.mff_stage1_workspace_bytes(p.S, p.D), dtype=torch.uint8, device=dev)
+        b = p.bars
+        _lib.check(lib.mff_stage1_part(_lib.ptr(b[0]), _lib.ptr(b[1]), _lib.ptr(b[2]), _lib.ptr(b[3]),
+                                       _lib.ptr(b[4]), _lib.ptr(p.mask), p.S, p.D, _lib.int_array(ids), 5,
+                                       _lib.ptr(v), _lib.ptr(s_), _lib.ptr(q), _lib.ptr(lv), _lib.ptr(ws),
+                                       st.cuda_stream, 1), "mff_stage1_part(1)")
+        return q, lv
+    q_full, lv_full = pdf_side(panel)
+    del lv_full
+    M = 5 * S
+    q_sorted = torch.empty((D, M), dtype=torch.int64, device=dev)
+    sws = torch.empty(lib.mff_pdf_workspace_bytes(S, 1, D), dtype=torch.uint8, device=dev)
+    _lib.check(lib.mff_pdf_sort(_lib.ptr(q_full), 1, S, D, 0, D, _lib.ptr(q_sorted), _lib.ptr(sws),
+                                st.cuda_stream), "mff_pdf_sort")
+    del sws
+    keep = torch.ones_like(q_sorted, dtype=torch.bool)
+    keep[:, 1:] = q_sorted[:, 1:] != q_sorted[:, :-1]
+    Mu = int(keep.sum(1).max().item())
+    dedup = torch.full((D, Mu), -1, dtype=torch.int64, device=dev)
+    pos = keep.to(torch.int64).cumsum(1) - 1
+    rr = torch.arange(D, device=dev).unsqueeze(1).expand(D, M)
+    dedup[rr[keep], pos[keep]] = q_sorted[keep]
+    del keep, pos, rr, q_sorted
+    out["pdf_list_distinct_Mu"] = Mu
+    # step 1: the owner sorts its days, R x 5 x S_loc queries each
+    S_all = S_loc
+    q_all = q_full[:, d0:d1, :S_all * R].reshape(5, nd, R, S_all).permute(2, 0, 1, 3).contiguous()
+    srt = torch.empty((nd, R * 5 * S_all), dtype=torch.int64, device=dev)
+    sws = torch.empty(lib.mff_pdf_workspace_bytes(S_all, R, nd), dtype=torch.uint8, device=dev)
+    out["pdf_sort_owner_days_ms"] = timed(lambda: _lib.check(lib.mff_pdf_sort(
+        _lib.ptr(q_all), R, S_all, nd, 0, nd, _lib.ptr(srt), _lib.ptr(sws), st.cuda_stream), "sort"))
+    del srt, sws
+    # step 3: own keys against every day's full list
+    q_loc, lv_loc = pdf_side(shard)
+    counts = torch.empty((D, Mu), dtype=torch.int32, device=dev)
+    cws = torch.empty(256, dtype=torch.uint8, device=dev)
+    out["pdf_count_full_lists_ms"] = timed(lambda: _lib.check(lib.mff_pdf_count(
+        _lib.ptr(lv_loc), S_loc, D, 0, D, _lib.ptr(dedup), Mu, _lib.ptr(counts), _lib.ptr(cws),
+        st.cuda_stream), "count"))
+    # step 5: origin lookup of the owner's days, finalize of the own queries
+    org = torch.empty((R, 5, nd, S_all), dtype=torch.int32, device=dev)
+    dd = dedup[d0:d1].contiguous()
+    cc = counts[d0:d1].contiguous()
+    out["pdf_origin_owner_days_ms"] = timed(lambda: _lib.check(lib.mff_pdf_origin_counts(
+        _lib.ptr(q_all), R, S_all, nd, 0, nd, _lib.ptr(dd), _lib.ptr(cc), Mu, _lib.ptr(org),
+        st.cuda_stream), "origin"))
+    own = torch.zeros((5, D, S_loc), dtype=torch.int32, device=dev)
+    fv = torch.empty((5, D, S_loc), dtype=torch.float64, device=dev)
+    fs = torch.empty((5, D, S_loc), dtype=torch.uint8, device=dev)
+    out["pdf_finalize_own_ms"] = timed(lambda: _lib.check(lib.mff_pdf_finalize_own(
+        _lib.ptr(q_loc), _lib.ptr(own), S_loc, D, _lib.int_array([0, 1, 2, 3, 4]), _lib.ptr(fv), _lib.ptr(fs),
+        st.cuda_stream), "finalize_own"))
+    del q_all, org, dd, cc, own, fv, fs, counts, dedup, q_loc, lv_loc, q_full
+    # stage 3: z on the shard (R moment sets), rank of the owner's days at full width
+    rows = val.shape[0]
+    vs = val[:, :, s0:s1].contiguous()
+    ss = state[:, :, s0:s1].contiguous()
+    mom = torch.empty((rows, D, 3), dtype=torch.float64, device=dev)
+    mom_all = torch.empty((R, rows, D, 3), dtype=torch.float64, device=dev)
+    zo = torch.empty_like(vs)
+    zs = torch.empty_like(ss)
+
+    def z():
+        _lib.check(lib.mff_xs_moments(_lib.ptr(vs), _lib.ptr(ss), rows, D, S_loc, _lib.ptr(mom), st.cuda_stream),
+                   "moments")
+        mom_all.copy_(mom.unsqueeze(0).expand(R, -1, -1, -1))
+        _lib.check(lib.mff_xs_zscore(_lib.ptr(vs), _lib.ptr(ss), rows, D, S_loc, _lib.ptr(mom_all), R,
+                                     _lib.ptr(zo), _lib.ptr(zs), st.cuda_stream), "zscore")
+    out["stage3_z_shard_ms"] = timed(z)
+    del vs, ss, zo, zs, mom, mom_all
+    vo = val[:, d0:d1].contiguous()
+    so = state[:, d0:d1].contiguous()
+    ro, rs_ = torch.empty_like(vo), torch.empty_like(so)
+    out["stage3_rank_owner_days_ms"] = timed(lambda: engine._xs_rank_local(lib, vo, so, ro, rs_, st.cuda_stream))
+    del vo, so, ro, rs_, shard
+    torch.cuda.empty_cache()
+    return {"rank_share_n8": out}
+
+
 def final_exposure_extras(val, state, days: int = 250, name: str = "vol_return1min"):
     """MinFreqFactor.cal_final_exposure(20, 'z', mode='days') (MF:187-240) on one
     factor's exposure of S stocks x `days` days taken from the pass output, as the
@@ -503,6 +638,7 @@ def main():
         extras["stage3_rank_GBps"] = round(xs_bytes / (ms * 1e-3) / 1e9, 1)
         if rank == 0 and world == 1:
             extras.update(final_exposure_extras(val, state))
+            extras.update(rank_share_extras(panel, val, state))
         del val, state
         if rank == 0:
             extras.update(ingest_extras(panel, args.ingest_days, args.ingest_host_days))
