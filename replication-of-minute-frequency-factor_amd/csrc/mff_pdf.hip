@@ -196,10 +196,13 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, 
 //   L[0] = Q[P0-1], L[1..nv] = distinct slice values > L[0], L[nv+1 .. nv+PDF_PAD] = ~0
 // The slice is copied into L coalesced, then compacted in place: each thread's contiguous
 // chunk (at most PDF_SETUP_PER entries) goes through registers, and the scan's trailing
-// barrier orders every read before the first write.  The bucket table is filled by
-// scatter: distinct value i writes T[b] = i for the buckets between its predecessor's and
-// its own (T[b] = the first value whose bucket is >= b, i.e. lower_bound of the bucket's
-// lower edge), NBK + 1 writes in all instead of a binary search per bucket.
+// barrier orders every read before the first write.  The bucket table T[b] = the first
+// value whose bucket is >= b (lower_bound of the bucket's lower edge) is built in two
+// parallel steps: each value that opens its bucket marks T[bucket] = its index, then a
+// block-wide suffix minimum fills the empty buckets (round 6; the round-3 scatter wrote each
+// empty run from one thread -- up to ~2,000 serial stores for the run above the last value,
+// as the top bucket index lies in [2048, 4096) -- and with one workgroup per CU nothing hid
+// that: the slice setup took ~20 us).
 constexpr int PDF_SETUP_MAXQ = PDF_ZQ32 > PDF_ZQ ? (PDF_ZQ32 > PDF_KCAP ? PDF_ZQ32 : PDF_KCAP) : (PDF_ZQ > PDF_KCAP ? PDF_ZQ : PDF_KCAP);
 constexpr int PDF_SETUP_PER = (PDF_SETUP_MAXQ + PDF_CT - 1) / PDF_CT;
 template <typename CT>
@@ -207,7 +210,22 @@ __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, in
                                                     uint64_t* L, CT* C, uint16_t* T,
                                                     uint32_t* wsum, int* occ_s, uint64_t lo_floor = 0ull) {
   const int nq = P1 - P0;
-  for (int i = threadIdx.x; i < nq; i += blockDim.x) L[1 + i] = Q[P0 + i];
+  // every load of the copy in flight before the first LDS store (a rolled loop waits for
+  // each load in turn: ~13 global round trips per slice, with one workgroup per CU
+  // nothing hides them)
+  {
+    uint64_t x[PDF_SETUP_PER];
+#pragma unroll
+    for (int k = 0; k < PDF_SETUP_PER; ++k) {
+      const int i = (int)threadIdx.x + k * (int)blockDim.x;
+      x[k] = i < nq ? Q[P0 + i] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < PDF_SETUP_PER; ++k) {
+      const int i = (int)threadIdx.x + k * (int)blockDim.x;
+      if (i < nq) L[1 + i] = x[k];
+    }
+  }
   // lo_floor: a slice whose queries are all >= the split key counts every key below it
   // as `below` (L0 = split key - 1), so it need not read the list those keys are in
   const uint64_t Lq = P0 > 0 ? Q[P0 - 1] : 0ull;
@@ -240,6 +258,7 @@ __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, in
   for (int k = 0; k < PDF_SETUP_PER; ++k)
     if ((keep >> k) & 1u) L[1 + off++] = v[k];
   for (int i = threadIdx.x; i < nq; i += blockDim.x) C[i] = (CT)0;
+  for (int b = threadIdx.x; b <= PDF_NBK; b += blockDim.x) T[b] = 0xFFFFu;  // unmarked
   if (threadIdx.x < PDF_PAD) L[1 + nu + threadIdx.x] = ~0ull;
   __syncthreads();
   PdfSlice sl;
@@ -253,10 +272,42 @@ __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, in
   while (sl.nv > 0 && ((sl.qmax - sl.qmin) >> sh) >= (uint64_t)PDF_NBK) ++sh;
   sl.sh = sh;
   const uint64_t* L1 = L + 1;
-  for (int i = threadIdx.x; i <= sl.nv; i += blockDim.x) {
-    const int bi = i < sl.nv ? (int)((L1[i] - sl.qmin) >> sh) : PDF_NBK;
+  for (int i = threadIdx.x; i < sl.nv; i += blockDim.x) {
+    const int bi = (int)((L1[i] - sl.qmin) >> sh);
     const int bp = i > 0 ? (int)((L1[i - 1] - sl.qmin) >> sh) : -1;
-    for (int b = bp + 1; b <= bi; ++b) T[b] = (uint16_t)i;
+    if (bi != bp) T[bi] = (uint16_t)i;  // the first value of bucket bi
+  }
+  __syncthreads();
+  {
+    // suffix minimum over T[0 .. NBK) with T[NBK] = nv: thread t owns buckets
+    // [KB t, KB t + KB); a wave-level reverse scan, then one across the waves
+    static_assert(PDF_NBK % PDF_CT == 0, "buckets per thread");
+    constexpr int KB = PDF_NBK / PDF_CT;
+    const int t = (int)threadIdx.x, lane = lane_id(), wv = t >> 6, nw = (int)blockDim.x >> 6;
+    uint32_t m[KB];
+    uint32_t run = 0xFFFFu;
+#pragma unroll
+    for (int k = KB - 1; k >= 0; --k) {
+      m[k] = min((uint32_t)T[KB * t + k], run);
+      run = m[k];
+    }
+    // inclusive reverse min over lanes >= lane, then exclusive (lanes > lane)
+    uint32_t inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_down((int)inc, o, 64);
+      if (lane + o < 64) inc = min(inc, y);
+    }
+    uint32_t after = (uint32_t)__shfl_down((int)inc, 1, 64);
+    if (lane == 63) after = 0xFFFFu;
+    if (lane == 0) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t carry = (uint32_t)sl.nv;  // T[NBK]
+    for (int w = wv + 1; w < nw; ++w) carry = min(carry, wsum[w]);
+    carry = min(carry, after);
+#pragma unroll
+    for (int k = 0; k < KB; ++k) T[KB * t + k] = (uint16_t)min(m[k], carry);
+    if (t == 0) T[PDF_NBK] = (uint16_t)sl.nv;
   }
   __syncthreads();
   int occ = 0;
@@ -370,18 +421,29 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
     if (!readA) {
       // every list-A key is below this slice: their bars, from list A's weight bytes
       // (1 B per entry, 16 per load; the day's slots start 64-B aligned)
+      // (four 16-B loads in flight per thread and round)
       const uint8_t* WA = a.lvl_w + (size_t)d * a.cap;
-      for (int i = 16 * (int)threadIdx.x; i < nA; i += 16 * (int)blockDim.x) {
-        if (i + 16 <= nA) {
-          const uint4 q = *reinterpret_cast<const uint4*>(WA + i);
-          const uint32_t wq[4] = {q.x, q.y, q.z, q.w};
+      const int step = 16 * (int)blockDim.x;
+      for (int i0 = 16 * (int)threadIdx.x; i0 < nA; i0 += 4 * step) {
+        uint4 q4[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t h = (wq[k] & 0x00FF00FFu) + ((wq[k] >> 8) & 0x00FF00FFu);
-            below += (h & 0xFFFFu) + (h >> 16);
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + r * step;
+          q4[r] = i + 16 <= nA ? *reinterpret_cast<const uint4*>(WA + i) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + r * step;
+          if (i + 16 <= nA) {
+            const uint32_t wq[4] = {q4[r].x, q4[r].y, q4[r].z, q4[r].w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const uint32_t h = (wq[k] & 0x00FF00FFu) + ((wq[k] >> 8) & 0x00FF00FFu);
+              below += (h & 0xFFFFu) + (h >> 16);
+            }
+          } else if (i < nA) {
+            for (int k = i; k < nA; ++k) below += WA[k];
           }
-        } else {
-          for (int k = i; k < nA; ++k) below += WA[k];
         }
       }
     }
