@@ -343,7 +343,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       if (qw) {
         const double rp = frsq(prod);  // (the same value as above: CSE)
         const double ip = rp * rp;     // 1 / prod
-        const double sc = fsqrt(Cv);   // cov < 0: NaN, as cov**0.5
+        // cov**0.5 from the bare hardware rsq estimate (~5e-8 relative, mff_fmath.h): every
+        // term of this mean is >= 0 (or NaN), so the estimate's error does not grow in the
+        // sum; the refined step is kept where terms can cancel (1 / prod: beta, the corrs)
+        const double sc = Cv * __builtin_amdgcn_rsq(Cv);  // cov < 0: NaN, as cov**0.5
         sq += (Cv == 0.0 ? 0.0 : sc) * ip;  // cov**0.5 / (vx*vy) / (50^1.5)   CM:137
         scs += Cv * Cv * ip;                // cov**2 / (vx*vy)     CM:212
         scr += Cv * rp;                     // cov / (vx*vy)**0.5   CM:261
