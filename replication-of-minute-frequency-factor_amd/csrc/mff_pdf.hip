@@ -208,7 +208,10 @@ constexpr int PDF_SETUP_PER = (PDF_SETUP_MAXQ + PDF_CT - 1) / PDF_CT;
 template <typename CT>
 __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, int P0, int P1,
                                                     uint64_t* L, CT* C, uint16_t* T,
-                                                    uint32_t* wsum, int* occ_s, uint64_t lo_floor = 0ull) {
+                                                    uint32_t* wsum, int* occ_s, uint64_t lo_floor = 0ull,
+                                                    const uint32_t* cfill = nullptr) {
+  // cfill (optional): per sorted position of the slice a count word; the counter of each
+  // distinct value then starts from the word at its first position instead of 0
   const int nq = P1 - P0;
   // every load of the copy in flight before the first LDS store (a rolled loop waits for
   // each load in turn: ~13 global round trips per slice, with one workgroup per CU
@@ -256,8 +259,12 @@ __device__ __forceinline__ PdfSlice pdf_slice_setup(const uint64_t* Q, int M, in
   uint32_t off = block_excl_scan(cnt, wsum, &nu);  // ends synced: every read above is done
 #pragma unroll
   for (int k = 0; k < PDF_SETUP_PER; ++k)
-    if ((keep >> k) & 1u) L[1 + off++] = v[k];
-  for (int i = threadIdx.x; i < nq; i += blockDim.x) C[i] = (CT)0;
+    if ((keep >> k) & 1u) {
+      if (cfill) C[off] = (CT)cfill[i0 + k];
+      L[1 + off++] = v[k];
+    }
+  if (!cfill)
+    for (int i = threadIdx.x; i < nq; i += blockDim.x) C[i] = (CT)0;
   for (int b = threadIdx.x; b <= PDF_NBK; b += blockDim.x) T[b] = 0xFFFFu;  // unmarked
   if (threadIdx.x < PDF_PAD) L[1 + nu + threadIdx.x] = ~0ull;
   __syncthreads();
@@ -818,26 +825,80 @@ __global__ __launch_bounds__(PDF_CT) void k_pdf_finalize(PdfArgs a) {
 // multi-rank, day-owner side: the counts of day d's sorted list (summed over ranks) at
 // each query's first sorted position, written in the queries' origin layout
 // [R][5][nd][S_all] (the all_to_all receive buffer of mff_pdf_sort), so one all_to_all
-// returns every rank the counts of its own queries.  Thread per query, binary search
-// over the day's sorted list (L2-resident).
-__global__ __launch_bounds__(256) void k_pdf_origin(const double* q_all, int RT, int S, int D, int d0, int nd,
-                                                     const uint64_t* q_sorted, const uint32_t* counts, int M,
-                                                     uint32_t* out) {
-  const size_t n = (size_t)RT * nd * S;
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const int s = (int)(i % S);
-  const size_t rd = i / S;
-  const int dd = (int)(rd % nd);
-  const int rt = (int)(rd / nd);
-  const double x = q_all[((size_t)rt * D + d0 + dd) * S + s];
-  uint32_t c = 0u;
-  if (!__builtin_isnan(x)) {
-    const uint64_t* Q = q_sorted + (size_t)dd * M;
-    const int j = lower_bound_u64(Q, 0, M, ord64(x));
-    c = counts[(size_t)dd * M + j];
+// returns every rank the counts of its own queries.  One workgroup per (day, slice of
+// sorted positions), as the count: the slice's distinct values, a bucket table and their
+// count words in LDS (pdf_slice_setup with cfill), then every origin query of the day
+// finds its value by the binary lifting of the count's key loop (round 6; the thread per
+// query with a global binary search over the day's list and 64-bit index divisions took
+// 0.66 ms for one rank's 313 days at N = 8, bench extras rank_share_n8).  Slice 0 also
+// writes 0 for the NaN queries (no level passed, or an absent stock-day).
+__global__ __launch_bounds__(PDF_CT) void k_pdf_origin_lds(const double* q_all, int RT, int S, int D, int d0, int nd,
+                                                          const uint64_t* q_sorted, const uint32_t* counts, int M,
+                                                          int Z, int Mz, uint32_t* out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ int occ_s;
+  __shared__ uint32_t wsum[16];
+  const int dd = blockIdx.x / Z, z = blockIdx.x % Z;
+  if (dd >= nd) return;
+  const uint64_t* Q = q_sorted + (size_t)dd * M;
+  const int P0 = z * Mz, P1 = min(M, P0 + Mz);
+  if (P0 >= P1) return;
+  uint64_t* L = reinterpret_cast<uint64_t*>(smem);
+  uint32_t* C = reinterpret_cast<uint32_t*>(L + Mz + 1 + PDF_PAD);
+  uint16_t* T = reinterpret_cast<uint16_t*>(C + Mz);
+  const PdfSlice sl = pdf_slice_setup(Q, M, P0, P1, L, C, T, wsum, &occ_s, 0ull, counts + (size_t)dd * M + P0);
+  const char* Lb = reinterpret_cast<const char*>(sl.L);
+  const bool shallow = sl.steps <= 6;
+  constexpr int RB = 4;
+  const int bd = (int)blockDim.x;
+  for (int rt = 0; rt < RT; ++rt) {
+    const double* qrow = q_all + ((size_t)rt * D + d0 + dd) * S;
+    uint32_t* orow = out + ((size_t)rt * nd + dd) * S;
+    for (int s0 = threadIdx.x; s0 < S; s0 += RB * bd) {
+      uint64_t key[RB];
+      bool in[RB], nan_[RB];
+      uint32_t jb[RB];
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const int s = s0 + k * bd;
+        const double q = s < S ? qrow[s] : 0.0;
+        nan_[k] = s < S && __builtin_isnan(q);
+        key[k] = ord64(q);
+        in[k] = s < S && !nan_[k] && sl.nv > 0 && key[k] > sl.L0 && key[k] <= sl.qmax;
+      }
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const bool g = in[k] && key[k] > sl.qmin;
+        jb[k] = g ? (uint32_t)sl.T[(key[k] - sl.qmin) >> sl.sh] << 3 : 0u;
+      }
+      if (shallow) {
+#pragma unroll
+        for (int st = 5; st >= 0; --st) {
+          if (st < sl.steps) {
+            const uint32_t bb = 8u << st;
+            uint64_t x[RB];
+#pragma unroll
+            for (int k = 0; k < RB; ++k) x[k] = *reinterpret_cast<const uint64_t*>(Lb + jb[k] + bb);
+#pragma unroll
+            for (int k = 0; k < RB; ++k) jb[k] += x[k] < key[k] ? bb : 0u;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < RB; ++k) {
+          if (!in[k]) continue;
+          int lo, hi;
+          sl.range(key[k], lo, hi);
+          jb[k] = (uint32_t)lower_bound_u64(sl.L + 1, lo, hi, key[k]) << 3;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        if (in[k]) orow[s0 + k * bd] = C[jb[k] >> 3];
+        else if (nan_[k] && z == 0) orow[s0 + k * bd] = 0u;
+      }
+    }
   }
-  out[i] = c;
 }
 
 // own queries [5][D][S] with their counts in the same layout (2 n_less + n_eq summed over
@@ -950,7 +1011,7 @@ static int pdf_launch(PdfArgs& a, const uint64_t* q_sorted, int M, hipStream_t s
   // one rank, one day per sorted list: slices aligned at PDF_KSPLIT (one more slot per day
   // for the split; MFF_PDF_KSLICE=0 keeps the plain position slices, A/B timing)
   const char* ks = getenv("MFF_PDF_KSLICE");
-  a.kslice = mode == 1 && a.packed && !a.frame && !(ks && ks[0] == '0');
+  a.kslice = mode != 2 && a.packed && !a.frame && !(ks && ks[0] == '0');
   if (a.kslice) {
     a.learn = pdf_learn_state(st);
     if (!a.learn) return -2;
@@ -967,15 +1028,14 @@ static int pdf_launch(PdfArgs& a, const uint64_t* q_sorted, int M, hipStream_t s
   } else {
     const long long nblk = ((long long)a.Z * a.nd + 7) / 8 * 8;
     MFF_REQUIRE(nblk < (1ll << 31), "mff_pdf_count: too many days in one call");
-    if (mode == 1) {
+    if (mode == 1)
       hipLaunchKernelGGL(k_pdf_count<true>, dim3((unsigned)nblk), dim3(PDF_CT), lds, st, a);
-      if (a.kslice) {
-        MFF_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_pdf_learn, dim3((unsigned)((a.nd + 15) / 16)), dim3(64), 0, st, q_sorted, M, a.learn);
-      }
-    }
     else
       hipLaunchKernelGGL(k_pdf_count<false>, dim3((unsigned)nblk), dim3(PDF_CT), lds, st, a);
+    if (a.kslice) {  // (the sharded count of the full day lists learns the same key on every rank)
+      MFF_LAUNCH_CHECK();
+      hipLaunchKernelGGL(k_pdf_learn, dim3((unsigned)((a.nd + 15) / 16)), dim3(64), 0, st, q_sorted, M, a.learn);
+    }
   }
   MFF_LAUNCH_CHECK();
   return 0;
@@ -1047,9 +1107,11 @@ int mff_pdf_origin_counts(const double* q_all, int R, int S_all, int D, int d0, 
   MFF_REQUIRE(R >= 1 && S_all > 0 && D > 0 && nd > 0 && d0 >= 0 && d0 + nd <= D && M > 0 && M <= PDF_MAXM,
               "mff_pdf_origin_counts: bad sizes R=%d S=%d D=%d d0=%d nd=%d M=%d", R, S_all, D, d0, nd, M);
   MFF_REQUIRE(q_all && q_sorted && counts && out, "mff_pdf_origin_counts: NULL buffer");
-  const size_t n = (size_t)R * 5 * nd * S_all;
-  hipLaunchKernelGGL(k_pdf_origin, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream), q_all,
-                     R * 5, S_all, D, d0, nd, q_sorted, counts, M, out);
+  int Z, Mz;
+  size_t lds;
+  pdf_slices(M, Z, Mz, lds, true);
+  hipLaunchKernelGGL(k_pdf_origin_lds, dim3((unsigned)((long long)Z * nd)), dim3(PDF_CT), lds, as_stream(stream),
+                     q_all, R * 5, S_all, D, d0, nd, q_sorted, counts, M, Z, Mz, out);
   MFF_LAUNCH_CHECK();
   return 0;
 }
