@@ -96,17 +96,34 @@ __host__ __device__ constexpr uint32_t kFamOf(int f) {
        : f < 42 ? F_LVL : f < 47 ? F_PDF : f < 50 ? F_ORDV : f < 52 ? F_TRD : f < 54 ? F_SUMV : F_TRD;
 }
 
+// The one field -> families table: kFieldFams[p] = the families whose values read field p
+// (open, high, low, close, volume).  Every grid kernel loads a field only for families
+// listed here (the serial kernels' planes kPlanes derive from it; the group kernel's load
+// predicates are checked against it), and a kept row-set stock-day's null field sends
+// exactly these families to mff_stage1_rows (rows_fams): a family the table misses for a
+// field would be stored by a grid kernel from that field's fill values under a null.
+inline constexpr uint32_t kFieldFams[5] = {
+    F_SEG | F_ORD | F_MOMR | F_TRD,                                              // open
+    F_OLS | F_MOMH,                                                              // high
+    F_OLS | F_MOMH,                                                              // low
+    F_SEG | F_ORD | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD,            // close
+    F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD,   // volume
+};
+// the fields (bit p) the families of `set` read
+__host__ __device__ constexpr uint32_t fields_of(uint32_t set) {
+  return ((set & kFieldFams[0]) ? 1u : 0u) | ((set & kFieldFams[1]) ? 2u : 0u) | ((set & kFieldFams[2]) ? 4u : 0u) |
+         ((set & kFieldFams[3]) ? 8u : 0u) | ((set & kFieldFams[4]) ? 16u : 0u);
+}
+
 // Row set (include/mff.h): the families mff_stage1_rows computes for a stock-day with
 // row-set flags `fl` (valid word 7, or its first row's `reserved`): every family, unless
 // the grid bars are kept (MFF_ROWS_KEEP) -- then those reading a field that holds a null
-// (the fields each family's grid kernel loads: open, high, low, close, volume)
+// (kFieldFams)
 __host__ __device__ constexpr uint32_t rows_fams(uint32_t fl) {
   const uint32_t nb = (fl >> MFF_ROWS_NULL_SHIFT) & 31u;
   return !(fl & MFF_ROWS_KEEP) ? ~0u
-         : ((nb & 1u) ? (F_SEG | F_ORD | F_MOMR | F_TRD) : 0u) |
-           ((nb & 6u) ? (F_OLS | F_MOMH) : 0u) |
-           ((nb & 8u) ? (F_SEG | F_ORD | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD) : 0u) |
-           ((nb & 16u) ? (F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD) : 0u);
+         : ((nb & 1u) ? kFieldFams[0] : 0u) | ((nb & 2u) ? kFieldFams[1] : 0u) | ((nb & 4u) ? kFieldFams[2] : 0u) |
+           ((nb & 8u) ? kFieldFams[3] : 0u) | ((nb & 16u) ? kFieldFams[4] : 0u);
 }
 // the families a grid kernel must not store for a stock-day whose valid word 7 is w7
 __host__ __device__ constexpr uint32_t grid_skip(uint32_t w7) { return (w7 & MFF_ROWS_LISTED) ? rows_fams(w7) : 0u; }

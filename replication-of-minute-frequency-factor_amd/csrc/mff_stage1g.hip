@@ -247,10 +247,14 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
           for (int k = 0; k < K; ++k) x[k] = dflt;
         }
       };
-      const uint32_t needO = F_SEG | F_MOMR | F_TRD;
-      const uint32_t needHL = F_OLS | F_MOMH;
-      const uint32_t needC = F_SEG | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD;
-      const uint32_t needV = F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD;
+      constexpr uint32_t needO = F_SEG | F_MOMR | F_TRD;
+      constexpr uint32_t needHL = F_OLS | F_MOMH;
+      constexpr uint32_t needC = F_SEG | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD;
+      constexpr uint32_t needV = F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD;
+      // a field is loaded only for families the field table lists for it (mff_internal.h)
+      static_assert(!(needO & ~kFieldFams[0]) && !(needHL & ~(kFieldFams[1] & kFieldFams[2])) &&
+                        !(needC & ~kFieldFams[3]) && !(needV & ~kFieldFams[4]),
+                    "k_stage1g loads a field for a family kFieldFams does not list");
       auto loadv = [&](uint32_t (&x)[K]) {  // volume, absent bars 0
         if (ln) {
           const uint4* p4 = reinterpret_cast<const uint4*>(a.fld[4] + sd * NBAR + 16 * g);
@@ -1120,19 +1124,13 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
     a.row[id] = (int8_t)r;
     a.fam |= kFactorFamily[id];
   }
-  constexpr uint32_t use[5] = {F_SEG | F_ORD | F_MOMR | F_TRD, F_OLS | F_MOMH, F_OLS | F_MOMH,
-                               F_SEG | F_ORD | F_MOMR | F_SUMC | F_CORR | F_LVL | F_PDF | F_TRD,
-                               F_ORD | F_MOMV | F_SUMC | F_SUMV | F_CORR | F_LVL | F_PDF | F_ORDV | F_TRD};
   // a kept row-set stock-day's null field sends exactly the families that read it to
-  // mff_stage1_rows (include/mff.h MFF_ROWS_KEEP; rows_fams in mff_internal.h)
-  static_assert(rows_fams(MFF_ROWS_KEEP | (1u << MFF_ROWS_NULL_SHIFT)) == use[0], "open");
-  static_assert(rows_fams(MFF_ROWS_KEEP | (2u << MFF_ROWS_NULL_SHIFT)) == use[1], "high");
-  static_assert(rows_fams(MFF_ROWS_KEEP | (4u << MFF_ROWS_NULL_SHIFT)) == use[2], "low");
-  static_assert(rows_fams(MFF_ROWS_KEEP | (8u << MFF_ROWS_NULL_SHIFT)) == use[3], "close");
-  static_assert(rows_fams(MFF_ROWS_KEEP | (16u << MFF_ROWS_NULL_SHIFT)) == use[4], "volume");
+  // mff_stage1_rows (include/mff.h MFF_ROWS_KEEP; rows_fams and kFieldFams in mff_internal.h)
+  static_assert(rows_fams(MFF_ROWS_KEEP | (1u << MFF_ROWS_NULL_SHIFT)) == kFieldFams[0], "open");
+  static_assert(rows_fams(MFF_ROWS_KEEP | (16u << MFF_ROWS_NULL_SHIFT)) == kFieldFams[4], "volume");
   static_assert(rows_fams(MFF_ROWS_LISTED) == ~0u && grid_skip(0u) == 0u, "listed whole / not listed");
   for (int f = 0; f < 5; ++f)
-    MFF_REQUIRE(!(a.fam & use[f]) || fld[f] != nullptr, "mff_stage1: field plane %d required", f);
+    MFF_REQUIRE(!(a.fam & kFieldFams[f]) || fld[f] != nullptr, "mff_stage1: field plane %d required", f);
   MFF_REQUIRE(!(a.fam & F_PDF) || (pdf_query != nullptr && pdf_levels != nullptr),
               "mff_stage1: doc_pdf requested but pdf_query / pdf_levels is NULL");
   hipStream_t st = as_stream(stream);

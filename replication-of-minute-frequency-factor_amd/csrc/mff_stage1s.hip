@@ -127,12 +127,9 @@ struct Mask {
   }
 };
 
-// planes a family set reads (bit p = plane p: open, high, low, close, volume)
-__host__ __device__ constexpr uint32_t kPlanes(uint32_t set) {
-  return ((set & (F_SEG | F_MOMR | F_TRD | F_ORD)) ? 1u : 0u) | ((set & (F_OLS | F_MOMH)) ? 6u : 0u) |
-         ((set & (F_SEG | F_MOMR | F_TRD | F_ORD | F_SUMC | F_CORR)) ? 8u : 0u) |
-         ((set & (F_TRD | F_ORD | F_MOMV | F_SUMV | F_SUMC | F_CORR)) ? 16u : 0u);
-}
+// planes a family set reads (bit p = plane p: open, high, low, close, volume): the field
+// table of mff_internal.h
+__host__ __device__ constexpr uint32_t kPlanes(uint32_t set) { return fields_of(set); }
 typedef __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
