@@ -73,13 +73,10 @@ constexpr int PDF_CT = 1024;     // threads per count / finalize workgroup (<= 1
 // The one value every stock-day holds is 1.0 (c_last / c_last: the last close's level),
 // so its equal keys are counted apart, in a full u32.
 constexpr int PDF_LB = 21;
-// count: level-list entries per thread per chunk (8 or 16) and whether the next chunk is
-// loaded while this one is searched
+// count: level-list entries per thread per chunk (8 or 16; the next chunk is loaded while
+// this one is searched)
 #ifndef MFF_PDF_UNR
 #define MFF_PDF_UNR 8
-#endif
-#ifndef MFF_PDF_PF
-#define MFF_PDF_PF 1
 #endif
 
 struct QLoader {
@@ -409,10 +406,12 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
   uint64_t* L = reinterpret_cast<uint64_t*>(smem);  // [mz + 1 + PDF_PAD]
   CT* C = reinterpret_cast<CT*>(L + mz + 1 + PDF_PAD);  // [mz]
   uint16_t* T = reinterpret_cast<uint16_t*>(C + mz);
+  __shared__ int nxt_s[2];  // the key loop's next chunk, per list
   if (threadIdx.x == 0) {
     *below_s = 0u;
     *inw_s = 0u;
     *one_s = 0u;
+    nxt_s[0] = nxt_s[1] = 0;
   }
   const PdfSlice sl = pdf_slice_setup(Q, a.M, P0, P1, L, C, T, wsum, occ_s, lo_floor);
 
@@ -455,9 +454,8 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
       }
     }
     // The day's level list is flat (stage 1 appends every stock-day's levels: key =
-    // c_last / c as ord64, weight = bars at the level), so a thread simply takes every
-    // blockDim-th entry, UNR at a time (their loads in flight together, their searches
-    // interleaved).  A key at or below Q[P0-1] only adds its weight to `below`; a key
+    // c_last / c as ord64, weight = bars at the level), so a thread simply takes chunks of
+    // UNR entries (their loads in flight together, their searches interleaved).  A key at or below Q[P0-1] only adds its weight to `below`; a key
     // above the slice belongs to a later slice.  Search: binary lifting from T[b]-1
     // (L1[T[b]-1] < key <= L1[T[b+1]]), one LDS read, compare and select per step.  With
     // at most 6 steps the probes stay inside the PDF_PAD sentinels (probe <= nv + 2^steps
@@ -576,31 +574,37 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
         }
       }
     };
-    const int stride = (int)blockDim.x;
+    // The chunks are handed out dynamically, 64 per wave-grab (lane l takes chunk b + l:
+    // a wave still reads 4 KB of keys contiguously) from an LDS counter per list: with one
+    // workgroup per CU a static round-robin split left the early waves waiting at the
+    // barrier after the loop for the late ones (round 6 stamps: ~19 % of a workgroup's
+    // cycles between wave 0's loop end and the scan, profiles/r06/count_stamps.log)
+    const int lane = lane_id();
+    auto grab = [&](int list) -> int {
+      int b = 0;
+      if (lane == 0) b = atomicAdd(&nxt_s[list], 64);
+      return __builtin_amdgcn_readfirstlane(b);
+    };
     for (int list = 0; list < 2; ++list) {
       if (list == 0 ? !readA : !readB) continue;
       s = list == 0 ? 0 : (int)a.cap - nB;
       e = list == 0 ? nA : (int)a.cap;
       s8 = s & ~(UNR - 1);  // 64-B aligned chunks (every day's region starts 64-B aligned)
       const int nch = (e - s8 + UNR - 1) / UNR;
-      uint64_t ka[UNR];
-      uint32_t wa[UNR];
-      if constexpr (MFF_PDF_PF) {
-        uint64_t kb[UNR];
-        uint32_t wb[UNR];
-        fetch(ka, wa, (int)threadIdx.x);
-        for (int c0 = (int)threadIdx.x; c0 < nch; c0 += 2 * stride) {
-          fetch(kb, wb, c0 + stride);
-          process(ka, wa);
-          if (c0 + stride >= nch) break;
-          fetch(ka, wa, c0 + 2 * stride);
-          process(kb, wb);
-        }
-      } else {  // no prefetch: the other waves hide a chunk's loads
-        for (int c0 = (int)threadIdx.x; c0 < nch; c0 += stride) {
-          fetch(ka, wa, c0);
-          process(ka, wa);
-        }
+      uint64_t ka[UNR], kb[UNR];
+      uint32_t wa[UNR], wb[UNR];
+      // software-pipelined over two register sets: the next grab's chunk loads before this
+      // chunk's searches (a chunk past the list loads zero weights: processed as nothing)
+      int b0 = grab(list);
+      fetch(ka, wa, b0 + lane);
+      while (b0 < nch) {  // wave-uniform
+        const int b1 = grab(list);
+        fetch(kb, wb, b1 + lane);
+        process(ka, wa);
+        if (b1 >= nch) break;
+        b0 = grab(list);
+        fetch(ka, wa, b0 + lane);
+        process(kb, wb);
       }
     }
     below = (uint32_t)__reduce_add_sync(~0ull, (int)below);
