@@ -327,29 +327,34 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       const bool vz = !cx && Vx != 0.0;
       const double prod = Vx * Vy;
       const bool qw = !cx && !cy && prod != 0.0;
-      double beta;
-      if (qw) {
-        // cov / var_x = cov * var_y / (var_x var_y): the window's 1 / prod serves beta too
-        // (one rounding more than the quotient, no division)
-        const double rp = frsq(prod);  // prod < 0: NaN, as sqrt(prod)
-        const double ip = rp * rp;     // 1 / prod
-        beta = Cv * Vy * ip;
-      } else {
-        beta = fdiv(vz ? (cy ? 0.0 : Cv) : y0 + Sy * 0.02, vz ? Vx : x0 + Sx * 0.02);
-      }
-      if (qw) {
-        const double rp = frsq(prod);  // (the same value as above: CSE)
-        const double ip = rp * rp;     // 1 / prod
-        // cov**0.5 from the bare hardware rsq estimate (~5e-8 relative, mff_fmath.h): every
-        // term of this mean is >= 0 (or NaN), so the estimate's error does not grow in the
-        // sum; the refined step is kept where terms can cancel (1 / prod: beta, the corrs)
-        const double sc = Cv * __builtin_amdgcn_rsq(Cv);  // cov < 0: NaN, as cov**0.5
-        sq += (Cv == 0.0 ? 0.0 : sc) * ip;  // cov**0.5 / (vx*vy) / (50^1.5)   CM:137
-        scs += Cv * Cv * ip;                // cov**2 / (vx*vy)     CM:212
-        scr += Cv * rp;                     // cov / (vx*vy)**0.5   CM:261
+      // cov / var_x = cov * var_y / (var_x var_y): the window's 1 / prod serves beta too
+      // (one rounding more than the quotient, no division).  One rsq per window, outside
+      // the branches (the two branch-local copies were not merged)
+      const double rp = frsq(prod);  // prod < 0: NaN, as sqrt(prod)
+      const double ip = rp * rp;     // 1 / prod
+      double beta = Cv * Vy * ip;
+      auto qsums = [&]() {
+        // cov**0.5 from the bare hardware sqrt (2^29 ulp = 1.2e-7 relative, as the rsq
+        // estimate, mff_fmath.h; 0 for cov == 0, NaN for cov < 0, as cov**0.5): every term
+        // of this mean is >= 0 (or NaN), so the estimate's error does not grow in the sum;
+        // the refined step is kept where terms can cancel (1 / prod: beta, the corrs)
+        sq += __builtin_amdgcn_sqrt(Cv) * ip;  // cov**0.5 / (vx*vy) / (50^1.5)   CM:137
+        scs += Cv * Cv * ip;                   // cov**2 / (vx*vy)     CM:212
+        scr += Cv * rp;                        // cov / (vx*vy)**0.5   CM:261
         ++Wq;
+      };
+      // the usual wave: every window regular, its sums without selects.  Otherwise a window
+      // constant on a side, or with a zero variance product, takes the quotient (rare; as a
+      // select the division ran for every window)
+      if (__builtin_amdgcn_ballot_w64(!qw) == 0ull) {
+        qsums();
+      } else {
+        if (!qw) beta = fdiv(vz ? (cy ? 0.0 : Cv) : y0 + Sy * 0.02, vz ? Vx : x0 + Sx * 0.02);
+        if (qw) qsums();
       }
-      if (W == 0) b0 = beta;  // betas shifted by the first one (a member)
+      // betas shifted by the first one (a member); in the full-wave walk every lane's first
+      // window is m = 49 (a scalar test)
+      if (ALLP ? m == 49 : W == 0) b0 = beta;
       const double db = beta - b0;
       bd1 += db; bd2 += db * db;
       bl = beta;
@@ -461,8 +466,10 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
           // lane meets its second non-zero-volume row (set B bounds the wave pair: its
           // walk 16.9 ms vs set A's 15.6 with both waves on one set; the branch instead of
           // six selects per bar: pair 16.2 -> 15.8 ms.  Set A's capture stays select-based:
-          // its branch form measured much slower)
+          // its branch form measured much slower).  The empty volatile asm keeps the
+          // compiler from turning the branch back into selects (round 6: 15.86 -> 15.69 ms)
           if (__builtin_amdgcn_ballot_w64(nzc == 1) != 0ull) {
+            asm volatile("");
             if (nzc == 1) { x5 = pcz; y5 = pvz; x6 = c; }
           }
           const double dy = pvz - y5, e5 = pcz - x5, e6 = c - x6;
