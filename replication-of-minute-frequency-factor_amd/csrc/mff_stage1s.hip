@@ -223,7 +223,6 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   // walk), so a constant subset sums to exact zeros (C3) without a min / max per bar
   double s1 = 0, s2 = 0, s3 = 0, s4 = 0, u1 = 0, u2 = 0, w1 = 0, w2 = 0;
   double xu = 0.0, xd = 0.0;
-  bool hu = false, hd = false;
   int nu = 0, ndn = 0;
   // ORD: products of close/open over the bars at or beyond the volume thresholds
   double p50 = 1.0, p20 = 1.0, pb50 = 1.0;
@@ -378,16 +377,14 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         const double dd = (ALLP || pk) ? r - x0r : 0.0, d2 = dd * dd;
         s1 += dd; s2 += d2; s3 = fma(d2, dd, s3); s4 = fma(d2, d2, s4);
         const bool up = pk & (r > 0.0), dn = pk & (r < 0.0);  // r is finite (no NaN case)
+        // first up / down member of each lane: the subset's count is still zero (no "seen"
+        // flags).  (Selects: a wave-uniform branch taken only while some lane meets its
+        // first one measured much slower here, round 3)
+        const bool cu = up & (nu == 0), cd = dn & (ndn == 0);
         nu += up ? 1 : 0;
         ndn += dn ? 1 : 0;
-        // first up / down member of each lane
-        const bool cu = up & !hu, cd = dn & !hd;
-        // (selects: a wave-uniform branch taken only while some lane meets its first one
-        // measured much slower here, round 3)
         xu = cu ? r : xu;
         xd = cd ? r : xd;
-        hu |= up;
-        hd |= dn;
         const double eu = up ? r - xu : 0.0, ed = dn ? r - xd : 0.0;
         u1 += eu; u2 = fma(eu, eu, u2);
         w1 += ed; w2 = fma(ed, ed, w2);
@@ -432,17 +429,19 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     // one reciprocal per close and per volume serves every quotient of this bar and
     // of the bars that follow it (pct_change, Amihud)
     double rc = 1.0, rv = 1.0;
+    // the full-wave walk: the previous present bar is bar m - 1, row k is bar k (scalar tests)
+    const bool hpv = ALLP ? m > 0 : hp;
     if (fam & (F_SUMC | F_CORR)) {
       rc = frcp(c);
       rv = frcp(vf != 0u ? v : 1.0);
     }
     if (fam & F_SUMC) {
-      if (hp && vf != 0u) amh += fabs(c - (double)cp) * (rcp_ * rv);  // |dc| / (c_prev * v)
+      if (hpv && vf != 0u) amh += fabs(c - (double)cp) * (rcp_ * rv);  // |dc| / (c_prev * v)
     }
     if (fam & F_CORR) {
       const double dc = c - xc, dv = v - yv;
       A1 += dc; A2 = fma(dc, dc, A2); B1 += dv; B2 = fma(dv, dv, B2); X0 = fma(dc, dv, X0);
-      if (hp) {
+      if (hpv) {
         X1 = fma(dc, dvp, X1);  // pvd: (close, previous volume)
         X2 = fma(dcp, dv, X2);  // pvl: (previous close, volume) = (close, next volume)
         const double ex = fdivr(c - (double)cp, (double)cp, rcp_) - x1;  // prv
@@ -452,7 +451,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
         nchv += chv ? 1 : 0;
         chlc = chc;
         chlv = chv;
-        const bool r1 = kr == 1;
+        const bool r1 = ALLP ? m == 1 : kr == 1;
         ch1c = r1 ? chc : ch1c;
         ch1v = r1 ? chv : ch1v;
       }
