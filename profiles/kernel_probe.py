@@ -16,6 +16,10 @@ S = int(os.environ.get("PROBE_S", "5000"))
 D = int(os.environ.get("PROBE_D", "2500"))
 dev = torch.device("cuda:0")
 bars, mask = synth.make_panel_device(S, D, dev, config=4)
+if os.environ.get("PROBE_RAGGED", "0") != "0":  # the bench's c5 panel: c4 made ragged in place
+    g = torch.Generator(device=dev)
+    g.manual_seed(20251029)
+    synth.make_ragged_device(bars, mask, g)
 panel = engine.DevicePanel(bars, mask, stocks_total=S)
 engine.stage1_launch_times(panel)
 res = {}
