@@ -254,9 +254,6 @@ __device__ __forceinline__ uint32_t gmin_u(uint32_t x) {
 // partners are DPP patterns inside the 16-lane row (xor 1, 2, 3 quad_perm; xor 7
 // row_half_mirror; xor 15 row_mirror; xor 8 row_ror:8) except xor 4 (ds_swizzle).
 constexpr int QP_XOR3 = 0x1B;   // quad_perm [3,2,1,0]
-#ifndef MFF_LANE_NET
-#define MFF_LANE_NET 1
-#endif
 constexpr int ROW_ROR8 = 0x128;
 
 template <int CTRL>
@@ -327,14 +324,7 @@ __device__ __forceinline__ void gsort16_lane(uint32_t (&a)[K]) {
 }
 __device__ __forceinline__ void gsort256u(uint32_t (&a)[K]) {
   // sizes 2..16 inside the lane
-#if MFF_LANE_NET
   gsort16_lane(a);
-#else
-  glocal<1, true>(a);
-  glocal<2, true>(a); glocal<1, false>(a);
-  glocal<4, true>(a); glocal<2, false>(a); glocal<1, false>(a);
-  glocal<8, true>(a); glocal<4, false>(a); glocal<2, false>(a); glocal<1, false>(a);
-#endif
   // size 32: flip with lane ^ 1
   gcross<1, 1, true>(a); glocal_tail(a);
   // size 64: flip lane ^ 3, then lane ^ 1

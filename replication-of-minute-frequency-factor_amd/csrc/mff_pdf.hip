@@ -43,10 +43,7 @@ constexpr int PDF_MAXM = 1 << 24;
 constexpr uint64_t PDF_KSPLIT0 = 0xBFF0000000000000ull;  // ord64(1.0)
 // slice capacity of the split-aligned count (LDS: 12 B per query + the bucket table,
 // within 160 KiB): two slices cover 25,800 queries, a day of 5,160 stocks
-#ifndef MFF_PDF_KCAP
-#define MFF_PDF_KCAP 12900
-#endif
-constexpr int PDF_KCAP = MFF_PDF_KCAP;
+constexpr int PDF_KCAP = 12900;
 // learned split key, one per device: sum / count of the per-day medians seen since the
 // last pass start, and the key in use
 struct PdfLearn {
@@ -56,15 +53,9 @@ struct PdfLearn {
   uint64_t key;
 };  // queries per day (all ranks): 2 n_less + n_eq stays in u32
 constexpr int PDF_ZQ = 9160;     // sorted queries per workgroup, u64 counters (LDS: 16 B each)
-#ifndef MFF_PDF_ZQ32
-#define MFF_PDF_ZQ32 12500
-#endif
-#ifndef MFF_PDF_NBK
-#define MFF_PDF_NBK 4096
-#endif
-constexpr int PDF_ZQ32 = MFF_PDF_ZQ32;  // sorted queries per count workgroup, packed u32 counters (12 B)
+constexpr int PDF_ZQ32 = 12500;  // sorted queries per count workgroup, packed u32 counters (12 B)
 constexpr int PDF_PAD = 64;      // ~0 sentinels after the slice's distinct values
-constexpr int PDF_NBK = MFF_PDF_NBK;  // bucket table over the workgroup's distinct query values
+constexpr int PDF_NBK = 4096;  // bucket table over the workgroup's distinct query values
 constexpr int PDF_CT = 1024;     // threads per count / finalize workgroup (<= 1024: wsum[16])
 // packed counter: n_less part in the low PDF_LB bits, n_eq part above.  Exact while a
 // slice's total weight stays below 2^PDF_LB (240 bars x S_loc < 2^21: S_loc <= 8738) and
@@ -75,9 +66,7 @@ constexpr int PDF_CT = 1024;     // threads per count / finalize workgroup (<= 1
 constexpr int PDF_LB = 21;
 // count: level-list entries per thread per chunk (8 or 16; the next chunk is loaded while
 // this one is searched)
-#ifndef MFF_PDF_UNR
-#define MFF_PDF_UNR 8
-#endif
+constexpr int PDF_UNR = 8;
 
 struct QLoader {
   const double* q;  // [R][5][D][S_loc]
@@ -461,7 +450,7 @@ __device__ __forceinline__ bool pdf_count_slice(const PdfArgs& a, int d, int dd,
     // at most 6 steps the probes stay inside the PDF_PAD sentinels (probe <= nv + 2^steps
     // - 2), so the steps are unrolled with constant strides: j is a byte offset and each
     // probe is one ds_read_b64 with an immediate offset.
-    constexpr int UNR = MFF_PDF_UNR;
+    constexpr int UNR = PDF_UNR;
     const uint64_t* L1 = L + 1;
     const char* Lb = reinterpret_cast<const char*>(L);
     const int nvc = sl.nv;
@@ -1009,13 +998,12 @@ static void pdf_slices(int M, int& Z, int& Mz, size_t& lds, bool packed) {
 static int pdf_launch(PdfArgs& a, const uint64_t* q_sorted, int M, hipStream_t st, int mode) {
   size_t lds;
   // packed counters for the count phases while a slice's weight (<= 240 bars per stock of
-  // this rank) fits the n_less field
+  // this rank) fits the n_less field (MFF_PDF_U64: the u64 counters always, a test hook)
   a.packed = mode != 2 && (long long)NBAR * a.S < (1ll << PDF_LB) && getenv("MFF_PDF_U64") == nullptr;
   pdf_slices(M, a.Z, a.Mz, lds, a.packed);
   // one rank, one day per sorted list: slices aligned at PDF_KSPLIT (one more slot per day
-  // for the split; MFF_PDF_KSLICE=0 keeps the plain position slices, A/B timing)
-  const char* ks = getenv("MFF_PDF_KSLICE");
-  a.kslice = mode != 2 && a.packed && !a.frame && !(ks && ks[0] == '0');
+  // for the split)
+  a.kslice = mode != 2 && a.packed && !a.frame;
   if (a.kslice) {
     a.learn = pdf_learn_state(st);
     if (!a.learn) return -2;

@@ -222,9 +222,6 @@ constexpr int SORT_REG = 32;  // segment_sort_binned takes M <= SORT_REG * block
 // differ from its reference (or a range over more than RS_NS bins) returns false with the
 // keys back in sk[0, size) for the bitonic.  The tables use sk's top slots, so a range
 // holds at most RS_CAP keys on this path.
-#ifndef MFF_SORT_RANK
-#define MFF_SORT_RANK 1
-#endif
 constexpr int RS_NS = 1024;    // sub-buckets per range
 constexpr int RS_MAXO = 48;    // non-reference keys per sub-bucket
 constexpr int RS_CAP = SORT_CAPB - (RS_NS * 4 + 3 * RS_NS * 2) / 8;  // 6912: tables in sk[RS_CAP, SORT_CAPB)
@@ -461,7 +458,7 @@ __device__ bool segment_sort_binned(const Loader& ld, int M, uint64_t* out, uint
   if (tid == 0) bins[SORT_NBIN] = tot;
   // ranges: bin b belongs to range start[b] / T (T + maxbin <= SORT_CAPB)
   // the rank placement takes ranges of at most RS_CAP keys (its tables use sk's top)
-  const uint32_t cap = MFF_SORT_RANK && maxbin <= (uint32_t)RS_CAP / 2 ? (uint32_t)RS_CAP : (uint32_t)SORT_CAPB;
+  const uint32_t cap = maxbin <= (uint32_t)RS_CAP / 2 ? (uint32_t)RS_CAP : (uint32_t)SORT_CAPB;
   const uint32_t T = cap - maxbin;
   int* rbeg = reinterpret_cast<int*>(ctl + 32);  // [32] first bin of each range, -1 = empty
   if (tid < 32) rbeg[tid] = -1;
@@ -483,21 +480,16 @@ __device__ bool segment_sort_binned(const Loader& ld, int M, uint64_t* out, uint
     int P = 2048;
     while (P < (int)size) P <<= 1;
     __syncthreads();  // the previous range's readers are done with sk
-    if (!MFF_SORT_RANK) {
-      for (int i = tid; i < P; i += nt) sk[i] = ~0ull;
-      __syncthreads();
-    }
     sort_walk(ld, tid, nt, [&](uint64_t k) {
       if (k == ~0ull) return;
       const int b = (int)((k - kmin) >> sh);
       if (b >= b0 && b < b1) sk[atomicAdd(&bins[b], 1u) - base] = k;
     });
     __syncthreads();
-    if (MFF_SORT_RANK && range_rank_sort(sk, bins, b0, b1, base, size, kmin, sh, out)) continue;
-    if (MFF_SORT_RANK) {  // the bitonic's padding (the rank path's tables may sit there)
-      for (int i = (int)size + tid; i < P; i += nt) sk[i] = ~0ull;
-      __syncthreads();
-    }
+    if (range_rank_sort(sk, bins, b0, b1, base, size, kmin, sh, out)) continue;
+    // the bitonic's padding (the rank path's tables may sit there)
+    for (int i = (int)size + tid; i < P; i += nt) sk[i] = ~0ull;
+    __syncthreads();
     switch (P) {
       case 2048: bitonic_regs<2>(sk); break;
       case 4096: bitonic_regs<4>(sk); break;

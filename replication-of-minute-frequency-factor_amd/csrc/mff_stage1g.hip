@@ -44,18 +44,14 @@ int launch_w64(const float* const fld[5], const uint32_t* valid, int S, int D, c
 int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D, const int8_t* row,
                   uint32_t fam, double* val, uint8_t* state, const uint32_t* ord_th, hipStream_t st);
 
-// 16 stock-days of one day per block iteration; MFF_GITER iterations per block.  One:
+// 16 stock-days of one day per block iteration; kGIter iterations per block.  One:
 // with a loop, everything derived from the lane ids (lane masks, offsets, the scratch
 // address) is hoisted out of it and stays live across it -- the ORD + LVL launch then
 // took 128 VGPRs (4 waves per SIMD) against 91 (5 waves) without; measured 15.5 against
 // 16.6 ms in the pass (profiles/r05/ab_giter.txt)
-#ifndef MFF_GITER
-#define MFF_GITER 1
-#endif
+constexpr int kGIter = 1;
 // waves per SIMD the group kernel is built for (its LDS allows 5 at 31.7 KB per block)
-#ifndef MFF_GWAVES
-#define MFF_GWAVES 5
-#endif
+constexpr int kGWaves = 5;
 // blocks of the exact-list launch (grid-stride over the device-side list count)
 constexpr int kExactGrid = 1024;
 
@@ -189,7 +185,7 @@ constexpr uint32_t G_OL = G_ORD | G_LVL;
 
 template <uint32_t SET>
 // (256, 5): at most 102 VGPRs, five waves per SIMD
-__global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
+__global__ __launch_bounds__(256, kGWaves) void k_stage1g(GArgs a) {
   // 2 KB per group plus 64 B of padding: the four groups of a wave start 16 banks apart,
   // so a store of 16 consecutive words per group covers the 64 banks once
   // per group: the sorted families need 2 x 240 words (level cumulative volumes and
@@ -204,12 +200,12 @@ __global__ __launch_bounds__(256, MFF_GWAVES) void k_stage1g(GArgs a) {
   uint64_t* scr = scratch[wave * 4 + grp];
   double* scr_d = reinterpret_cast<double*>(scr);
   const uint32_t fam = a.fam & SET;
-  const int ntile = (a.S + 16 * MFF_GITER - 1) / (16 * MFF_GITER);
+  const int ntile = (a.S + 16 * kGIter - 1) / (16 * kGIter);
   const int d = blockIdx.x / ntile;
-  const int s0 = (blockIdx.x % ntile) * (16 * MFF_GITER);
+  const int s0 = (blockIdx.x % ntile) * (16 * kGIter);
   const size_t plane = (size_t)a.D * a.S;
 
-  for (int it = 0; it < MFF_GITER; ++it) {
+  for (int it = 0; it < kGIter; ++it) {
     const int s = s0 + it * 16 + wave * 4 + grp;
     const bool act = s < a.S;
     const size_t sd = (size_t)d * a.S + (act ? s : 0);
@@ -1140,7 +1136,7 @@ static int stage1_parts(const float* open, const float* high, const float* low, 
   a.ord_th = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(workspace) + 256 + (size_t)S * D * sizeof(int));
   const char* impl = getenv("MFF_STAGE1_IMPL");
   const bool w64 = impl && strcmp(impl, "w64") == 0;
-  const long long nblk = (long long)((S + 16 * MFF_GITER - 1) / (16 * MFF_GITER)) * D;
+  const long long nblk = (long long)((S + 16 * kGIter - 1) / (16 * kGIter)) * D;
   // one 16-lane group launch; it stores its own group's rows (and the queries) only
   auto group_launch = [&](int gi) -> int {
     const uint32_t set = gi < 2 ? g16::kGroups[gi] : g16::G_OL;

@@ -63,25 +63,9 @@ constexpr uint32_t kSerAB = kSerA | kSerB;  // one pass over open, close, volume
 // The wave pair's split of sets A + B.  Timed alone with both waves on one set (c4):
 // set A 14.3 ms, set B 18.0 ms, the pair 17.3 ms: set B is the longer walk, so the
 // volume moments and sums (MOMV, SUMV: the running volume sum is set A's TRD sum
-// already) move to the set-A wave (MFF_PAIR_SPLIT=1).
-#ifndef MFF_PAIR_SPLIT
-#define MFF_PAIR_SPLIT 1
-#endif
-constexpr uint32_t kPairA = MFF_PAIR_SPLIT ? (kSerA | F_MOMV | F_SUMV) : kSerA;
-constexpr uint32_t kPairB = MFF_PAIR_SPLIT ? (F_SUMC | F_CORR) : kSerB;
-#ifndef MFF_PAIR_AB
-#define MFF_PAIR_AB 1
-#endif
-#ifndef MFF_SERA_FAST
-#define MFF_SERA_FAST 1
-#endif
-// set B's all-present quad path: in the pair form set B shares set A's register budget
-#ifndef MFF_SERB_FAST
-#define MFF_SERB_FAST 1
-#endif
-#ifndef MFF_SERH_FAST
-#define MFF_SERH_FAST 1
-#endif
+// already) move to the set-A wave.
+constexpr uint32_t kPairA = kSerA | F_MOMV | F_SUMV;
+constexpr uint32_t kPairB = F_SUMC | F_CORR;
 
 // ---- presence bits of one stock-day: 8 words, bit m%32 of word m/32 (compile-time
 // word indices only, so the array stays in registers)
@@ -191,8 +175,9 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   const uint32_t* V = reinterpret_cast<const uint32_t*>(a.fld[4]) + sd * NBAR;
 
   // sets with an all-present form of the bar walk
-  constexpr bool kAllpSet = (SET == kSerA && MFF_SERA_FAST) || (PAIR && SET == kPairA && MFF_SERA_FAST) ||
-                            (PAIR && SET == kPairB && MFF_SERB_FAST);
+  // (set B's own kernel has no room for the second copy of the bar walk; in the pair form
+  // set B shares set A's register budget)
+  constexpr bool kAllpSet = SET == kSerA || (PAIR && (SET == kPairA || SET == kPairB));
 
   // ---------------------------------------------------------------- shifts
   double x0r = 0.0, x0v = 0.0;
@@ -694,7 +679,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     // the pair's two waves walk the same stock-days, so they take the same branch (and
     // pass the same barriers either way)
     // (set H: the full-wave walk of olsbar; its own kernel, no barriers, so any wave may)
-    if ((kAllpSet || (!PAIR && SET == kSerH && MFF_SERH_FAST)) &&
+    if ((kAllpSet || (!PAIR && SET == kSerH)) &&
         __builtin_amdgcn_ballot_w64(n > 0 && n != NBAR) == 0ull)
       walk(std::true_type());
     else walk(std::false_type());
@@ -877,7 +862,7 @@ int launch_serial(const float* const fld[5], const uint32_t* valid, int S, int D
     return b;
   };
   const dim3 grid((unsigned)nblk), blk(256);
-  if (MFF_PAIR_AB && (a.fam & kSerAB) == kSerAB) {  // sets A and B in one wave-pair launch
+  if ((a.fam & kSerAB) == kSerAB) {  // sets A and B in one wave-pair launch
     hipLaunchKernelGGL(k_stage1s_pair, dim3((unsigned)(((long long)S * D + 63) / 64)), dim3(128), 0, st,
                        patched(kSerAB));
     if ((a.fam & kSerH) == kSerH) hipLaunchKernelGGL((k_stage1s<kSerH, true>), grid, blk, 0, st, patched(kSerH));

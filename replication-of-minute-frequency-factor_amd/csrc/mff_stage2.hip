@@ -354,9 +354,6 @@ __global__ __launch_bounds__(64) void k_stage2_ring(const double* val, const uin
 // z NaN (C6); NaN / inf propagate to mean and std as in the two-pass form.
 constexpr int S2_U = 4;  // 4 in flight + 4 processed: <= 96 VGPRs at N = 20 (5 waves/SIMD)
 static_assert(S2_U == 4, "the chunk fast path's window offsets assume 4 days per chunk");
-#ifndef MFF_S2_CHUNK
-#define MFF_S2_CHUNK 1
-#endif
 constexpr int S2_THREADS = 256;
 
 // window w[B .. B + N) of an array of at least B + N registers (B a compile-time offset)
@@ -479,7 +476,7 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
     }
     sp = 0u;
     bool allp = false;
-    if constexpr (MFF_S2_CHUNK && N + S2_U <= 64) {
+    if constexpr (N + S2_U <= 64) {
      if (method != MFF_ROLL_O) {
       bool mine = true;
 #pragma unroll
@@ -487,7 +484,7 @@ __global__ __launch_bounds__(S2_THREADS) void k_stage2_reg(const double* val, co
       allp = __builtin_amdgcn_ballot_w64(!mine) == 0ull;  // wave-uniform
      }
     }
-    if constexpr (MFF_S2_CHUNK && N + S2_U <= 64) if (allp) {
+    if constexpr (N + S2_U <= 64) if (allp) {
       // every lane has the chunk's S2_U days: they enter at w[N + u], window u is
       // w[u + 1 .. u + N], its nulls bits u + 1 .. u + N of the extended mask
       uint64_t nm = nullm;

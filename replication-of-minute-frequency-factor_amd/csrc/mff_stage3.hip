@@ -291,21 +291,9 @@ __global__ __launch_bounds__(SORT_THREADS) void k_xs_rank(const double* val, con
 //    bucket's scan covers its non-reference keys only.
 // A segment with a bucket of more than XR_MAXO non-reference keys under both schemes is
 // appended to a list for the sorting kernel (k_xs_rank).
-#ifndef MFF_XB1
-#define MFF_XB1 1024
-#endif
-#ifndef MFF_XB2
-#define MFF_XB2 2048
-#endif
-constexpr int XB1 = MFF_XB1;
-constexpr int XB2 = MFF_XB2;
-#ifndef MFF_XR_PREFETCH
-#define MFF_XR_PREFETCH 0
-#endif
-#ifndef MFF_XR_THREADS
-#define MFF_XR_THREADS 1024
-#endif
-constexpr int XR_THREADS = MFF_XR_THREADS;  // default block; XR_THREADS is also the kernel template parameter
+constexpr int XB1 = 1024;
+constexpr int XB2 = 2048;
+constexpr int XR_THREADS = 1024;  // default block; XR_THREADS is also the kernel template parameter
 constexpr int XR_PER = 8192 / XR_THREADS;   // values per thread at most (M <= 8192)
 constexpr int XR_PER_LO = (5 * 1024) / XR_THREADS;  // the smaller instantiation (S <= 5120 at R = 1)
 constexpr int XR_MAXO = 48;
@@ -317,34 +305,6 @@ __device__ __forceinline__ uint32_t get16(const uint32_t* w, uint32_t i) { retur
 __device__ __forceinline__ uint32_t inc16(uint32_t* w, uint32_t i) {
   return (atomicAdd(&w[i >> 1], 1u << (16 * (i & 1))) >> (16 * (i & 1))) & 0xFFFFu;
 }
-// inc16 with the wave's hot bucket aggregated: the active lanes holding the first active
-// lane's counter index take one atomic (the count) and slots base + their rank among
-// themselves; the others take one atomic each.  Tie-heavy days put most of a wave's
-// values into one bucket, whose LDS word would otherwise take 64 serialized atomics per
-// wave-instruction.  Slots inside a bucket are interchangeable (any key may be slot 0).
-// Measured slower at c4 (all 58 rows 11.0 -> 11.9 ms): off by default.
-#ifndef MFF_XR_AGG
-#define MFF_XR_AGG 0
-#endif
-__device__ __forceinline__ uint32_t inc16_agg(uint32_t* w, uint32_t i) {
-  if (!MFF_XR_AGG) return inc16(w, i);
-  const uint32_t i0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
-  const uint64_t same = __ballot(i == i0);
-  uint32_t r;
-  if (i == i0) {
-    const uint32_t before = __builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
-    uint32_t base = 0u;
-    if (before == 0u) {
-      const uint32_t sh = 16u * (i0 & 1u);
-      base = (atomicAdd(&w[i0 >> 1], (uint32_t)__popcll(same) << sh) >> sh) & 0xFFFFu;
-    }
-    r = (uint32_t)__builtin_amdgcn_readfirstlane((int)base) + before;
-  } else {
-    r = inc16(w, i);
-  }
-  return r;
-}
-
 struct XrBucket {
   int scheme;          // 0 linear, 1 log
   double xmin_h, scale;
@@ -500,13 +460,10 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
   };
   reset_mm();
   __syncthreads();
-  // LOCAL with MFF_XR_PREFETCH: the next segment's values are loaded while this one is
-  // ranked (registers for a second copy: 9 VGPRs spilled); otherwise each segment loads
-  // its own (the default: 125 VGPRs, no spills, 10.6 -> 10.5 ms for all 58 rows at c4)
-  constexpr bool PF = LOCAL && MFF_XR_PREFETCH;
-  if (PF) load(blockIdx.x);
+  // each segment loads its own values (loading the next segment's while this one is
+  // ranked needs registers for a second copy: 9 VGPRs spilled, measured slower)
   for (size_t seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
-    if (!PF) load(seg);
+    load(seg);
     double x[PER];
     uint32_t inc = 0u, stv = 0u, stn = 0u;  // included; state VALUE; state NULL
 #pragma unroll
@@ -518,7 +475,6 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
       stv |= (sb == MFF_STATE_VALUE ? 1u : 0u) << j;
       stn |= (sb == MFF_STATE_NULL ? 1u : 0u) << j;
     }
-    if (PF) load(seg + gridDim.x);  // in flight while this segment is ranked
     for (int w = tid; w < XB1 / 2; w += XR_THREADS) h1[w] = 0u;
     for (int w = tid; w < XB2 / 2; w += XR_THREADS) { bins[w] = 0u; eqc[w] = 0u; ctr[w] = 0u; }
     if (tid == 0) ctl[0] = 0u;
@@ -563,7 +519,7 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
       for (int j = 0; j < PER; ++j) {
         if ((inc >> j) & 1u) {
           double f;
-          inc16_agg(h1, bk.l1(x[j], f));
+          inc16(h1, bk.l1(x[j], f));
         }
       }
       __syncthreads();
@@ -598,7 +554,7 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
       for (int j = 0; j < PER; ++j) {
         if ((inc >> j) & 1u) {
           const uint32_t b = bk(x[j]);
-          bp[j] = (b << 16) | inc16_agg(bins, b);
+          bp[j] = (b << 16) | inc16(bins, b);
         } else {
           bp[j] = 0u;
         }
@@ -634,7 +590,7 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
           const uint32_t b = bp[j] >> 16;
           if (sk[get16(bins, b)] == ord64(x[j])) {
             isref |= 1u << j;
-            inc16_agg(eqc, b);
+            inc16(eqc, b);
           }
         }
       }
@@ -674,7 +630,7 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
     for (int j = 0; j < PER; ++j) {
       if (((inc & ~isref) >> j) & 1u) {
         const uint32_t b = bp[j] >> 16;
-        sk[get16(bins, b) + get16(eqc, b) + inc16_agg(ctr, b)] = ord64(x[j]);
+        sk[get16(bins, b) + get16(eqc, b) + inc16(ctr, b)] = ord64(x[j]);
       }
     }
     reset_mm();
@@ -737,10 +693,7 @@ __global__ __launch_bounds__(XR_THREADS, XR_THREADS == 256 ? 2 : 2048 / XR_THREA
 // Same ranks (exact, S6 average) and the same hand-over to k_xs_rank as
 // k_xs_rank_bucket (XD_MAXO non-reference keys in a bucket under both schemes).
 constexpr int XD_MAXO = 48;
-#ifndef MFF_XD_B2
-#define MFF_XD_B2 4096
-#endif
-constexpr int XD_B2 = MFF_XD_B2;  // level-2 buckets of the 1,024-thread instantiations
+constexpr int XD_B2 = 4096;  // level-2 buckets of the 1,024-thread instantiations
 
 // exclusive scan of W consecutive counters per thread (c -> offsets); returns the total.
 // A DPP wave scan, then the wave totals through LDS (one read per lane, a 16-lane DPP scan,

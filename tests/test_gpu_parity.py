@@ -133,9 +133,13 @@ def test_doc_pdf_merge_path(dev):
     assert not bad, "\n".join(bad)
 
 
-def test_doc_pdf_four_slices(dev):
+@pytest.mark.parametrize("u64", [False, True])
+def test_doc_pdf_four_slices(dev, u64, monkeypatch):
     """M = 5*S = 25,000 queries per day (the bench's stock count): two packed-counter LDS
-    query slices in mff_pdf_count (three with MFF_PDF_U64; ranks exact, tolerance 0)."""
+    query slices in mff_pdf_count (three with u64 counters, MFF_PDF_U64 -- the path of
+    S_loc > 8,738 stocks; ranks exact, tolerance 0)."""
+    if u64:
+        monkeypatch.setenv("MFF_PDF_U64", "1")
     import mff_oracle as O
     from mff import synth
     panel = synth.make_panel(5000, 1, config=13)
