@@ -698,23 +698,19 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
   MFF_REQUIRE(N >= 1, "mff_stage2: N=%d < 1", N);
   MFF_REQUIRE(method >= MFF_ROLL_O && method <= MFF_ROLL_STD, "mff_stage2: unknown method %d", method);
   MFF_REQUIRE(val && state && out_val && out_state, "mff_stage2: NULL buffer");
-  // day segments (MFF_S2_SEGS, default 4): more waves in flight for the memory system (a
+  // four day segments: more waves in flight for the memory system (a
   // (row, stock) lane per wave-slot otherwise walks all D days: ~4.4 waves per SIMD at c4);
   // each segment of >= 16 N days (a multiple of S2_U) rebuilds its window from the N
   // present days before it.  z at N = 20, 58 rows at c4: 3.56 -> 3.28 ms (4 or 8 segments,
   // profiles/r04f/s2_segments.log)
-  const char* sg = getenv("MFF_S2_SEGS");
-  int nseg = sg ? atoi(sg) : 4;
-  int seg = D;
-  if (nseg > 1) {
-    seg = (D + nseg - 1) / nseg;
-    if (seg < 16 * N) seg = 16 * N;
-    seg = (seg + S2_U - 1) / S2_U * S2_U;
-  }
+  constexpr int kS2Segs = 4;
+  int seg = (D + kS2Segs - 1) / kS2Segs;
+  if (seg < 16 * N) seg = 16 * N;
+  seg = (seg + S2_U - 1) / S2_U * S2_U;
   // MFF_S2_SEG_DAYS: an explicit segment length (tests: segments shorter than the window)
   const char* sdays = getenv("MFF_S2_SEG_DAYS");
   if (sdays && atoi(sdays) > 0) seg = (atoi(sdays) + S2_U - 1) / S2_U * S2_U;
-  nseg = (D + seg - 1) / seg;
+  const int nseg = (D + seg - 1) / seg;
   const long long nreg = (long long)nseg * rows * ((S + S2_THREADS - 1) / S2_THREADS);
   MFF_REQUIRE(nreg < (1ll << 31), "mff_stage2: grid too large");
 #define MFF_S2_REG(NN)                                                                                      \
@@ -723,7 +719,8 @@ extern "C" int mff_stage2(const double* val, const uint8_t* state, int rows, int
                        state, D, S, method, out_val, out_state, rows, seg);                                 \
     MFF_LAUNCH_CHECK();                                                                                     \
     return 0;
-  // MFF_STAGE2_IMPL=ring / slide: a sliding kernel for every N (A/B timing)
+  // MFF_STAGE2_IMPL=ring / slide: a sliding kernel for every N (a test hook: the sliding
+  // kernels are the path of N > 64)
   const char* impl = getenv("MFF_STAGE2_IMPL");
   const bool force_slide = impl && (impl[0] == 's' || impl[0] == 'r');
 #define MFF_S2_REG4(a) MFF_S2_REG(a) MFF_S2_REG(a + 1) MFF_S2_REG(a + 2) MFF_S2_REG(a + 3)
