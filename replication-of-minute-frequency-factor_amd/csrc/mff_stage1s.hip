@@ -251,8 +251,9 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
   double x5 = 0, y5 = 0, x6 = 0;
   int nzc = 0;
   // carries: previous present bar, previous present non-zero-volume bar
-  float cp = 1.f, czp = 1.f;
-  uint32_t vp = 0u, vzp = 1u;
+  float cp = 1.f;
+  uint32_t vp = 0u;
+  double czp = 1.0, vzp = 1.0;  // (as doubles: no conversion per row)
   double rcp_ = 1.0, rcz = 1.0, rvz = 1.0;  // their reciprocals (frcp)
   bool hp = false, hz = false;
 
@@ -418,7 +419,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     const bool hpv = ALLP ? m > 0 : hp;
     if (fam & (F_SUMC | F_CORR)) {
       rc = frcp(c);
-      rv = frcp(vf != 0u ? v : 1.0);
+      rv = frcp(v);  // read for rows with volume only (1/0 never is)
     }
     if (fam & F_SUMC) {
       if (hpv && vf != 0u) amh += fabs(c - (double)cp) * (rcp_ * rv);  // |dc| / (c_prev * v)
@@ -444,8 +445,8 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       dvp = dv;
       if (vf != 0u) {  // rows with volume != 0 (CM:855-866, 924-930)
         if (hz) {
-          const double pcz = fdivr(c - (double)czp, (double)czp, rcz);
-          const double pvz = fdivr(v - (double)vzp, (double)vzp, rvz);
+          const double pcz = fdivr(c - czp, czp, rcz);
+          const double pvz = fdivr(v - vzp, vzp, rvz);
           // first pair: the shifts, behind a wave-uniform branch taken only while some
           // lane meets its second non-zero-volume row (set B bounds the wave pair: its
           // walk 16.9 ms vs set A's 15.6 with both waves on one set; the branch instead of
@@ -461,7 +462,7 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
           F1 += e5; F2 = fma(e5, e5, F2); FX = fma(e5, dy, FX);  // prvr
           G1 += e6; G2 = fma(e6, e6, G2); GX = fma(e6, dy, GX);  // pvr
         }
-        czp = cf; vzp = vf; rcz = rc; rvz = rv; hz = true; ++nzc;
+        czp = c; vzp = v; rcz = rc; rvz = rv; hz = true; ++nzc;
       }
     }
     cp = cf; vp = vf; rcp_ = rc; hp = true; ++kr;
