@@ -400,14 +400,22 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
       }
     }
     if (!(fam & (F_MOMV | F_SUMV | F_SUMC | F_CORR))) return;
-    if (fam & F_SUMV) {  // snapshots of the sum through bars 30, 209, 236 (before bar m's add)
-      if (m == 31) S30 = sumv;
-      if (m == 210) S209 = sumv;
-      if (m == 237) S236 = sumv;
+    if (fam & F_SUMV) {  // snapshots of the sum through bars 30, 209, 236
+      if (fam & F_TRD) {  // TRD's running sum tv holds it (bar m included)
+        if (m == 30) S30 = tv;
+        if (m == 209) S209 = tv;
+        if (m == 236) S236 = tv;
+      } else {  // (before bar m's add)
+        if (m == 31) S30 = sumv;
+        if (m == 210) S209 = sumv;
+        if (m == 237) S236 = sumv;
+      }
     }
     if (!pk) return;
     const double c = (double)cf, v = (double)vf;
-    if (fam & (F_MOMV | F_SUMV)) sumv += v;
+    // the day's volume sum: TRD's running sum tv when the set computes TRD (the pair's set A:
+    // the same exact integer sum over the present bars), else its own
+    if ((fam & (F_MOMV | F_SUMV)) && !(fam & F_TRD)) sumv += v;
     if (fam & F_MOMV) {
       const double dd = v - x0v, d2 = dd * dd;
       t1 += dd; t2 += d2; t3 = fma(d2, dd, t3); t4 = fma(d2, d2, t4);
@@ -758,21 +766,22 @@ __device__ __forceinline__ void s1s_body(const SArgs& a, float4* pbuf) {
     // skew/kurt of v / sum(v) == of v (scale-free); sum(v) = 0 -> shares NaN
     double sk, ku;
     skew_kurt(m, sk, ku);
-    if (sumv == 0.0) sk = ku = qnan();
+    if (((fam & F_TRD) ? tv : sumv) == 0.0) sk = ku = qnan();
     val(24, sk);
     val(25, ku);
     val(26, sk / ku);
   }
   if (fam & F_SUMV) {
-    const double spre = S236, scls = sumv - S236, shead = S30, stail = sumv - S209;
+    const double sv = (fam & F_TRD) ? tv : sumv;
+    const double spre = S236, scls = sv - S236, shead = S30, stail = sv - S209;
     if (M.any_in(0, 236)) val(28, spre); else absent(28);
     if (M.any_in(237, 239)) val(29, scls); else absent(29);
     const double vfirst = x0v;
-    val(30, vfirst / sumv);
-    val(31, scls / sumv);
+    val(30, vfirst / sv);
+    val(31, scls / sv);
     val(32, vfirst);
-    val(52, sumv > 0.0 ? shead / sumv : 0.125);
-    val(53, sumv > 0.0 ? stail / sumv : 0.125);
+    val(52, sv > 0.0 ? shead / sv : 0.125);
+    val(53, sv > 0.0 ? stail / sv : 0.125);
   }
   if (fam & F_SUMC) val(27, amh);  // liq_amihud_1min
   if (fam & F_OLS) {
